@@ -1,0 +1,196 @@
+/*
+ * dpemu.h -- C ABI of the MI355X-native batched QubiC distributed-processor
+ * emulator (libdpemu.so).
+ *
+ * The emulator executes the 128-bit machine code that distproc's assembler
+ * writes into cmd_mem (python/distproc/assembler.py:341-429,623-641) across
+ * many (shot, core) lanes, cycle-exact against the gateware:
+ *   proc core           hdl/proc.sv:9-171, ctrl.v:55-595, alu.v, instr_ptr.v,
+ *                       qclk.v, reg_file.v, cmd_mem.v (READ_LATENCY=3)
+ *   pulse emission      hdl/pulse_reg.sv:16-107, pulse_iface.sv
+ *   measurement fproc   hdl/fproc_meas.sv, fproc_lut.sv, core_state_mgr.sv,
+ *                       meas_lut.sv
+ *   sync barrier        hdl/sync_iface.sv + ctrl.v:347-363,510-552 (the
+ *                       controller itself is build-defined)
+ * and synthesises DDS I/Q samples from the pulse events (build-defined DDS).
+ *
+ * Each entry point replaces one piece of the reference simulation path
+ * (SURVEY.md §8b): the cocotb/Verilator harness of toplevel_sim
+ * (sim_modules/toplevel_sim.sv:13-33; cocotb/proc/test_proc.py:29-38 loads
+ * cmd_mem, drives reset/fproc/sync, samples pulse_iface every clock).
+ *
+ * Conventions: return 0 on success, a negative DPEMU_E* code on failure (no
+ * exceptions cross the ABI; dpemu_last_error() has the message).  Caller
+ * owns every pointer it passes.  Device-pointer outputs must be device
+ * memory of the context's device; NULL skips that output.  A context is not
+ * re-entrant; use one per device (one process per GPU).
+ */
+#ifndef DPEMU_H
+#define DPEMU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPEMU_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------- */
+#define DPEMU_OK            0
+#define DPEMU_E_INVALID   (-22)   /* bad argument / inconsistent config  */
+#define DPEMU_E_NOMEM     (-12)   /* device allocation failed            */
+#define DPEMU_E_DEVICE     (-5)   /* HIP runtime error                   */
+#define DPEMU_E_NOPROG     (-2)   /* run before load_programs            */
+
+/* ---- lane terminal status (summary.w1 bits 23:16) -------------------- */
+#define DPEMU_ST_DONE        1    /* decoded DONE (1010) or opcode 0000 (ctrl.v:365-397) */
+#define DPEMU_ST_MAX_CYCLES  2    /* next decode, or a wait's end, beyond max_cycles     */
+#define DPEMU_ST_HUNG_OPCODE 3    /* opcode[7:4] in 1101..1111: DECODE forever (ctrl.v:399-414) */
+#define DPEMU_ST_DEADLOCK    4    /* sync / fproc wait that can never complete           */
+
+/* ---- lane flags (summary.w1 bits 31:24) ------------------------------ */
+#define DPEMU_F_LATE          0x01 /* trig/idle decoded after cmd_time: waits for qclk wrap */
+#define DPEMU_F_EVENT_OVF     0x02 /* more events than event_cap (count still exact)        */
+#define DPEMU_F_TRACE_OVF     0x04 /* more register-trace records than trace_cap            */
+#define DPEMU_F_MEAS_OVF      0x08 /* more measurements than meas_cap                       */
+#define DPEMU_F_DOUBLE_STROBE 0x10 /* trig at the first decode with cmd_time 0: the reset
+                                      hold keeps qclk at 0 two cycles -> two cstrobes      */
+
+/* ---- fproc back ends --------------------------------------------------*/
+#define DPEMU_FPROC_MEAS 0        /* hdl/fproc_meas.sv: latest stored bit, ready at D+2   */
+#define DPEMU_FPROC_LUT  1        /* hdl/fproc_lut.sv: id==0 wait own meas, else LUT      */
+
+/* ---- event kinds (event.w2 bits 31:28) ------------------------------- */
+#define DPEMU_EV_STROBE      0    /* pulse_iface.cstrobe high: pulse register snapshot    */
+#define DPEMU_EV_PULSE_RESET 1    /* pulse_iface.reset high (PULSE_RESET decode cycle)    */
+
+/* ---- register-trace pseudo addresses ---------------------------------- */
+#define DPEMU_TRACE_QCLK_LOAD 16  /* INC_QCLK loaded qclk (value = qclk at t)             */
+#define DPEMU_TRACE_QCLK_RST  17  /* SYNC reset qclk (value 0 at t)                       */
+
+#define DPEMU_MAX_CORES 64
+
+/*
+ * Timebase: cycle t = 0 is the first DECODE after reset.  qclk(0) = qclk(1) = 0
+ * (reset hold, proc.sv:125-136), qclk(t) = t - 1 afterwards until INC_QCLK or
+ * SYNC reload it.  All times are emulated fabric clocks (2 ns at 500 MHz).
+ */
+typedef struct dpemu_config {
+    uint32_t cores_per_shot;   /* C: power of two, 1..64; lane = shot*C + core        */
+    uint32_t n_groups;         /* program groups; group(s) = (s/shots_per_group)%n_groups */
+    uint32_t shots_per_group;  /* >= 1                                                  */
+    uint32_t max_cycles;       /* <= 2^31 - 64                                          */
+    uint32_t event_cap;        /* event slots per lane                                   */
+    uint32_t trace_cap;        /* register-trace slots per lane (0 = no trace)           */
+    uint32_t meas_cap;         /* measurement slots per lane (<= 32)                     */
+    uint32_t fproc_mode;       /* DPEMU_FPROC_*                                          */
+    uint32_t meas_elem;        /* strobe with (cfg & 3) == meas_elem is a readout; 0xFF none */
+    uint32_t meas_latency;     /* readout strobe -> meas_valid, clocks (>= 1)           */
+    uint32_t sync_latency;     /* last sync enable -> sync.ready, clocks (>= 1)         */
+    uint32_t reserved0;
+    uint64_t sync_mask;        /* participant cores (bit c); 0 = all C cores             */
+    uint64_t seed;             /* Philox4x32-10 key                                      */
+    uint32_t lut_mask;         /* meas_lut mask (nonzero), meas_lut.sv:16                */
+    uint32_t reserved1;
+    uint32_t p1_threshold[DPEMU_MAX_CORES]; /* P(meas=1) = thr/2^32; 0xFFFFFFFF = always 1 */
+    uint64_t lut_table[256];   /* meas_lut table: lut_out = table[addr], bit c -> core c */
+} dpemu_config;
+
+/*
+ * Per-lane summary, 8 x u32:
+ *   w0 t_end      decode cycle of DONE (done_gate from t_end+1) or of the stop
+ *   w1 ip[15:0] | status[23:16] | flags[31:24]
+ *   w2 n_events   strobe + pulse_reset events (may exceed event_cap)
+ *   w3 n_instr    instructions decoded (DONE included)
+ *   w4 qclk_end   qclk at t_end
+ *   w5 n_meas     measurements taken
+ *   w6 meas_bits  outcome of measurement m in bit m (m < 32)
+ *   w7 n_trace    register-trace records (may exceed trace_cap)
+ *
+ * Event (slot-major: slot k of lane L at index k*n_lanes + L):
+ *   ev_main uint4 {t, qclk, env[23:0] | cfg<<24 | kind<<28, phase[16:0] | freq<<17}
+ *   ev_amp  uint16 amp
+ * Trace (slot-major): uint4 {t (first cycle the value is visible), addr, value, 0}
+ * Meas  (slot-major): uint2 {valid cycle, bit}
+ * Histogram: uint64 [n_groups][2^C] (C <= 12), key bit c = last outcome of core c.
+ */
+typedef struct dpemu_outputs {
+    uint32_t *summary;    /* [n_lanes][8]                      */
+    uint32_t *ev_main;    /* [event_cap][n_lanes][4]           */
+    uint16_t *ev_amp;     /* [event_cap][n_lanes]              */
+    uint32_t *trace;      /* [trace_cap][n_lanes][4]           */
+    uint32_t *meas;       /* [meas_cap][n_lanes][2]            */
+    uint32_t *regs;       /* [16][n_lanes] final register file */
+    uint64_t *hist;       /* [n_groups][2^C], accumulated      */
+} dpemu_outputs;
+
+typedef struct dpemu_ctx dpemu_ctx;
+
+/* Library / device --------------------------------------------------- */
+int         dpemu_abi_version(void);
+int         dpemu_create(int device, dpemu_ctx **out);
+int         dpemu_destroy(dpemu_ctx *ctx);
+const char *dpemu_last_error(dpemu_ctx *ctx);
+
+/*
+ * Programs: n_programs cmd_mem images.  `words` holds every program's
+ * little-endian u128 commands as u32 quads (word i of the u128 = bits
+ * [32i+31:32i], cmd_mem_iface.sv:19-21), program p starting at quad
+ * offsets[p] with n_instr[p] commands (assembler cmd_buf bytes reinterpret
+ * directly).  Fetch beyond n_instr reads 0 (= DONE), as the zero-initialised
+ * 2^16-deep cmd_mem of toplevel_sim does.
+ * prog_table[g*C + c] = program run by core c of shots in group g.
+ */
+int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *offsets,
+                        const uint32_t *n_instr, uint32_t n_programs,
+                        const uint32_t *prog_table, uint32_t n_groups, uint32_t cores_per_shot);
+
+/* Emulate shots [shot_begin, shot_begin + n_shots) on `stream` (hipStream_t or
+ * NULL).  n_lanes = n_shots * C.  Outputs are device pointers. */
+int dpemu_run(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin, uint64_t n_shots,
+              const dpemu_outputs *out, void *stream);
+
+/* Same, with host output pointers (the library stages device buffers). */
+int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
+                   uint64_t n_shots, const dpemu_outputs *host_out);
+
+/*
+ * DDS synthesis (build-defined fixed point).  One channel =
+ * one (lane, element) pair.  Channel ch reads the events of lane
+ * ch_lane[ch] (slot-major as written by dpemu_run, n_lanes stride, count
+ * from the summary) keeping strobes whose cfg & 3 == ch_elem[ch], plus
+ * pulse_reset events.  env_tables / freq_tables: concatenated u32 buffers
+ * (assembler env_buffers / freq_buffers format), channel ch using
+ * env_off[ch] / freq_off[ch] (u32 offsets).  Output iq[ch][n_samples] as
+ * int16 {I, Q} pairs (4 B/sample) for samples [0, n_samples) of the
+ * channel, sample j at cycle j / spc[ch].  sin_lut: 4096 int16 Q15 (see
+ * dpemu_dds_sin_lut).
+ */
+typedef struct dpemu_dds_channels {
+    uint32_t n_channels;
+    uint32_t n_lanes;          /* stride of the event arrays */
+    uint32_t n_samples;        /* samples per channel        */
+    uint32_t reserved;
+    const uint32_t *ch_lane;   /* [n_channels] */
+    const uint32_t *ch_elem;   /* [n_channels] */
+    const uint32_t *spc;       /* [n_channels] samples per clock (1..16) */
+    const uint32_t *interp;    /* [n_channels] output samples per envelope sample (>=1) */
+    const uint32_t *env_off;   /* [n_channels] */
+    const uint32_t *env_len;   /* [n_channels] u32 words available */
+    const uint32_t *freq_off;  /* [n_channels] */
+    const uint32_t *freq_len;  /* [n_channels] u32 words available */
+} dpemu_dds_channels;
+
+int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uint32_t *summary,
+              const uint32_t *ev_main, const uint16_t *ev_amp, const uint32_t *env_tables,
+              const uint32_t *freq_tables, int16_t *iq_out, void *stream);
+
+/* The Q15 sine table both the DDS kernel and its CPU restatement use. */
+int dpemu_dds_sin_lut(int16_t *out4096);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPEMU_H */

@@ -1,0 +1,278 @@
+"""TEST INFRASTRUCTURE -- ctypes binding of the CPU oracle (liboracle.so).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline
+leg import this package, and only as the checker / CPU baseline; the product
+path (``distributed_processor_amd``) never does.
+
+* ``RtlTB``      per-clock proc + toplevel_sim cmd_mem, cocotb semantics
+                 (inputs set before ``edge()`` apply to that clock; values read
+                 after it are those of the clock just simulated)
+* ``FprocTB``    fproc_meas / fproc_lut in isolation (fproc_*_sim.sv)
+* ``rtl_run_shot``  per-clock multi-core shot with the build-defined
+                 measurement model and sync controller
+* ``fast_run``   event-driven model, dpemu_run-compatible outputs
+"""
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'liboracle.so')
+
+FPROC_MEAS = 0
+FPROC_LUT = 1
+FPROC_EXTERNAL = 99
+T0 = 6   # clocks from the start of reset to the first DECODE in rtl_run_shot
+
+
+def build(force=False):
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(['make', '-s', '-C', HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = C.CDLL(LIB_PATH)
+        _setup(_lib)
+    return _lib
+
+
+class Comb(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in (
+        'state', 'opcode', 'qclk', 'cstrobe', 'env', 'phase', 'freq', 'amp', 'cfg',
+        'pulse_reset', 'done_gate', 'sync_enable', 'fproc_enable', 'fproc_id',
+        'instr_ptr', 'load_en', 'load_addr')] + [
+        ('cmd_buf_out', C.c_uint32 * 4)] + [(n, C.c_uint32) for n in (
+            'reg_we', 'reg_wa', 'reg_wd', 'qclk_load', 'qclk_rst_ctrl')]
+
+
+class ShotCfg(C.Structure):
+    _fields_ = [('cores', C.c_uint32), ('fproc_mode', C.c_uint32), ('sync_external', C.c_uint32),
+                ('meas_elem', C.c_uint32), ('meas_latency', C.c_uint32), ('sync_latency', C.c_uint32),
+                ('sync_mask', C.c_uint64), ('seed', C.c_uint64), ('lut_mask', C.c_uint32),
+                ('p1_threshold', C.c_uint32 * 64), ('lut_table', C.c_uint64 * 256)]
+
+
+class LaneOut(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in (
+        'status', 'flags', 't_end', 'ip', 'qclk_end', 'n_instr', 'n_events', 'n_trace',
+        'n_meas', 'meas_bits')] + [('regs', C.c_uint32 * 16),
+                                   ('ev', C.POINTER(C.c_uint32)), ('amp', C.POINTER(C.c_uint16)),
+                                   ('tr', C.POINTER(C.c_uint32)), ('meas', C.POINTER(C.c_uint32))]
+
+
+def _setup(L):
+    vp = C.c_void_p
+    L.rtl_tb_new.restype = vp
+    L.rtl_tb_free.argtypes = [vp]
+    L.rtl_tb_set.argtypes = [vp, C.c_int, C.c_int, C.c_uint32, C.c_int]
+    L.rtl_tb_write.argtypes = [vp, C.c_int, C.c_uint32, C.POINTER(C.c_uint32)]
+    L.rtl_tb_edge.argtypes = [vp]
+    L.rtl_tb_snap.argtypes = [vp]
+    L.rtl_tb_snap.restype = C.POINTER(Comb)
+    L.rtl_tb_reg.argtypes = [vp, C.c_int]
+    L.rtl_tb_reg.restype = C.c_uint32
+    L.rtl_fproc_tb_new.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]
+    L.rtl_fproc_tb_new.restype = vp
+    L.rtl_fproc_tb_free.argtypes = [vp]
+    L.rtl_fproc_tb_set.argtypes = [vp, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
+    L.rtl_fproc_tb_edge.argtypes = [vp]
+    L.rtl_fproc_tb_ready.argtypes = [vp]
+    L.rtl_fproc_tb_ready.restype = C.c_uint32
+    L.rtl_fproc_tb_data.argtypes = [vp, C.c_int]
+    L.rtl_fproc_tb_data.restype = C.c_uint32
+    L.rtl_run_shot.argtypes = [C.POINTER(ShotCfg), C.POINTER(C.POINTER(C.c_uint32)),
+                               C.POINTER(C.c_uint32), C.c_uint64, C.c_uint32, C.c_uint32,
+                               C.c_uint32, C.c_uint32, C.POINTER(LaneOut)]
+    L.rtl_run_shot.restype = C.c_int
+    L.oracle_pulse_reg.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint32, C.c_int]
+    L.oracle_alu.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+    L.oracle_alu.restype = C.c_uint32
+    L.oracle_philox_u32.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]
+    L.oracle_philox_u32.restype = C.c_uint32
+    if hasattr(L, 'fast_run'):
+        L.fast_run.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
+        L.fast_run.restype = C.c_int
+    if hasattr(L, 'oracle_dds'):
+        L.oracle_dds_sin_lut.argtypes = [C.c_void_p]
+
+
+def _u128_to_u32x4(word):
+    arr = (C.c_uint32 * 4)()
+    for i in range(4):
+        arr[i] = (int(word) >> (32 * i)) & 0xFFFFFFFF
+    return arr
+
+
+class RtlTB:
+    """toplevel_sim driven like a cocotb test (sim_modules/toplevel_sim.sv:13-33)."""
+
+    def __init__(self):
+        self._L = lib()
+        self._h = self._L.rtl_tb_new()
+        self.reset = 0
+        self.fproc_ready = 0
+        self.fproc_data = 0
+        self.sync_ready = 0
+
+    def __del__(self):
+        if getattr(self, '_h', None):
+            self._L.rtl_tb_free(self._h)
+            self._h = None
+
+    def _push(self):
+        self._L.rtl_tb_set(self._h, int(self.reset), int(self.fproc_ready),
+                           int(self.fproc_data) & 0xFFFFFFFF, int(self.sync_ready))
+
+    def edge(self, n=1):
+        """``await RisingEdge(dut.clk)`` n times."""
+        for _ in range(n):
+            self._push()
+            self._L.rtl_tb_edge(self._h)
+
+    def load_commands(self, cmd_list, start_addr=0):
+        """cocotb/proc/test_proc.py:29-38: one cmd_mem write per clock."""
+        addr = start_addr
+        for cmd in cmd_list:
+            self._L.rtl_tb_write(self._h, 1, addr, _u128_to_u32x4(cmd))
+            self.edge()
+            addr += 1
+        self._L.rtl_tb_write(self._h, 0, 0, None)
+
+    @property
+    def snap(self):
+        return self._L.rtl_tb_snap(self._h).contents
+
+    def reg(self, i):
+        return self._L.rtl_tb_reg(self._h, i)
+
+    def cmd_buf_out(self):
+        w = self.snap.cmd_buf_out
+        return sum(int(w[i]) << (32 * i) for i in range(4))
+
+    def __getattr__(self, name):
+        if name in ('cstrobe', 'freq', 'phase', 'env', 'amp', 'cfg', 'qclk', 'done_gate',
+                    'pulse_reset', 'sync_enable', 'fproc_enable', 'fproc_id', 'state', 'instr_ptr'):
+            return int(getattr(self.snap, name))
+        raise AttributeError(name)
+
+
+class FprocTB:
+    """fproc_meas_sim / fproc_lut_sim (N_CORES=5 in the reference testbenches)."""
+
+    def __init__(self, mode, n=5, lut_mask=0b00011, lut_table=(0b00000, 0b00100, 0b10000, 0b01000)):
+        self._L = lib()
+        tbl = (C.c_uint64 * 256)()
+        for i, v in enumerate(lut_table):
+            tbl[i] = v
+        self.n = n
+        self._h = self._L.rtl_fproc_tb_new(mode, n, lut_mask, tbl)
+        self.reset = 0
+        self.meas = 0
+        self.meas_valid = 0
+        self.fproc_enable = 0
+        self.fproc_id = [0] * n
+
+    def __del__(self):
+        if getattr(self, '_h', None):
+            self._L.rtl_fproc_tb_free(self._h)
+            self._h = None
+
+    def edge(self, n=1):
+        for _ in range(n):
+            ids = (C.c_uint32 * self.n)(*[int(x) for x in self.fproc_id])
+            self._L.rtl_fproc_tb_set(self._h, int(self.reset), int(self.meas), int(self.meas_valid),
+                                     int(self.fproc_enable), ids)
+            self._L.rtl_fproc_tb_edge(self._h)
+
+    @property
+    def fproc_ready(self):
+        return self._L.rtl_fproc_tb_ready(self._h)
+
+    def fproc_data(self, c):
+        return self._L.rtl_fproc_tb_data(self._h, c)
+
+
+class PulseRegTB:
+    """pulse_reg in isolation (sim_modules/pulsereg_sim.sv)."""
+
+    def __init__(self):
+        self._L = lib()
+        self.state = (C.c_uint32 * 5)()
+        self.pulse_cmd_in = 0
+        self.reg_in = 0
+        self.pulse_write_en = 0
+
+    def edge(self):
+        # pulse_cmd_in is cmd[115:37]; rebuild the full word for the C hook
+        lc = _u128_to_u32x4((int(self.pulse_cmd_in) & ((1 << 79) - 1)) << 37)
+        self._L.oracle_pulse_reg(self.state, lc, int(self.reg_in) & 0xFFFFFFFF, int(self.pulse_write_en))
+
+    env_word = property(lambda self: self.state[0])
+    phase = property(lambda self: self.state[1])
+    freq = property(lambda self: self.state[2])
+    amp = property(lambda self: self.state[3])
+    cfg = property(lambda self: self.state[4])
+
+
+def make_shot_cfg(cores, fproc_mode=FPROC_MEAS, meas_elem=2, meas_latency=1, sync_latency=1,
+                  sync_mask=0, seed=0x5EED, p1=None, lut_mask=0b11, lut_table=None,
+                  sync_external=0):
+    cfg = ShotCfg()
+    cfg.cores = cores
+    cfg.fproc_mode = fproc_mode
+    cfg.sync_external = sync_external
+    cfg.meas_elem = meas_elem
+    cfg.meas_latency = meas_latency
+    cfg.sync_latency = sync_latency
+    cfg.sync_mask = sync_mask
+    cfg.seed = seed
+    cfg.lut_mask = lut_mask
+    p1 = p1 if p1 is not None else [1 << 31] * cores
+    for i, v in enumerate(p1):
+        cfg.p1_threshold[i] = v
+    for i, v in enumerate(lut_table or []):
+        cfg.lut_table[i] = v
+    return cfg
+
+
+def rtl_run_shot(cfg, programs, shot, horizon, ev_cap=256, tr_cap=256, meas_cap=32):
+    """programs: list (per core) of (n,4) uint32 arrays.  Returns (all_done, [lane dicts])."""
+    L = lib()
+    ncore = cfg.cores
+    progs = [np.ascontiguousarray(p, dtype=np.uint32).reshape(-1, 4) for p in programs]
+    pp = (C.POINTER(C.c_uint32) * ncore)(*[p.ctypes.data_as(C.POINTER(C.c_uint32)) for p in progs])
+    ni = (C.c_uint32 * ncore)(*[len(p) for p in progs])
+    outs = (LaneOut * ncore)()
+    bufs = []
+    for c in range(ncore):
+        ev = np.zeros((ev_cap, 4), np.uint32)
+        amp = np.zeros(ev_cap, np.uint16)
+        tr = np.zeros((max(tr_cap, 1), 4), np.uint32)
+        ms = np.zeros((max(meas_cap, 1), 2), np.uint32)
+        bufs.append((ev, amp, tr, ms))
+        outs[c].ev = ev.ctypes.data_as(C.POINTER(C.c_uint32))
+        outs[c].amp = amp.ctypes.data_as(C.POINTER(C.c_uint16))
+        outs[c].tr = tr.ctypes.data_as(C.POINTER(C.c_uint32))
+        outs[c].meas = ms.ctypes.data_as(C.POINTER(C.c_uint32))
+    ok = L.rtl_run_shot(C.byref(cfg), pp, ni, shot, horizon, ev_cap, tr_cap, meas_cap, outs)
+    res = []
+    for c in range(ncore):
+        o = outs[c]
+        ev, amp, tr, ms = bufs[c]
+        ne, nt, nm = min(o.n_events, ev_cap), min(o.n_trace, tr_cap), min(o.n_meas, meas_cap)
+        res.append({'status': o.status, 'flags': o.flags, 't_end': o.t_end, 'ip': o.ip,
+                    'qclk_end': o.qclk_end, 'n_instr': o.n_instr, 'n_events': o.n_events,
+                    'n_trace': o.n_trace, 'n_meas': o.n_meas, 'meas_bits': o.meas_bits,
+                    'regs': np.array(o.regs[:], np.uint32),
+                    'events': ev[:ne].copy(), 'amp': amp[:ne].copy(), 'trace': tr[:nt].copy(),
+                    'meas': ms[:nm].copy()})
+    return bool(ok), res

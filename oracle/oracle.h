@@ -1,0 +1,173 @@
+/*
+ * oracle/oracle.h -- TEST INFRASTRUCTURE: CPU restatements used as checkers.
+ *
+ *   oracle_rtl  (rtl_model.c)  literal per-clock restatement of the hdl/ modules
+ *   oracle_fast (fast_model.c) event-driven restatement: the closed-form
+ *               decode-to-decode timing of SURVEY.md §2.4, pinned to
+ *               oracle_rtl by fuzzing (tests/test_fast_vs_rtl.py)
+ *   oracle_dds  (dds_ref.c)    fixed-point DDS restatement
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load liboracle.so, and only as the checker / CPU baseline.
+ */
+#ifndef DPEMU_ORACLE_H
+#define DPEMU_ORACLE_H
+
+#include <stdint.h>
+#include "../include/dpemu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORACLE_FPROC_EXTERNAL 99   /* testbench drives fproc_ready/data (cocotb style) */
+
+uint32_t oracle_alu(uint32_t ctrl, uint32_t in0, uint32_t in1);
+void oracle_pulse_reg(uint32_t pr[5], const uint32_t lc[4], uint32_t reg_in, int write_en);
+uint32_t oracle_philox_u32(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m);
+
+/* ---- per-clock model ---------------------------------------------------- */
+typedef struct {
+    uint8_t reset_reg, reset_sr, qclk_trig, cstrobe_p;
+    uint8_t state; uint32_t mwc;
+    uint32_t lc[4];
+    uint32_t ipv, ipv_inc, ra[3];
+    uint32_t alu_in0, alu_in1, alu_out, qclk;
+    uint32_t p_env, p_phase, p_freq, p_amp, p_cfg; uint8_t p_cstrobe;
+    uint8_t reg_we; uint32_t reg_wa, reg_wd;
+} rtl_core_regs;
+
+typedef struct {
+    uint32_t state, opcode, qclk;
+    uint32_t cstrobe, env, phase, freq, amp, cfg;      /* pulse_iface */
+    uint32_t pulse_reset, done_gate, sync_enable, fproc_enable, fproc_id;
+    uint32_t instr_ptr, load_en, load_addr;
+    uint32_t cmd_buf_out[4];
+    uint32_t reg_we, reg_wa, reg_wd, qclk_load, qclk_rst_ctrl;
+} rtl_core_comb;
+
+typedef struct {
+    /* registers (proc.sv, ctrl.v, instr_ptr.v, cmd_mem.v, alu.v, qclk.v, pulse_reg.sv) */
+    uint8_t reset_reg, reset_sr, qclk_trig, cstrobe_p;
+    uint8_t state; uint32_t mwc;
+    uint32_t lc[4];
+    uint32_t ipv, ipv_inc, ra[3];
+    uint32_t regs[16];
+    uint32_t alu_in0, alu_in1, alu_out, qclk;
+    uint32_t p_env, p_phase, p_freq, p_amp, p_cfg; uint8_t p_cstrobe;
+    /* program */
+    const uint32_t *prog; uint32_t n_instr, addr_mask;
+    /* this clock */
+    rtl_core_comb comb;
+    rtl_core_regs nxt;
+} rtl_core;
+
+void rtl_core_init(rtl_core *c, const uint32_t *prog, uint32_t n_instr, int addr_width);
+void rtl_core_eval(rtl_core *c, int reset, int fproc_ready, uint32_t fproc_data, int sync_ready);
+void rtl_core_commit(rtl_core *c);
+
+typedef struct {
+    uint32_t cores;          /* C */
+    uint32_t fproc_mode;     /* DPEMU_FPROC_MEAS / _LUT / ORACLE_FPROC_EXTERNAL */
+    uint32_t sync_external;  /* testbench drives sync_ready */
+    uint32_t meas_elem, meas_latency, sync_latency;
+    uint64_t sync_mask, seed;
+    uint32_t lut_mask;
+    uint32_t p1_threshold[DPEMU_MAX_CORES];
+    uint64_t lut_table[256];
+} oracle_shot_cfg;
+
+#define RTL_MQ 64
+typedef struct { uint64_t t[RTL_MQ]; uint8_t bit[RTL_MQ]; uint32_t head, tail; } rtl_meas_q;
+
+typedef struct {
+    int reset;
+    int drive_meas; uint64_t meas_valid, meas;
+    int fproc_ready[DPEMU_MAX_CORES]; uint32_t fproc_data[DPEMU_MAX_CORES];
+    int sync_ready;
+} rtl_ext_inputs;
+
+/* fproc back end: fproc_meas.sv, or core_state_mgr.sv + meas_lut.sv */
+typedef struct {
+    uint32_t mode, n, addr_mask, lut_mask;
+    uint64_t lut_table[256];
+    /* fproc_meas registers */
+    uint8_t arm[DPEMU_MAX_CORES], ready[DPEMU_MAX_CORES];
+    uint32_t addr[DPEMU_MAX_CORES], data[DPEMU_MAX_CORES];
+    uint64_t meas_reg;
+    /* core_state_mgr / meas_lut registers */
+    uint8_t cs[DPEMU_MAX_CORES];
+    uint8_t lut_state; uint64_t lut_valid, lut_addr;
+    /* this clock */
+    int out_ready[DPEMU_MAX_CORES]; uint32_t out_data[DPEMU_MAX_CORES];
+    int lut_ready; uint64_t lut_v, lut_a;
+} rtl_fproc;
+
+void rtl_fproc_init(rtl_fproc *f, uint32_t mode, uint32_t n, uint32_t lut_mask, const uint64_t *lut_table);
+void rtl_fproc_eval(rtl_fproc *f, uint64_t valid, uint64_t meas);
+void rtl_fproc_commit(rtl_fproc *f, int reset, uint64_t valid, uint64_t meas,
+                      const uint32_t *enable, const uint32_t *id);
+
+typedef struct {
+    oracle_shot_cfg cfg;
+    uint64_t shot, cycle;
+    rtl_core core[DPEMU_MAX_CORES];
+    rtl_fproc fp;
+    uint64_t sync_mask;
+    /* measurement model */
+    rtl_meas_q mq[DPEMU_MAX_CORES];
+    uint32_t n_meas[DPEMU_MAX_CORES];
+    uint64_t cur_valid, cur_meas;
+    /* sync controller */
+    uint64_t sync_arrived; int sync_pend; uint64_t sync_t;
+} rtl_shot;
+
+typedef struct rtl_tb rtl_tb;
+rtl_tb *rtl_tb_new(void);
+void rtl_tb_free(rtl_tb *tb);
+void rtl_tb_set(rtl_tb *tb, int reset, int fproc_ready, uint32_t fproc_data, int sync_ready);
+void rtl_tb_write(rtl_tb *tb, int en, uint32_t addr, const uint32_t *word);
+void rtl_tb_edge(rtl_tb *tb);
+const rtl_core_comb *rtl_tb_snap(const rtl_tb *tb);
+uint32_t rtl_tb_reg(const rtl_tb *tb, int i);
+
+typedef struct rtl_fproc_tb rtl_fproc_tb;
+rtl_fproc_tb *rtl_fproc_tb_new(uint32_t mode, uint32_t n, uint32_t lut_mask, const uint64_t *lut_table);
+void rtl_fproc_tb_free(rtl_fproc_tb *tb);
+void rtl_fproc_tb_set(rtl_fproc_tb *tb, int reset, uint64_t meas, uint64_t valid, uint64_t enable_mask,
+                      const uint32_t *id);
+void rtl_fproc_tb_edge(rtl_fproc_tb *tb);
+uint32_t rtl_fproc_tb_ready(const rtl_fproc_tb *tb);
+uint32_t rtl_fproc_tb_data(const rtl_fproc_tb *tb, int c);
+
+void rtl_shot_init(rtl_shot *s, const oracle_shot_cfg *cfg, const uint32_t *const *progs,
+                   const uint32_t *n_instr, uint64_t shot_index);
+void rtl_shot_step(rtl_shot *s, const rtl_ext_inputs *ext);
+
+/* per-lane result of one shot, dpemu formats */
+typedef struct {
+    uint32_t status, flags, t_end, ip, qclk_end, n_instr;
+    uint32_t n_events, n_trace, n_meas, meas_bits;
+    uint32_t regs[16];
+    uint32_t *ev;      /* [ev_cap][4] */
+    uint16_t *amp;     /* [ev_cap]    */
+    uint32_t *tr;      /* [tr_cap][4] */
+    uint32_t *meas;    /* [meas_cap][2] */
+} oracle_lane_out;
+
+int rtl_run_shot(const oracle_shot_cfg *cfg, const uint32_t *const *progs, const uint32_t *n_instr,
+                 uint64_t shot, uint32_t horizon, uint32_t ev_cap, uint32_t tr_cap,
+                 uint32_t meas_cap, oracle_lane_out *out);
+
+/* ---- event-driven model, dpemu_run-compatible batch entry ------------------ */
+int fast_run(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
+             const uint32_t *n_instr, const uint32_t *prog_table, uint64_t shot_begin,
+             uint64_t n_shots, const dpemu_outputs *out, int n_threads);
+
+/* ---- DDS restatement --------------------------------------------------------- */
+void oracle_dds_sin_lut(int16_t *out4096);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
