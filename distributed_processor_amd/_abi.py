@@ -1,0 +1,130 @@
+"""ctypes mirror of include/dpemu.h (structs, constants, output layout)."""
+
+import ctypes as C
+
+import numpy as np
+
+ABI_VERSION = 1
+MAX_CORES = 64
+MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
+
+ST_DONE, ST_MAX_CYCLES, ST_HUNG_OPCODE, ST_DEADLOCK = 1, 2, 3, 4
+F_LATE, F_EVENT_OVF, F_TRACE_OVF, F_MEAS_OVF, F_DOUBLE_STROBE = 0x01, 0x02, 0x04, 0x08, 0x10
+FPROC_MEAS, FPROC_LUT = 0, 1
+EV_STROBE, EV_PULSE_RESET = 0, 1
+TRACE_QCLK_LOAD, TRACE_QCLK_RST = 16, 17
+MAX_CYCLES_LIMIT = 2 ** 31 - 64
+
+STATUS_NAMES = {0: 'running', ST_DONE: 'done', ST_MAX_CYCLES: 'max_cycles',
+                ST_HUNG_OPCODE: 'hung_opcode', ST_DEADLOCK: 'deadlock'}
+
+
+class Config(C.Structure):
+    _fields_ = [('cores_per_shot', C.c_uint32), ('n_groups', C.c_uint32),
+                ('shots_per_group', C.c_uint32), ('max_cycles', C.c_uint32),
+                ('event_cap', C.c_uint32), ('trace_cap', C.c_uint32), ('meas_cap', C.c_uint32),
+                ('fproc_mode', C.c_uint32), ('meas_elem', C.c_uint32), ('meas_latency', C.c_uint32),
+                ('sync_latency', C.c_uint32), ('reserved0', C.c_uint32),
+                ('sync_mask', C.c_uint64), ('seed', C.c_uint64),
+                ('lut_mask', C.c_uint32), ('reserved1', C.c_uint32),
+                ('p1_threshold', C.c_uint32 * MAX_CORES), ('lut_table', C.c_uint64 * 256)]
+
+
+class Outputs(C.Structure):
+    _fields_ = [('summary', C.c_void_p), ('ev_main', C.c_void_p), ('ev_amp', C.c_void_p),
+                ('trace', C.c_void_p), ('meas', C.c_void_p), ('regs', C.c_void_p),
+                ('hist', C.c_void_p)]
+
+
+class DDSChannels(C.Structure):
+    _fields_ = [('n_channels', C.c_uint32), ('n_lanes', C.c_uint32), ('n_samples', C.c_uint32),
+                ('reserved', C.c_uint32)] + [(n, C.c_void_p) for n in (
+                    'ch_lane', 'ch_elem', 'spc', 'interp', 'env_off', 'env_len', 'freq_off', 'freq_len')]
+
+
+DEFAULT_LUT_TABLE = (0b00000, 0b00100, 0b10000, 0b01000)   # meas_lut.sv:17-20
+
+
+def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 20,
+                event_cap=64, trace_cap=0, meas_cap=8, fproc_mode=FPROC_MEAS, meas_elem=2,
+                meas_latency=64, sync_latency=1, sync_mask=0, seed=0x5EED, p1=0.5,
+                lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE):
+    """Validated Config.  p1: float or per-core list of P(meas = 1)."""
+    C_ = int(cores_per_shot)
+    if C_ < 1 or C_ > MAX_CORES or (C_ & (C_ - 1)):
+        raise ValueError('cores_per_shot must be a power of two in [1, 64]')
+    if not (0 < max_cycles <= MAX_CYCLES_LIMIT):
+        raise ValueError('max_cycles must be in (0, 2^31 - 64]')
+    if meas_latency < 1 or sync_latency < 1:
+        raise ValueError('meas_latency and sync_latency must be >= 1')
+    if lut_mask == 0:
+        raise ValueError('lut_mask must be nonzero')
+    if meas_cap > 32:
+        raise ValueError('meas_cap must be <= 32')
+    cfg = Config()
+    cfg.cores_per_shot = C_
+    cfg.n_groups = int(n_groups)
+    cfg.shots_per_group = int(shots_per_group)
+    cfg.max_cycles = int(max_cycles)
+    cfg.event_cap = int(event_cap)
+    cfg.trace_cap = int(trace_cap)
+    cfg.meas_cap = int(meas_cap)
+    cfg.fproc_mode = int(fproc_mode)
+    cfg.meas_elem = int(meas_elem)
+    cfg.meas_latency = int(meas_latency)
+    cfg.sync_latency = int(sync_latency)
+    cfg.sync_mask = int(sync_mask)
+    cfg.seed = int(seed) & (2 ** 64 - 1)
+    cfg.lut_mask = int(lut_mask)
+    ps = list(p1) if isinstance(p1, (list, tuple, np.ndarray)) else [p1] * C_
+    for c, p in enumerate(ps):
+        cfg.p1_threshold[c] = prob_to_threshold(p)
+    for i, v in enumerate(lut_table):
+        cfg.lut_table[i] = int(v)
+    return cfg
+
+
+def prob_to_threshold(p):
+    p = float(p)
+    if p >= 1.0:
+        return 0xFFFFFFFF
+    if p <= 0.0:
+        return 0
+    return min(int(round(p * 2 ** 32)), 0xFFFFFFFE)
+
+
+def alloc_host_outputs(cfg, n_shots, want=('summary', 'ev_main', 'ev_amp', 'trace', 'meas',
+                                           'regs', 'hist')):
+    """numpy arrays laid out as dpemu_outputs describes (host side)."""
+    n_lanes = int(n_shots) * cfg.cores_per_shot
+    out = {}
+    if 'summary' in want:
+        out['summary'] = np.zeros((n_lanes, 8), np.uint32)
+    if 'ev_main' in want and cfg.event_cap:
+        out['ev_main'] = np.zeros((cfg.event_cap, n_lanes, 4), np.uint32)
+    if 'ev_amp' in want and cfg.event_cap:
+        out['ev_amp'] = np.zeros((cfg.event_cap, n_lanes), np.uint16)
+    if 'trace' in want and cfg.trace_cap:
+        out['trace'] = np.zeros((cfg.trace_cap, n_lanes, 4), np.uint32)
+    if 'meas' in want and cfg.meas_cap:
+        out['meas'] = np.zeros((cfg.meas_cap, n_lanes, 2), np.uint32)
+    if 'regs' in want:
+        out['regs'] = np.zeros((16, n_lanes), np.uint32)
+    if 'hist' in want and cfg.cores_per_shot <= 12:
+        out['hist'] = np.zeros((cfg.n_groups, 1 << cfg.cores_per_shot), np.uint64)
+    return out
+
+
+def outputs_struct(arrays):
+    o = Outputs()
+    for name, _ in Outputs._fields_:
+        a = arrays.get(name)
+        setattr(o, name, a.ctypes.data if a is not None else None)
+    return o
+
+
+def unpack_summary(summary):
+    s = np.asarray(summary)
+    return {'t_end': s[:, 0], 'ip': s[:, 1] & 0xFFFF, 'status': (s[:, 1] >> 16) & 0xFF,
+            'flags': s[:, 1] >> 24, 'n_events': s[:, 2], 'n_instr': s[:, 3], 'qclk_end': s[:, 4],
+            'n_meas': s[:, 5], 'meas_bits': s[:, 6], 'n_trace': s[:, 7]}

@@ -223,6 +223,47 @@ class PulseRegTB:
     cfg = property(lambda self: self.state[4])
 
 
+def fast_run(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots, threads=0,
+             want=('summary', 'ev_main', 'ev_amp', 'trace', 'meas', 'regs', 'hist')):
+    """Event-driven model over shots [shot_begin, shot_begin + n_shots).
+
+    cfg: distributed_processor_amd._abi.Config; words: (n, 4) uint32 of all
+    programs; returns the dict of host output arrays (dpemu_outputs layout)."""
+    from distributed_processor_amd import _abi
+    L = lib()
+    words = np.ascontiguousarray(words, dtype=np.uint32)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+    n_instr = np.ascontiguousarray(n_instr, dtype=np.uint32)
+    prog_table = np.ascontiguousarray(prog_table, dtype=np.uint32)
+    out = _abi.alloc_host_outputs(cfg, n_shots, want)
+    ostruct = _abi.outputs_struct(out)
+    rc = L.fast_run(C.addressof(cfg), words.ctypes.data, offsets.ctypes.data, n_instr.ctypes.data,
+                    prog_table.ctypes.data, int(shot_begin), int(n_shots), C.addressof(ostruct),
+                    int(threads))
+    if rc != 0:
+        raise RuntimeError('fast_run failed: {}'.format(rc))
+    return out
+
+
+def shot_cfg_from_config(cfg):
+    """oracle_shot_cfg equivalent of a dpemu Config."""
+    s = ShotCfg()
+    s.cores = cfg.cores_per_shot
+    s.fproc_mode = cfg.fproc_mode
+    s.sync_external = 0
+    s.meas_elem = cfg.meas_elem
+    s.meas_latency = cfg.meas_latency
+    s.sync_latency = cfg.sync_latency
+    s.sync_mask = cfg.sync_mask
+    s.seed = cfg.seed
+    s.lut_mask = cfg.lut_mask
+    for i in range(64):
+        s.p1_threshold[i] = cfg.p1_threshold[i]
+    for i in range(256):
+        s.lut_table[i] = cfg.lut_table[i]
+    return s
+
+
 def make_shot_cfg(cores, fproc_mode=FPROC_MEAS, meas_elem=2, meas_latency=1, sync_latency=1,
                   sync_mask=0, seed=0x5EED, p1=None, lut_mask=0b11, lut_table=None,
                   sync_external=0):

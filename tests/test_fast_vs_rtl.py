@@ -1,0 +1,122 @@
+"""oracle_fast (event-driven closed forms) vs oracle_rtl (per clock), bit for bit.
+
+Every lane of every fuzzed shot must agree on: terminal state (t_end, ip,
+qclk_end, instruction count, final registers), the full pulse-event stream
+(cstrobe snapshots and pulse_reset), the register/qclk trace and the
+measurement records.  Lanes that never finish (late triggers, deadlocks,
+hang opcodes, runaway loops) are compared on every event up to the
+simulated horizon.
+"""
+
+import numpy as np
+import pytest
+
+import oracle
+from distributed_processor_amd import _abi
+from tests.progfuzz import pack_programs, random_case
+
+HORIZON = 6000
+EV_CAP, TR_CAP, MEAS_CAP = 128, 128, 16
+
+
+def run_both(case, n_shots=4, seed=0x5EED, meas_latency=20, sync_latency=1, sync_mask=0, shot0=0):
+    C = case['ncores']
+    mode = _abi.FPROC_MEAS if case['mode'] == 'meas' else _abi.FPROC_LUT
+    cfg = _abi.make_config(C, n_groups=case['n_groups'], shots_per_group=1, max_cycles=HORIZON,
+                           event_cap=EV_CAP, trace_cap=TR_CAP, meas_cap=MEAS_CAP, fproc_mode=mode,
+                           meas_latency=meas_latency, sync_latency=sync_latency, sync_mask=sync_mask,
+                           seed=seed, p1=0.5)
+    words, offs, ni = pack_programs(case['progs'])
+    fast = oracle.fast_run(cfg, words, offs, ni, case['table'], shot0, n_shots)
+    scfg = oracle.shot_cfg_from_config(cfg)
+    rtl = []
+    for s in range(n_shots):
+        shot = shot0 + s
+        g = shot % case['n_groups']
+        progs = [np.asarray(__import__('distributed_processor_amd').isa.words_to_u32(case['progs'][case['table'][g * C + c]]))
+                 for c in range(C)]
+        ok, lanes = oracle.rtl_run_shot(scfg, progs, shot, HORIZON + 16, EV_CAP, TR_CAP, MEAS_CAP)
+        rtl.append(lanes)
+    return cfg, fast, rtl
+
+
+def compare(cfg, fast, rtl, n_shots):
+    C = cfg.cores_per_shot
+    n_lanes = n_shots * C
+    summ = _abi.unpack_summary(fast['summary'])
+    stats = {'done': 0, 'other': 0, 'events': 0}
+    for s in range(n_shots):
+        for c in range(C):
+            L = s * C + c
+            r = rtl[s][c]
+            ne = min(int(summ['n_events'][L]), EV_CAP)
+            fev = fast['ev_main'][:ne, L]
+            famp = fast['ev_amp'][:ne, L]
+            nt = min(int(summ['n_trace'][L]), TR_CAP)
+            ftr = fast['trace'][:nt, L]
+            nm = min(int(summ['n_meas'][L]), MEAS_CAP)
+            fms = fast['meas'][:nm, L]
+            ctx = 'shot {} core {}'.format(s, c)
+            if r['status'] == _abi.ST_DONE:
+                stats['done'] += 1
+                assert summ['status'][L] == _abi.ST_DONE, ctx
+                assert summ['t_end'][L] == r['t_end'], ctx
+                assert summ['ip'][L] == r['ip'], ctx
+                assert summ['qclk_end'][L] == r['qclk_end'], ctx
+                assert summ['n_instr'][L] == r['n_instr'], ctx
+                assert summ['n_events'][L] == r['n_events'], ctx
+                np.testing.assert_array_equal(fev, r['events'], err_msg=ctx)
+                np.testing.assert_array_equal(famp, r['amp'], err_msg=ctx)
+                assert summ['n_trace'][L] == r['n_trace'], ctx
+                np.testing.assert_array_equal(ftr, r['trace'], err_msg=ctx)
+                assert summ['n_meas'][L] == r['n_meas'], ctx
+                np.testing.assert_array_equal(fms, r['meas'], err_msg=ctx)
+                assert summ['meas_bits'][L] == r['meas_bits'], ctx
+                np.testing.assert_array_equal(fast['regs'][:, L], r['regs'], err_msg=ctx)
+            else:
+                stats['other'] += 1
+                assert summ['status'][L] != _abi.ST_DONE, ctx
+                lim = HORIZON - 16
+                fe = fev[fev[:, 0] <= lim]
+                re_ = r['events'][r['events'][:, 0] <= lim] if len(r['events']) else r['events']
+                np.testing.assert_array_equal(fe, re_.reshape(-1, 4), err_msg=ctx)
+                ft = ftr[ftr[:, 0] <= lim]
+                rt = r['trace'][r['trace'][:, 0] <= lim] if len(r['trace']) else r['trace']
+                np.testing.assert_array_equal(ft, rt.reshape(-1, 4), err_msg=ctx)
+            stats['events'] += ne
+    return stats
+
+
+@pytest.mark.parametrize('seed', range(60))
+def test_fuzz_fast_vs_rtl(seed):
+    case = random_case(seed)
+    n_shots = 3
+    cfg, fast, rtl = run_both(case, n_shots=n_shots, shot0=seed * 7)
+    compare(cfg, fast, rtl, n_shots)
+
+
+@pytest.mark.parametrize('seed', range(20))
+def test_fuzz_multicore_sync_fproc(seed):
+    case = random_case(1000 + seed, ncores=4, mode='meas', allow_late=False, allow_hang=False)
+    cfg, fast, rtl = run_both(case, n_shots=3, meas_latency=1 + seed % 5, sync_latency=1 + seed % 3)
+    st = compare(cfg, fast, rtl, 3)
+    assert st['events'] > 0
+
+
+@pytest.mark.parametrize('seed', range(20))
+def test_fuzz_lut(seed):
+    case = random_case(2000 + seed, ncores=4, mode='lut', allow_late=False, allow_hang=False)
+    cfg, fast, rtl = run_both(case, n_shots=3, meas_latency=2 + seed % 7)
+    compare(cfg, fast, rtl, 3)
+
+
+def test_fuzz_mostly_finishes():
+    """guard against a fuzzer that only produces non-terminating lanes"""
+    done = other = 0
+    for seed in range(30):
+        case = random_case(seed, allow_late=False, allow_hang=False, mode='meas')
+        cfg, fast, rtl = run_both(case, n_shots=2)
+        st = compare(cfg, fast, rtl, 2)
+        done += st['done']
+        other += st['other']
+    assert done > 3 * other
