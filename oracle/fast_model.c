@@ -55,7 +55,6 @@ typedef struct {
     uint64_t shot;
     uint32_t C, addr_mask;
     uint64_t part;                   /* sync participants */
-    uint32_t last_S; int have_S;     /* most recent barrier ready cycle */
     /* meas_lut */
     int lut_ready_next;              /* last fire cycle + 1 is LUT_READY */
     uint32_t lut_last_fire;
@@ -189,9 +188,8 @@ static void try_barrier(fshot *s)
         if (s->L[c].wait_d > maxd) maxd = s->L[c].wait_d;
     }
     uint32_t S = maxd + s->cfg->sync_latency;
-    s->last_S = S; s->have_S = 1;
     for (uint32_t c = 0; c < s->C; c++)
-        if (s->L[c].mode == M_SYNC && s->L[c].wait_d + 1 <= S) sync_release(s, &s->L[c], S);
+        if ((s->part >> c) & 1) sync_release(s, &s->L[c], S);
 }
 
 /* ---- meas_lut evolution over the merged measurement stream ------------------ */
@@ -242,6 +240,7 @@ static uint32_t strobe_bound(const fshot *s, const flane *l)
     case M_RUN: return l->t + 2;
     case M_LUT: return l->wait_d + 7;
     case M_SYNC: {
+        if (!((s->part >> (l->lane % s->C)) & 1)) return INF32;   /* never released */
         uint64_t m = 0;
         for (uint32_t c = 0; c < s->C; c++) {
             if (!((s->part >> c) & 1)) continue;
@@ -388,11 +387,8 @@ static void exec_one(fshot *s, flane *l)
         return;
     }
     case 0x7:
+        /* a core outside sync_mask never receives ready: it waits forever */
         l->mode = M_SYNC; l->wait_d = D;
-        if (!((s->part >> (l->lane % s->C)) & 1) && s->have_S && D + 1 <= s->last_S) {
-            sync_release(s, l, s->last_S);       /* non-participant caught by a pending barrier */
-            return;
-        }
         try_barrier(s);
         return;
     default:

@@ -360,7 +360,10 @@ void rtl_shot_step(rtl_shot *s, const rtl_ext_inputs *ext)
     }
     int sready = s->cfg.sync_external ? ext->sync_ready : (s->sync_pend && s->sync_t == s->cycle);
 
-    for (uint32_t c = 0; c < C; c++) rtl_core_eval(&s->core[c], reset, fready[c], fdata[c], sready);
+    /* the controller drives ready to the barrier's participants only */
+    for (uint32_t c = 0; c < C; c++)
+        rtl_core_eval(&s->core[c], reset, fready[c], fdata[c],
+                      sready && (s->cfg.sync_external || ((s->sync_mask >> c) & 1)));
 
     /* measurement model: a readout strobe schedules meas_valid latency clocks later */
     for (uint32_t c = 0; c < C; c++) {
@@ -384,8 +387,8 @@ void rtl_shot_step(rtl_shot *s, const rtl_ext_inputs *ext)
         rtl_fproc_commit(&s->fp, reset, valid, meas, en, id);
     }
 
-    /* sync controller (build-defined): ready to every core `sync_latency` clocks
-     * after the last participant's enable; then the next barrier begins */
+    /* sync controller (build-defined): ready to the participants `sync_latency`
+     * clocks after the last participant's enable; then the next barrier begins */
     if (!s->cfg.sync_external) {
         uint64_t en = 0;
         for (uint32_t c = 0; c < C; c++) if (s->core[c].comb.sync_enable) en |= 1ull << c;

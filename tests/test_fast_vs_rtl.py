@@ -120,3 +120,12 @@ def test_fuzz_mostly_finishes():
         done += st['done']
         other += st['other']
     assert done > 3 * other
+
+
+@pytest.mark.parametrize('seed', range(10))
+def test_fuzz_partial_sync_mask(seed):
+    """cores outside sync_mask that execute SYNC never get ready (DEADLOCK);
+    the participants' barriers complete without them"""
+    case = random_case(3000 + seed, ncores=4, mode='meas', allow_late=False, allow_hang=False)
+    cfg, fast, rtl = run_both(case, n_shots=2, sync_mask=0b0111, sync_latency=1 + seed % 4)
+    compare(cfg, fast, rtl, 2)
