@@ -9,7 +9,7 @@ MAX_CORES = 64
 MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
 
 ST_DONE, ST_MAX_CYCLES, ST_HUNG_OPCODE, ST_DEADLOCK = 1, 2, 3, 4
-F_LATE, F_EVENT_OVF, F_TRACE_OVF, F_MEAS_OVF, F_DOUBLE_STROBE = 0x01, 0x02, 0x04, 0x08, 0x10
+F_LATE, F_EVENT_OVF, F_TRACE_OVF, F_MEAS_OVF, F_DOUBLE_STROBE, F_GUARD = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 FPROC_MEAS, FPROC_LUT = 0, 1
 EV_STROBE, EV_PULSE_RESET = 0, 1
 TRACE_QCLK_LOAD, TRACE_QCLK_RST = 16, 17

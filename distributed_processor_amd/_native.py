@@ -1,0 +1,52 @@
+"""ctypes binding of libdpemu.so (include/dpemu.h).  No fallback: if the HIP
+library is missing or a GPU call fails, this raises."""
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libdpemu.so')
+
+# every entry point declared in include/dpemu.h
+EXPORTS = ('dpemu_abi_version', 'dpemu_create', 'dpemu_destroy', 'dpemu_last_error',
+           'dpemu_load_programs', 'dpemu_run', 'dpemu_run_host', 'dpemu_dds', 'dpemu_dds_sin_lut')
+
+_lib = None
+
+
+class DpemuError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise DpemuError('libdpemu.so not built ({}); run __graft_entry__.build() '
+                         '(hipcc --offload-arch=gfx950)'.format(path))
+    L = C.CDLL(path)
+    vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+    L.dpemu_abi_version.restype = C.c_int
+    L.dpemu_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.dpemu_destroy.argtypes = [vp]
+    L.dpemu_last_error.argtypes = [vp]
+    L.dpemu_last_error.restype = C.c_char_p
+    L.dpemu_load_programs.argtypes = [vp, vp, vp, vp, u32, vp, u32, u32]
+    L.dpemu_run.argtypes = [vp, vp, u64, u64, vp, vp]
+    L.dpemu_run_host.argtypes = [vp, vp, u64, u64, vp]
+    L.dpemu_dds.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.dpemu_dds_sin_lut.argtypes = [vp]
+    from . import _abi
+    if L.dpemu_abi_version() != _abi.ABI_VERSION:
+        raise DpemuError('ABI version mismatch: library {} vs host {}'.format(
+            L.dpemu_abi_version(), _abi.ABI_VERSION))
+    _lib = L
+    return L
+
+
+def check(ctx_handle, rc, what):
+    if rc != 0:
+        L = load_library()
+        msg = L.dpemu_last_error(ctx_handle)
+        raise DpemuError('{} failed ({}): {}'.format(what, rc, msg.decode() if msg else ''))

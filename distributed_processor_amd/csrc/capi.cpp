@@ -1,0 +1,319 @@
+// capi.cpp -- the extern "C" boundary of libdpemu.so (include/dpemu.h).
+//
+// Replaces the reference's simulation harness: where the
+// cocotb testbench loaded cmd_mem word by word (cocotb/proc/test_proc.py:29-38)
+// and clocked one Verilator toplevel_sim, dpemu_load_programs uploads every
+// assembled program once and dpemu_run executes n_shots x C cores on the GPU.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+using namespace dpemu;
+
+struct dpemu_ctx {
+    int device = 0;
+    std::string err;
+    // programs
+    uint4 *d_words = nullptr;
+    uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
+    uint32_t n_programs = 0, n_groups = 0, C = 0;
+    uint64_t n_quads = 0;
+    bool has_fproc = false, has_sync = false;
+    // run constants
+    uint32_t *d_thr = nullptr;
+    uint64_t *d_lut = nullptr;
+    std::vector<uint32_t> thr_cache;
+    std::vector<uint64_t> lut_cache;
+    // DDS
+    int16_t *d_sin = nullptr;
+    uint32_t *d_ch = nullptr;
+    uint32_t ch_cap = 0;
+};
+
+static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...) __attribute__((format(printf, 3, 4)));
+static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, call)                                                                  \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(ctx, DPEMU_E_DEVICE, "%s: %s", #call, hipGetErrorString(e_));      \
+    } while (0)
+
+static void free_programs(dpemu_ctx *ctx)
+{
+    (void)hipFree(ctx->d_words); (void)hipFree(ctx->d_offsets); (void)hipFree(ctx->d_ninstr); (void)hipFree(ctx->d_table);
+    ctx->d_words = nullptr; ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
+    ctx->n_programs = 0;
+}
+
+extern "C" {
+
+int dpemu_abi_version(void) { return DPEMU_ABI_VERSION; }
+
+int dpemu_create(int device, dpemu_ctx **out)
+{
+    if (!out) return DPEMU_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return DPEMU_E_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return DPEMU_E_DEVICE;
+    dpemu_ctx *ctx = new dpemu_ctx();
+    ctx->device = device;
+    if (hipMalloc(&ctx->d_thr, DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&ctx->d_lut, 256 * sizeof(uint64_t)) != hipSuccess) {
+        delete ctx;
+        return DPEMU_E_NOMEM;
+    }
+    std::vector<int16_t> lut(4096);
+    dpemu_dds_sin_lut(lut.data());
+    if (hipMalloc(&ctx->d_sin, 4096 * sizeof(int16_t)) != hipSuccess ||
+        hipMemcpy(ctx->d_sin, lut.data(), 4096 * sizeof(int16_t), hipMemcpyHostToDevice) != hipSuccess) {
+        delete ctx;
+        return DPEMU_E_NOMEM;
+    }
+    *out = ctx;
+    return DPEMU_OK;
+}
+
+int dpemu_destroy(dpemu_ctx *ctx)
+{
+    if (!ctx) return DPEMU_E_INVALID;
+    (void)hipSetDevice(ctx->device);
+    free_programs(ctx);
+    (void)hipFree(ctx->d_thr); (void)hipFree(ctx->d_lut); (void)hipFree(ctx->d_sin); (void)hipFree(ctx->d_ch);
+    delete ctx;
+    return DPEMU_OK;
+}
+
+const char *dpemu_last_error(dpemu_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *offsets,
+                        const uint32_t *n_instr, uint32_t n_programs, const uint32_t *prog_table,
+                        uint32_t n_groups, uint32_t cores_per_shot)
+{
+    if (!ctx) return DPEMU_E_INVALID;
+    if (!words || !offsets || !n_instr || !prog_table || n_programs == 0 || n_groups == 0)
+        return fail(ctx, DPEMU_E_INVALID, "load_programs: null array or empty program set");
+    const uint32_t C = cores_per_shot;
+    if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1)))
+        return fail(ctx, DPEMU_E_INVALID, "cores_per_shot %u is not a power of two in [1, 64]", C);
+    uint64_t quads = 0;
+    bool fp = false, sy = false;
+    for (uint32_t i = 0; i < n_programs; i++) {
+        if (n_instr[i] > 65536u)
+            return fail(ctx, DPEMU_E_INVALID, "program %u: %u commands exceed the 2^16-deep cmd_mem", i, n_instr[i]);
+        quads = std::max<uint64_t>(quads, (uint64_t)offsets[i] + n_instr[i]);
+    }
+    for (uint32_t i = 0; i < n_programs; i++)
+        for (uint32_t k = 0; k < n_instr[i]; k++) {
+            const uint32_t op4 = words[4 * ((uint64_t)offsets[i] + k) + 3] >> 28;
+            fp |= (op4 == 4 || op4 == 5);
+            sy |= (op4 == 7);
+        }
+    for (uint64_t i = 0; i < (uint64_t)n_groups * C; i++)
+        if (prog_table[i] >= n_programs)
+            return fail(ctx, DPEMU_E_INVALID, "prog_table[%llu] = %u >= n_programs", (unsigned long long)i, prog_table[i]);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    free_programs(ctx);
+    HIPCHK(ctx, hipMalloc(&ctx->d_words, std::max<uint64_t>(quads, 1) * 16));
+    HIPCHK(ctx, hipMalloc(&ctx->d_offsets, n_programs * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->d_ninstr, n_programs * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->d_table, (uint64_t)n_groups * C * 4));
+    if (quads) HIPCHK(ctx, hipMemcpy(ctx->d_words, words, quads * 16, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->d_offsets, offsets, n_programs * 4, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->d_ninstr, n_instr, n_programs * 4, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->d_table, prog_table, (uint64_t)n_groups * C * 4, hipMemcpyHostToDevice));
+    ctx->n_programs = n_programs;
+    ctx->n_groups = n_groups;
+    ctx->C = C;
+    ctx->n_quads = quads;
+    ctx->has_fproc = fp;
+    ctx->has_sync = sy;
+    return DPEMU_OK;
+}
+
+static int validate(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t n_shots, bool want_hist)
+{
+    if (!cfg) return fail(ctx, DPEMU_E_INVALID, "null config");
+    if (!ctx->n_programs) return fail(ctx, DPEMU_E_NOPROG, "run before load_programs");
+    if (cfg->cores_per_shot != ctx->C)
+        return fail(ctx, DPEMU_E_INVALID, "cores_per_shot %u != loaded %u", cfg->cores_per_shot, ctx->C);
+    if (cfg->n_groups != ctx->n_groups)
+        return fail(ctx, DPEMU_E_INVALID, "n_groups %u != loaded %u", cfg->n_groups, ctx->n_groups);
+    if (cfg->shots_per_group == 0) return fail(ctx, DPEMU_E_INVALID, "shots_per_group == 0");
+    if (cfg->max_cycles == 0 || cfg->max_cycles > 0x7FFFFFC0u)
+        return fail(ctx, DPEMU_E_INVALID, "max_cycles must be in (0, 2^31 - 64]");
+    if (cfg->meas_latency < 1 || cfg->meas_latency > (1u << 20) || cfg->sync_latency < 1 ||
+        cfg->sync_latency > (1u << 20))
+        return fail(ctx, DPEMU_E_INVALID, "meas_latency / sync_latency must be in [1, 2^20]");
+    if ((uint64_t)cfg->max_cycles + cfg->meas_latency + 16 >= 0x80000000ull)
+        return fail(ctx, DPEMU_E_INVALID, "max_cycles + meas_latency must stay below 2^31");
+    if (cfg->meas_cap > 32) return fail(ctx, DPEMU_E_INVALID, "meas_cap > 32");
+    if (cfg->fproc_mode > 1) return fail(ctx, DPEMU_E_INVALID, "fproc_mode %u", cfg->fproc_mode);
+    if (cfg->lut_mask == 0) return fail(ctx, DPEMU_E_INVALID, "lut_mask must be nonzero");
+    if (n_shots * cfg->cores_per_shot >= 0x80000000ull)
+        return fail(ctx, DPEMU_E_INVALID, "n_shots * cores_per_shot must be < 2^31 per run");
+    if (want_hist && cfg->cores_per_shot > 12)
+        return fail(ctx, DPEMU_E_INVALID, "histogram needs cores_per_shot <= 12");
+    return DPEMU_OK;
+}
+
+static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin, uint64_t n_shots,
+                    const dpemu_outputs *out, hipStream_t stream)
+{
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const uint32_t C = cfg->cores_per_shot;
+    std::vector<uint32_t> thr(cfg->p1_threshold, cfg->p1_threshold + DPEMU_MAX_CORES);
+    std::vector<uint64_t> lut(cfg->lut_table, cfg->lut_table + 256);
+    if (thr != ctx->thr_cache) {
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_thr, thr.data(), thr.size() * 4, hipMemcpyHostToDevice, stream));
+        ctx->thr_cache = thr;
+    }
+    if (lut != ctx->lut_cache) {
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_lut, lut.data(), lut.size() * 8, hipMemcpyHostToDevice, stream));
+        ctx->lut_cache = lut;
+    }
+    KParams p{};
+    p.words = ctx->d_words;
+    p.offsets = ctx->d_offsets; p.n_instr = ctx->d_ninstr; p.prog_table = ctx->d_table;
+    p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
+    p.summary = out->summary;
+    p.ev_main = reinterpret_cast<uint4 *>(out->ev_main);
+    p.ev_amp = out->ev_amp;
+    p.trace = reinterpret_cast<uint4 *>(out->trace);
+    p.meas = reinterpret_cast<uint2 *>(out->meas);
+    p.regs_out = out->regs;
+    p.hist = reinterpret_cast<unsigned long long *>(out->hist);
+    p.shot_begin = shot_begin;
+    p.n_lanes = (uint32_t)(n_shots * C);
+    p.C = C;
+    p.log2C = 0;
+    while ((1u << p.log2C) < C) p.log2C++;
+    p.n_groups = cfg->n_groups; p.shots_per_group = cfg->shots_per_group;
+    p.max_cycles = cfg->max_cycles;
+    p.event_cap = out->ev_main || out->ev_amp ? cfg->event_cap : 0;
+    p.trace_cap = out->trace ? cfg->trace_cap : 0;
+    p.meas_cap = cfg->meas_cap;
+    p.fproc_mode = cfg->fproc_mode; p.meas_elem = cfg->meas_elem;
+    p.meas_latency = cfg->meas_latency; p.sync_latency = cfg->sync_latency;
+    const uint64_t all = (C >= 64) ? ~0ull : ((1ull << C) - 1);
+    p.sync_mask = cfg->sync_mask ? (cfg->sync_mask & all) : all;
+    p.seed = cfg->seed;
+    p.lut_mask = cfg->lut_mask;
+    const uint64_t guard = (uint64_t)C * (cfg->max_cycles / 3u + 4u) + 1024u;
+    p.iter_guard = guard > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)guard;
+    int feat = 0;
+    if (ctx->has_fproc) feat |= (cfg->fproc_mode == DPEMU_FPROC_LUT) ? FEAT_LUT : FEAT_FPROC;
+    if (ctx->has_sync) feat |= FEAT_SYNC;
+    if (feat == (FEAT_LUT | FEAT_SYNC) || feat == FEAT_LUT || feat == 0 || feat == FEAT_FPROC ||
+        feat == FEAT_SYNC || feat == (FEAT_FPROC | FEAT_SYNC)) {
+        HIPCHK(ctx, launch_interp(p, feat, stream));
+    } else {
+        return fail(ctx, DPEMU_E_INVALID, "no kernel for feature set %d", feat);
+    }
+    return DPEMU_OK;
+}
+
+int dpemu_run(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin, uint64_t n_shots,
+              const dpemu_outputs *out, void *stream)
+{
+    if (!ctx) return DPEMU_E_INVALID;
+    if (!out) return fail(ctx, DPEMU_E_INVALID, "null outputs");
+    int rc = validate(ctx, cfg, n_shots, out->hist != nullptr);
+    if (rc) return rc;
+    if (n_shots == 0) return DPEMU_OK;
+    return run_impl(ctx, cfg, shot_begin, n_shots, out, (hipStream_t)stream);
+}
+
+int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin, uint64_t n_shots,
+                   const dpemu_outputs *host_out)
+{
+    if (!ctx) return DPEMU_E_INVALID;
+    if (!host_out) return fail(ctx, DPEMU_E_INVALID, "null outputs");
+    int rc = validate(ctx, cfg, n_shots, host_out->hist != nullptr);
+    if (rc) return rc;
+    if (n_shots == 0) return DPEMU_OK;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const uint64_t nl = n_shots * cfg->cores_per_shot;
+    struct Buf { void *host; void *dev; size_t bytes; bool in; };
+    Buf bufs[7] = {
+        {host_out->summary, nullptr, nl * 32, false},
+        {host_out->ev_main, nullptr, (size_t)cfg->event_cap * nl * 16, false},
+        {host_out->ev_amp, nullptr, (size_t)cfg->event_cap * nl * 2, false},
+        {host_out->trace, nullptr, (size_t)cfg->trace_cap * nl * 16, false},
+        {host_out->meas, nullptr, (size_t)cfg->meas_cap * nl * 8, false},
+        {host_out->regs, nullptr, nl * 64, false},
+        {host_out->hist, nullptr, (size_t)cfg->n_groups * (cfg->cores_per_shot <= 12 ? (1u << cfg->cores_per_shot) : 0) * 8, true},
+    };
+    int result = DPEMU_OK;
+    for (auto &b : bufs) {
+        if (!b.host || !b.bytes) { b.host = nullptr; continue; }
+        if (hipMalloc(&b.dev, b.bytes) != hipSuccess) { result = fail(ctx, DPEMU_E_NOMEM, "device allocation of %zu bytes failed", b.bytes); break; }
+        hipError_t e = b.in ? hipMemcpy(b.dev, b.host, b.bytes, hipMemcpyHostToDevice) : hipMemset(b.dev, 0, b.bytes);
+        if (e != hipSuccess) { result = fail(ctx, DPEMU_E_DEVICE, "%s", hipGetErrorString(e)); break; }
+    }
+    if (result == DPEMU_OK) {
+        dpemu_outputs d{};
+        d.summary = (uint32_t *)bufs[0].dev; d.ev_main = (uint32_t *)bufs[1].dev;
+        d.ev_amp = (uint16_t *)bufs[2].dev; d.trace = (uint32_t *)bufs[3].dev;
+        d.meas = (uint32_t *)bufs[4].dev; d.regs = (uint32_t *)bufs[5].dev;
+        d.hist = (uint64_t *)bufs[6].dev;
+        result = run_impl(ctx, cfg, shot_begin, n_shots, &d, nullptr);
+        if (result == DPEMU_OK) {
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess) result = fail(ctx, DPEMU_E_DEVICE, "kernel: %s", hipGetErrorString(e));
+        }
+        for (auto &b : bufs)
+            if (result == DPEMU_OK && b.host && b.dev &&
+                hipMemcpy(b.host, b.dev, b.bytes, hipMemcpyDeviceToHost) != hipSuccess)
+                result = fail(ctx, DPEMU_E_DEVICE, "copy back failed");
+    }
+    for (auto &b : bufs) if (b.dev) (void)hipFree(b.dev);
+    return result;
+}
+
+// Q15 sine table of the DDS: round(32767 sin(2 pi i / 4096)), built with integer-exact
+// symmetry from the first quadrant so every build gets the same bytes.
+int dpemu_dds_sin_lut(int16_t *out)
+{
+    if (!out) return DPEMU_E_INVALID;
+    for (int i = 0; i <= 1024; i++) {
+        const double v = std::round(32767.0 * std::sin(2.0 * M_PI * (double)i / 4096.0));
+        const int16_t q = (int16_t)v;
+        out[i & 4095] = q;                 // [0, pi/2]
+        if (i < 1024) out[2048 - i] = q;   // (pi/2, pi]
+        out[(2048 + i) & 4095] = (int16_t)-q;
+        if (i < 1024 && i > 0) out[4096 - i] = (int16_t)-q;
+    }
+    return DPEMU_OK;
+}
+
+}  // extern "C"
+
+extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uint32_t *summary,
+                         const uint32_t *ev_main, const uint16_t *ev_amp, const uint32_t *env_tables,
+                         const uint32_t *freq_tables, int16_t *iq_out, void *stream)
+{
+    (void)ch; (void)summary; (void)ev_main; (void)ev_amp; (void)env_tables; (void)freq_tables;
+    (void)iq_out; (void)stream;
+    return fail(ctx, DPEMU_E_INVALID, "dpemu_dds: not built yet");
+}

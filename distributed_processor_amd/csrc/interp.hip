@@ -1,0 +1,540 @@
+// interp.hip -- lockstep ISA interpreter for the QubiC distributed processor
+// on CDNA4 (gfx950).
+//
+// One thread = one (shot, core) lane.  Lane L = shot_local * C + core with C a
+// power of two <= 64, so the C cores of a shot are adjacent lanes of ONE
+// wavefront: every cross-core interaction of the gateware -- fproc reads of
+// another core's measurement (hdl/fproc_meas.sv), the meas_lut syndrome FSM
+// (hdl/core_state_mgr.sv, hdl/meas_lut.sv) and the sync barrier
+// (hdl/sync_iface.sv + build-defined controller) -- is resolved inside the
+// wave with shuffles, ballots and LDS; nothing crosses a workgroup.
+//
+// Each loop iteration retires at most one instruction per lane and advances
+// that lane's next-DECODE cycle by the closed-form latency of hdl/ctrl.v
+// (see oracle/fast_model.c for the restatement this kernel is pinned to).
+// Per-lane state lives in VGPRs (ip, next-decode cycle t, qclk anchor, pulse
+// register image, counters); the 16 x 32-bit reg_file lives in LDS as
+// [reg][lane] so a runtime register index is one ds_read_b32 with no bank
+// conflict.  Measurements (valid cycle << 1 | bit) live in LDS [slot][lane]
+// so other cores of the shot can read them.
+//
+// Cross-core ordering: a read of qubit q at DECODE cycle D (fproc_meas) needs
+// every meas_valid with cycle <= D.  Each lane publishes a lower bound of its
+// next readout strobe; the read proceeds once min(bound) + meas_latency > D.
+// The lane with the smallest pending read is never blocked by another read,
+// so the shot always progresses (a group with no progress is a true deadlock).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace dpemu {
+
+#define INF32 0xFFFFFFFFu
+
+enum : uint32_t { M_RUN = 0, M_SYNC = 1, M_LUT = 2, M_FIN = 3 };
+
+__device__ __forceinline__ uint32_t alu_op(uint32_t op, uint32_t a, uint32_t b)
+{
+    // alu.v:20-50; le = sub[31] ^ overflow == signed a < b
+    const uint32_t sub = a - b;
+    const uint32_t lt = (int32_t)a < (int32_t)b;
+    uint32_t r = a;                 // 0: id0
+    r = (op == 1) ? a + b : r;
+    r = (op == 2) ? sub : r;
+    r = (op == 3) ? (uint32_t)(sub == 0) : r;
+    r = (op == 4) ? lt : r;
+    r = (op == 5) ? (lt ^ 1u) : r;
+    r = (op == 6) ? b : r;
+    r = (op == 7) ? 0u : r;
+    return r;
+}
+
+// Philox4x32-10, output word 0 (counter = shot_lo, shot_hi, core, m; key = seed)
+__device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m)
+{
+    uint32_t c0 = (uint32_t)shot, c1 = (uint32_t)(shot >> 32), c2 = core, c3 = m;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return c0;
+}
+
+// group reductions over the C adjacent lanes of a shot (all lanes converged)
+template <int OP>   // 0 = min, 1 = max
+__device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t C)
+{
+    for (uint32_t m = 1; m < C; m <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)m, 64);
+        v = OP == 0 ? (o < v ? o : v) : (o > v ? o : v);
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t group_bits(uint64_t ballot, uint32_t lane_in_wave, uint32_t C)
+{
+    const uint32_t base = lane_in_wave & ~(C - 1);
+    const uint64_t gm = (C >= 64) ? ~0ull : ((1ull << C) - 1);
+    return (ballot >> base) & gm;
+}
+
+__device__ __forceinline__ void wave_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int FEAT>
+__global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
+{
+    constexpr bool FPROC = (FEAT & FEAT_FPROC) != 0;
+    constexpr bool SYNC = (FEAT & FEAT_SYNC) != 0;
+    constexpr bool LUT = (FEAT & FEAT_LUT) != 0;
+    constexpr bool XMEAS = FPROC || LUT;             // measurements readable by other lanes
+    constexpr int MT = XMEAS ? MEAS_LOOKUP : 1;
+    constexpr int NF = LUT ? LUT_FIRE_CAP : 1;
+
+    __shared__ uint32_t s_regs[16][BLOCK];
+    __shared__ uint32_t s_mt[MT][BLOCK];
+    // meas_lut per shot (slots indexed by the shot leader's tid)
+    __shared__ uint32_t s_cur[LUT ? BLOCK : 1];       // merge cursor into lane's s_mt
+    __shared__ uint32_t s_fire_t[NF][LUT ? BLOCK : 1];
+    __shared__ uint64_t s_fire_o[NF][LUT ? BLOCK : 1];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = blockIdx.x * BLOCK + tid;
+    const uint32_t C = p.C;
+    const uint32_t core = lane & (C - 1);
+    const uint32_t wl = tid & 63;                    // lane within the wavefront
+    const bool valid = lane < p.n_lanes;
+    const uint64_t shot = p.shot_begin + (uint64_t)(lane >> p.log2C);
+    const uint32_t leader_tid = tid & ~(C - 1);
+
+    uint32_t base = 0, nprog = 0, grp = 0;
+    if (valid) {
+        grp = (uint32_t)((shot / p.shots_per_group) % p.n_groups);
+        const uint32_t prog = p.prog_table[(uint64_t)grp * C + core];
+        base = p.offsets[prog];
+        nprog = p.n_instr[prog];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
+    if constexpr (XMEAS) {
+#pragma unroll
+        for (int m = 0; m < MT; m++) s_mt[m][tid] = INF32;
+    }
+    if constexpr (LUT) s_cur[tid] = 0;
+
+    // lane state
+    uint32_t mode = valid ? M_RUN : M_FIN;
+    uint32_t ip = 0, t = 0, qa_t = 1, qa_q = 0;      // qclk(0) = qclk(1) = 0: reset hold
+    uint32_t pe = 0, pp = 0, pa = 0;                 // pulse regs: env|cfg<<24, phase|freq<<17, amp
+    uint32_t wait_d = 0, status = 0, flags = 0;
+    uint32_t n_ev = 0, n_tr = 0, n_meas = 0, n_exec = 0, meas_bits = 0, last_bit = 0;
+    uint32_t t_end = 0, ip_end = 0, qclk_end = 0;
+    // leader-only meas_lut state
+    uint64_t lut_valid = 0, lut_addr = 0;
+    uint32_t lut_last_fire = INF32, nfire = 0;
+
+    const uint64_t n_lanes = p.n_lanes;
+    const bool is_part = SYNC ? (((p.sync_mask >> core) & 1ull) != 0) : false;
+
+    auto finish = [&](uint32_t st, uint32_t at) {
+        status = st; mode = M_FIN; t_end = at; ip_end = ip;
+        qclk_end = (at < qa_t) ? 0u : qa_q + (at - qa_t);
+    };
+
+    auto emit_event = [&](uint32_t te, uint32_t kind) {
+        if (n_ev < p.event_cap) {
+            const uint64_t idx = (uint64_t)n_ev * n_lanes + lane;
+            if (p.ev_main) {
+                const uint32_t q = (te < qa_t) ? 0u : qa_q + (te - qa_t);
+                p.ev_main[idx] = make_uint4(te, q, pe | (kind << 28), pp);
+            }
+            if (p.ev_amp) p.ev_amp[idx] = (uint16_t)pa;
+        } else flags |= F_EVENT_OVF;
+        n_ev++;
+        if (kind == 0 && p.meas_elem != 0xFFu && ((pe >> 24) & 3u) == p.meas_elem) {
+            const uint32_t r = philox_u32(p.seed, shot, core, n_meas);
+            const uint32_t thr = p.p1_thr[core];
+            const uint32_t bit = (thr == INF32) || (r < thr);
+            const uint32_t tv = te + p.meas_latency;
+            if constexpr (XMEAS) {
+                if (n_meas < MEAS_LOOKUP) s_mt[n_meas < MT ? n_meas : 0][tid] = (tv << 1) | bit;
+            }
+            if (n_meas < p.meas_cap) {
+                if (p.meas) p.meas[(uint64_t)n_meas * n_lanes + lane] = make_uint2(tv, bit);
+            } else flags |= F_MEAS_OVF;
+            if (n_meas >= MEAS_LOOKUP) flags |= F_MEAS_OVF;
+            if (n_meas < 32 && bit) meas_bits |= 1u << n_meas;
+            last_bit = bit;
+            n_meas++;
+        }
+    };
+
+    auto emit_trace = [&](uint32_t tt, uint32_t addr, uint32_t val) {
+        if (n_tr < p.trace_cap) {
+            if (p.trace) p.trace[(uint64_t)n_tr * n_lanes + lane] = make_uint4(tt, addr, val, 0u);
+        } else if (p.trace_cap) flags |= F_TRACE_OVF;
+        n_tr++;
+    };
+
+    // latest measurement of group lane q with valid cycle <= d (slots sorted, INF = empty)
+    auto meas_lookup = [&](uint32_t q_tid, uint32_t d) -> uint32_t {
+        uint32_t res = 0;
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+            const uint32_t e = s_mt[m][q_tid];
+            if (e != INF32 && (e >> 1) <= d) res = e & 1u;
+        }
+        return res;
+    };
+
+    uint32_t iter = 0;
+    for (;;) {
+        if (!__any(mode != M_FIN)) break;
+        // internal-error guard: a correct run retires an instruction of >= 3 cycles
+        // in some lane of every live shot each iteration, so it never gets here
+        if (++iter > p.iter_guard) {
+            if (mode != M_FIN) { flags |= F_GUARD; finish(ST_DEADLOCK, t); }
+            break;
+        }
+
+        // ---------------- fetch + decode (RUN lanes) ----------------
+        bool run = (mode == M_RUN);
+        if (run && t > p.max_cycles) { finish(ST_MAX_CYCLES, t); run = false; }
+        uint4 w = make_uint4(0u, 0u, 0u, 0u);
+        if (run && ip < nprog) w = p.words[base + ip];
+        const uint32_t op4 = w.w >> 28;
+        const uint32_t alu = (w.w >> 24) & 7u;
+        const uint32_t in0_reg = (w.w >> 27) & 1u;
+        const uint32_t rs0 = (w.w >> 20) & 15u;
+        const uint32_t rs1 = (w.z >> 20) & 15u;
+        const uint32_t reg0 = s_regs[rs0][tid];
+        const uint32_t reg1 = s_regs[rs1][tid];
+        const uint32_t imm = (w.z >> 24) | (w.w << 8);
+        const uint32_t in0 = in0_reg ? reg0 : imm;
+        const uint32_t qD = (t < qa_t) ? 0u : qa_q + (t - qa_t);
+        const bool is_fproc = run && (op4 == 4u || op4 == 5u);
+
+        // ---------------- cross-core phase (converged) ----------------
+        uint32_t gmin = INF32;
+        bool any_run_grp = true;
+        bool released = false;
+        if constexpr (SYNC || XMEAS) {
+            if constexpr (SYNC) {
+                // barrier: complete when every participant is in SYNC_WAIT
+                const uint32_t key = is_part ? ((mode == M_SYNC) ? wait_d : (mode == M_RUN) ? t
+                                             : (mode == M_LUT) ? wait_d + 5u : INF32) : 0u;
+                const uint32_t maxkey = group_reduce<1>(key, C);
+                const uint64_t b = __ballot(is_part && mode == M_SYNC);
+                const uint64_t pm = __ballot(is_part);
+                const bool all_arrived = group_bits(b, wl, C) == group_bits(pm, wl, C) &&
+                                         group_bits(pm, wl, C) != 0ull;
+                if (mode == M_SYNC && is_part && all_arrived) {
+                    const uint32_t S = maxkey + p.sync_latency;
+                    if (S > p.max_cycles) finish(ST_MAX_CYCLES, wait_d);
+                    else {
+                        qa_t = S + 2u; qa_q = 0u;
+                        emit_trace(S + 2u, TRACE_QCLK_RST, 0u);
+                        ip = (ip + 1u) & 0xFFFFu;
+                        t = S + 3u;
+                        mode = M_RUN;
+                    }
+                    released = true;
+                }
+                // strobe bound of a waiting participant
+                uint32_t bound = INF32;
+                if (mode == M_RUN) bound = t + 2u;
+                else if (mode == M_LUT) bound = wait_d + 7u;
+                else if (mode == M_SYNC && is_part && maxkey != INF32)
+                    bound = maxkey + p.sync_latency + 5u;
+                gmin = group_reduce<0>(bound, C);
+            } else {
+                const uint32_t bound = (mode == M_RUN) ? t + 2u : (mode == M_LUT) ? wait_d + 7u : INF32;
+                gmin = group_reduce<0>(bound, C);
+            }
+            if constexpr (LUT) any_run_grp = group_bits(__ballot(mode == M_RUN), wl, C) != 0ull;
+        }
+
+        // ---------------- execute ----------------
+        bool executed = false;
+        if (run) {
+            bool stall = false;
+            if constexpr (FPROC) {
+                // fproc_meas read at D = t needs every meas_valid <= D known
+                if (is_fproc && p.fproc_mode == 0u) {
+                    const uint64_t h = (uint64_t)gmin + p.meas_latency;
+                    stall = !(h > (uint64_t)t);
+                }
+            }
+            if (!stall) {
+                executed = true;
+                n_exec++;
+                const uint32_t D = t;
+                switch (op4) {
+                case 0x0: case 0xA:
+                    finish(ST_DONE, D);
+                    break;
+                case 0xD: case 0xE: case 0xF:
+                    finish(ST_HUNG_OPCODE, D);
+                    break;
+                case 0xB:
+                    emit_event(D, 1u);
+                    ip = (ip + 1u) & 0xFFFFu; t = D + 3u;
+                    break;
+                case 0x8: case 0x9: case 0xC: {
+                    bool go = true;
+                    uint32_t tT = D;
+                    bool dbl = false;
+                    if (op4 != 0x8) {
+                        const uint32_t T = (w.x >> 5) | (w.y << 27);
+                        uint64_t wait;
+                        if (D < qa_t) { dbl = (T == 0u); wait = dbl ? 0ull : (uint64_t)(qa_t - D) + (uint32_t)(T - qa_q); }
+                        else wait = (uint32_t)(T - qD);
+                        if (wait >= 0x80000000ull) flags |= F_LATE;
+                        if (wait > (uint64_t)(p.max_cycles - D)) { finish(ST_MAX_CYCLES, D); go = false; }
+                        else tT = D + (uint32_t)wait;
+                    }
+                    if (go && op4 != 0xC) {
+                        // pulse_reg.sv:59-97
+                        const uint32_t env_i = ((w.z >> 26) | (w.w << 6)) & 0xFFFFFFu;
+                        const uint32_t ph_i = (w.z >> 7) & 0x1FFFFu;
+                        const uint32_t fr_i = ((w.y >> 28) | (w.z << 4)) & 0x1FFu;
+                        const uint32_t amp_i = (w.y >> 10) & 0xFFFFu;
+                        const uint32_t cfg_i = (w.y >> 5) & 0xFu;
+                        if ((w.w >> 19) & 1u) pe = (pe & 0xFF000000u) | (((w.w >> 18) & 1u) ? (reg0 & 0xFFFFFFu) : env_i);
+                        if ((w.z >> 25) & 1u) pp = (pp & 0xFFFE0000u) | (((w.z >> 24) & 1u) ? (reg0 & 0x1FFFFu) : ph_i);
+                        if ((w.z >> 6) & 1u) pp = (pp & 0x1FFFFu) | ((((w.z >> 5) & 1u) ? (reg0 & 0x1FFu) : fr_i) << 17);
+                        if ((w.y >> 27) & 1u) pa = ((w.y >> 26) & 1u) ? (reg0 & 0xFFFFu) : amp_i;
+                        if ((w.y >> 9) & 1u) pe = (pe & 0xFFFFFFu) | (cfg_i << 24);
+                    }
+                    if (go) {
+                        if (op4 == 0x9) {
+                            emit_event(tT + 2u, 0u);
+                            if (dbl) { emit_event(tT + 3u, 0u); flags |= F_DOUBLE_STROBE; }
+                        }
+                        ip = (ip + 1u) & 0xFFFFu;
+                        t = tT + 3u;
+                    }
+                    break;
+                }
+                case 0x1: {
+                    const uint32_t out = alu_op(alu, in0, reg1);
+                    const uint32_t rd = (w.z >> 16) & 15u;
+                    s_regs[rd][tid] = out;
+                    emit_trace(D + 3u, rd, out);
+                    ip = (ip + 1u) & 0xFFFFu; t = D + 4u;
+                    break;
+                }
+                case 0x2:
+                    ip = (w.z >> 4) & 0xFFFFu; t = D + 4u;
+                    break;
+                case 0x3: {
+                    const uint32_t out = alu_op(alu, in0, reg1);
+                    ip = (out & 1u) ? ((w.z >> 4) & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                    t = D + 6u;
+                    break;
+                }
+                case 0x6: {
+                    const uint32_t out = alu_op(alu, in0, qD);
+                    qa_t = D + 3u; qa_q = out + 3u;
+                    emit_trace(D + 3u, TRACE_QCLK_LOAD, out + 3u);
+                    ip = (ip + 1u) & 0xFFFFu; t = D + 4u;
+                    break;
+                }
+                case 0x7:
+                    if constexpr (SYNC) { mode = M_SYNC; wait_d = D; }
+                    else { finish(ST_DEADLOCK, D); }   // not reached: host selects SYNC kernels
+                    break;
+                case 0x4: case 0x5: {
+                    const uint32_t id = (w.y >> 20) & 0xFFu;
+                    bool have = false;
+                    uint32_t R = 0, data = 0;
+                    if constexpr (XMEAS) {
+                        if (p.fproc_mode == 0u) {
+                            R = D + 2u;
+                            data = meas_lookup(leader_tid + (id & (C - 1)), D);
+                            have = true;
+                        } else if (id == 0u) {
+                            // core_state_mgr WAIT_MEAS: first own meas_valid at >= D + 1
+#pragma unroll
+                            for (int m = MT - 1; m >= 0; m--) {
+                                const uint32_t e = s_mt[m][tid];
+                                if (e != INF32 && (e >> 1) >= D + 1u) { R = e >> 1; data = e & 1u; have = true; }
+                            }
+                            if (!have) { finish(ST_DEADLOCK, D); }
+                        } else {
+                            mode = M_LUT; wait_d = D;
+                        }
+                    } else {
+                        finish(ST_DEADLOCK, D);          // not reached: host selects FPROC kernels
+                    }
+                    if (have) {
+                        if (R > p.max_cycles) finish(ST_MAX_CYCLES, D);
+                        else {
+                            const uint32_t out = alu_op(alu, in0, data);
+                            if (op4 == 4u) {
+                                const uint32_t rd = (w.z >> 16) & 15u;
+                                s_regs[rd][tid] = out;
+                                emit_trace(R + 3u, rd, out);
+                                ip = (ip + 1u) & 0xFFFFu; t = R + 4u;
+                            } else {
+                                ip = (out & 1u) ? ((w.z >> 4) & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                                t = R + 6u;
+                            }
+                        }
+                    }
+                    break;
+                }
+                default:
+                    break;
+                }
+            }
+        }
+
+        // ---------------- meas_lut (per shot, by the shot's leader lane) ----------------
+        if constexpr (LUT) {
+            wave_fence();
+            bool fired = false;
+            if (tid == leader_tid && valid) {
+                uint32_t H = INF32;
+                if (any_run_grp && gmin != INF32) {
+                    const uint64_t h = (uint64_t)gmin + p.meas_latency - 1u;
+                    H = h > INF32 ? INF32 : (uint32_t)h;
+                }
+                const bool stop_at_fire = !any_run_grp;
+                for (;;) {
+                    uint32_t tmin = INF32;
+                    for (uint32_t c = 0; c < C; c++) {
+                        const uint32_t cur = s_cur[leader_tid + c];
+                        if (cur < (uint32_t)MT) {
+                            const uint32_t e = s_mt[cur < (uint32_t)MT ? cur : 0][leader_tid + c];
+                            if (e != INF32 && (e >> 1) < tmin) tmin = e >> 1;
+                        }
+                    }
+                    if (tmin == INF32 || tmin > H) break;
+                    uint64_t v = 0, mv = 0;
+                    for (uint32_t c = 0; c < C; c++) {
+                        const uint32_t cur = s_cur[leader_tid + c];
+                        if (cur < (uint32_t)MT) {
+                            const uint32_t e = s_mt[cur < (uint32_t)MT ? cur : 0][leader_tid + c];
+                            if (e != INF32 && (e >> 1) == tmin) {
+                                v |= 1ull << c;
+                                if (e & 1u) mv |= 1ull << c;
+                                s_cur[leader_tid + c] = cur + 1u;
+                            }
+                        }
+                    }
+                    // meas_lut.sv:40-56: LUT_READY the cycle after a fire ignores inputs
+                    if (lut_last_fire != INF32 && tmin == lut_last_fire + 1u) continue;
+                    const uint64_t nv = lut_valid | v, na = lut_addr | (v & mv);
+                    if (((uint64_t)p.lut_mask & nv) == (uint64_t)p.lut_mask) {
+                        lut_last_fire = tmin;
+                        if (nfire < (uint32_t)NF) {
+                            s_fire_t[nfire < (uint32_t)NF ? nfire : 0][tid] = tmin;
+                            s_fire_o[nfire < (uint32_t)NF ? nfire : 0][tid] = p.lut_table[na & 0xFFu];
+                        }
+                        nfire++;
+                        lut_valid = 0; lut_addr = 0;
+                        fired = true;
+                        if (stop_at_fire) break;
+                    } else { lut_valid = nv; lut_addr = na; }
+                }
+            }
+            // publish the leader's fire count to the group
+            const uint32_t nf_grp = (uint32_t)__shfl((int)nfire, (int)(wl & ~(C - 1)), 64);
+            const bool grp_fired = group_bits(__ballot(fired), wl, C) != 0ull;
+            wave_fence();
+            if (mode == M_LUT) {
+                const uint32_t n = nf_grp < (uint32_t)NF ? nf_grp : (uint32_t)NF;
+                for (uint32_t k = 0; k < n; k++) {
+                    const uint32_t tf = s_fire_t[k][leader_tid];
+                    if (tf >= wait_d + 1u) {
+                        const uint64_t out_bits = s_fire_o[k][leader_tid];
+                        const uint4 w2 = p.words[base + ip];     // the waiting fproc instruction
+                        const uint32_t op4b = w2.w >> 28, alub = (w2.w >> 24) & 7u;
+                        const uint32_t in0b = ((w2.w >> 27) & 1u) ? s_regs[(w2.w >> 20) & 15u][tid]
+                                                                  : ((w2.z >> 24) | (w2.w << 8));
+                        if (tf > p.max_cycles) { finish(ST_MAX_CYCLES, wait_d); }
+                        else {
+                            const uint32_t out = alu_op(alub, in0b, (uint32_t)((out_bits >> core) & 1ull));
+                            if (op4b == 4u) {
+                                const uint32_t rd = (w2.z >> 16) & 15u;
+                                s_regs[rd][tid] = out;
+                                emit_trace(tf + 3u, rd, out);
+                                ip = (ip + 1u) & 0xFFFFu; t = tf + 4u;
+                            } else {
+                                ip = (out & 1u) ? ((w2.z >> 4) & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                                t = tf + 6u;
+                            }
+                            mode = M_RUN;
+                        }
+                        released = true;
+                        break;
+                    }
+                }
+            }
+            if (grp_fired) released = released || (tid == leader_tid);
+        }
+
+        // ---------------- deadlock: a shot with no progress can never progress ----------------
+        if constexpr (SYNC || LUT) {
+            const uint64_t prog = __ballot(executed || released);
+            if (group_bits(prog, wl, C) == 0ull && (mode == M_SYNC || mode == M_LUT))
+                finish(ST_DEADLOCK, wait_d);
+        }
+        if constexpr (FPROC || XMEAS) wave_fence();
+    }
+
+    if (!valid) return;
+    if (p.summary) {
+        uint4 *s = reinterpret_cast<uint4 *>(p.summary + 8ull * lane);
+        s[0] = make_uint4(t_end, (ip_end & 0xFFFFu) | ((status & 0xFFu) << 16) | ((flags & 0xFFu) << 24),
+                          n_ev, n_exec);
+        s[1] = make_uint4(qclk_end, n_meas, meas_bits, n_tr);
+    }
+    if (p.regs_out) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = s_regs[r][tid];
+    }
+    if (p.hist) {
+        const uint64_t key = group_bits(__ballot(last_bit != 0u), wl, C);
+        if (core == 0u) atomicAdd(&p.hist[(uint64_t)grp * (1ull << C) + key], 1ull);
+    }
+}
+
+#define INSTANTIATE(F) template __global__ void interp_kernel<F>(const KParams p);
+INSTANTIATE(0)
+INSTANTIATE(FEAT_FPROC)
+INSTANTIATE(FEAT_SYNC)
+INSTANTIATE(FEAT_FPROC | FEAT_SYNC)
+INSTANTIATE(FEAT_LUT)
+INSTANTIATE(FEAT_LUT | FEAT_SYNC)
+
+hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream)
+{
+    const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
+    if (blocks == 0) return hipSuccess;
+    switch (feat) {
+    case 0: hipLaunchKernelGGL(interp_kernel<0>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    case FEAT_FPROC: hipLaunchKernelGGL(interp_kernel<FEAT_FPROC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    case FEAT_SYNC: hipLaunchKernelGGL(interp_kernel<FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    case FEAT_FPROC | FEAT_SYNC:
+        hipLaunchKernelGGL(interp_kernel<FEAT_FPROC | FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    case FEAT_LUT: hipLaunchKernelGGL(interp_kernel<FEAT_LUT>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    case FEAT_LUT | FEAT_SYNC:
+        hipLaunchKernelGGL(interp_kernel<FEAT_LUT | FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace dpemu

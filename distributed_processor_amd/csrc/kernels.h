@@ -1,0 +1,68 @@
+// kernels.h -- device-side parameter blocks and launchers of libdpemu.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dpemu.h"
+
+namespace dpemu {
+
+constexpr uint32_t BLOCK = 256;                 // 4 wavefronts per workgroup
+constexpr uint32_t MEAS_LOOKUP = DPEMU_MEAS_LOOKUP;
+constexpr uint32_t LUT_FIRE_CAP = DPEMU_LUT_FIRE_CAP;
+
+// kernel specialisations, chosen per run from the opcodes the programs use
+constexpr int FEAT_FPROC = 1;   // fproc_meas reads (ALU_FPROC / JUMP_FPROC)
+constexpr int FEAT_SYNC = 2;    // SYNC barriers
+constexpr int FEAT_LUT = 4;     // fproc_lut back end
+
+constexpr uint32_t ST_DONE = DPEMU_ST_DONE, ST_MAX_CYCLES = DPEMU_ST_MAX_CYCLES;
+constexpr uint32_t ST_HUNG_OPCODE = DPEMU_ST_HUNG_OPCODE, ST_DEADLOCK = DPEMU_ST_DEADLOCK;
+constexpr uint32_t F_LATE = DPEMU_F_LATE, F_EVENT_OVF = DPEMU_F_EVENT_OVF;
+constexpr uint32_t F_TRACE_OVF = DPEMU_F_TRACE_OVF, F_MEAS_OVF = DPEMU_F_MEAS_OVF;
+constexpr uint32_t F_DOUBLE_STROBE = DPEMU_F_DOUBLE_STROBE, F_GUARD = DPEMU_F_GUARD;
+constexpr uint32_t TRACE_QCLK_LOAD = DPEMU_TRACE_QCLK_LOAD, TRACE_QCLK_RST = DPEMU_TRACE_QCLK_RST;
+
+struct KParams {
+    // programs
+    const uint4 *words;
+    const uint32_t *offsets, *n_instr, *prog_table;
+    const uint32_t *p1_thr;
+    const uint64_t *lut_table;
+    // outputs (device, nullable)
+    uint32_t *summary;
+    uint4 *ev_main;
+    uint16_t *ev_amp;
+    uint4 *trace;
+    uint2 *meas;
+    uint32_t *regs_out;
+    unsigned long long *hist;
+    // run
+    uint64_t shot_begin;
+    uint32_t n_lanes, C, log2C, n_groups, shots_per_group;
+    uint32_t max_cycles, event_cap, trace_cap, meas_cap;
+    uint32_t fproc_mode, meas_elem, meas_latency, sync_latency;
+    uint64_t sync_mask, seed;
+    uint32_t lut_mask;
+    uint32_t iter_guard;
+};
+
+hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
+
+// ---- DDS ------------------------------------------------------------------
+struct DDSParams {
+    const uint32_t *summary;
+    const uint4 *ev_main;
+    const uint16_t *ev_amp;
+    const uint32_t *env, *freq;
+    const int16_t *sin_lut;
+    const uint32_t *ch;            // per-channel descriptors, DDS_CH_WORDS u32 each
+    uint32_t *iq;                  // [n_channels][n_samples] packed {I16 low, Q16 high}
+    uint32_t n_channels, n_lanes, n_samples, event_cap;
+};
+constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
+
+hipError_t launch_dds(const DDSParams &p, hipStream_t stream);
+
+}  // namespace dpemu

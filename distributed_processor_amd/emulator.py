@@ -1,0 +1,232 @@
+"""Host front end: run assembled distproc programs on the MI355X emulator.
+
+Drop-in for the reference simulation path: where the reference loads one
+``cmd_buf`` into a Verilator ``toplevel_sim`` and clocks it from cocotb
+(cocotb/proc/test_proc.py:29-38, sim_modules/toplevel_sim.sv:13-33), here the
+output of ``GlobalAssembler.get_assembled_program()`` (assembler.py:623-641)
+-- ``{core_ind: {'cmd_buf': bytes, 'env_buffers': [...], 'freq_buffers': [...]}}``
+-- or raw command words go to :class:`Emulator`, which runs n_shots x C
+cores on the GPU through libdpemu.so and returns pulse events, register
+traces, measurements and outcome histograms.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Iterable, List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import _abi, isa
+from ._native import DpemuError, check, load_library
+
+ProgramLike = Union[bytes, Sequence[int], np.ndarray]
+
+
+def _to_u32(prog: ProgramLike) -> np.ndarray:
+    if isinstance(prog, (bytes, bytearray)):
+        return isa.cmd_buf_to_u32(bytes(prog))
+    if isinstance(prog, np.ndarray) and prog.dtype == np.uint32:
+        return np.ascontiguousarray(prog.reshape(-1, 4))
+    return isa.words_to_u32([int(w) for w in prog])
+
+
+def _next_pow2(n: int) -> int:
+    c = 1
+    while c < n:
+        c <<= 1
+    return c
+
+
+def _shot_programs(shot) -> Dict[int, np.ndarray]:
+    """one shot's programs: assembler dict {core: {'cmd_buf': ...}}, dict
+    {core: words}, or a list (index = core)."""
+    if isinstance(shot, dict):
+        out = {}
+        for k, v in shot.items():
+            if isinstance(v, dict):
+                v = v['cmd_buf']
+            out[int(k)] = _to_u32(v)
+        return out
+    return {c: _to_u32(p) for c, p in enumerate(shot)}
+
+
+class ProgramSet:
+    """cmd_mem images for every (group, core), packed for the device.
+
+    groups: list of shots' programs (see ``_shot_programs``); group g runs for
+    shots with (shot // shots_per_group) % n_groups == g.  Identical programs
+    are stored once.
+    """
+
+    def __init__(self, groups: Sequence, cores_per_shot: Optional[int] = None):
+        if isinstance(groups, dict):
+            groups = [groups]
+        per_group = [_shot_programs(g) for g in groups]
+        if not per_group:
+            raise ValueError('no programs')
+        ncore = max((max(g) + 1 if g else 1) for g in per_group)
+        C_ = cores_per_shot or _next_pow2(ncore)
+        if C_ < ncore or C_ & (C_ - 1) or C_ > _abi.MAX_CORES:
+            raise ValueError('cores_per_shot must be a power of two >= {}'.format(ncore))
+        uniq: Dict[bytes, int] = {}
+        blobs: List[np.ndarray] = []
+        table = np.zeros(len(per_group) * C_, np.uint32)
+        empty = np.zeros((0, 4), np.uint32)
+        for g, progs in enumerate(per_group):
+            for c in range(C_):
+                p = progs.get(c, empty)
+                key = p.tobytes()
+                if key not in uniq:
+                    uniq[key] = len(blobs)
+                    blobs.append(p)
+                table[g * C_ + c] = uniq[key]
+        self.cores_per_shot = C_
+        self.n_groups = len(per_group)
+        self.n_instr = np.array([len(b) for b in blobs], np.uint32)
+        self.offsets = np.concatenate([[0], np.cumsum(self.n_instr)[:-1]]).astype(np.uint32)
+        self.words = (np.concatenate(blobs) if sum(self.n_instr) else np.zeros((1, 4), np.uint32)).astype(np.uint32)
+        self.words = np.ascontiguousarray(self.words)
+        self.table = table
+
+    @property
+    def n_programs(self):
+        return len(self.n_instr)
+
+
+class EmulationResult:
+    """Host copies of a run's outputs (layouts as in include/dpemu.h)."""
+
+    def __init__(self, cfg, n_shots, shot_begin, arrays):
+        self.cfg = cfg
+        self.n_shots = n_shots
+        self.shot_begin = shot_begin
+        self.arrays = arrays
+        self.summary = _abi.unpack_summary(arrays['summary'])
+
+    @property
+    def n_lanes(self):
+        return self.n_shots * self.cfg.cores_per_shot
+
+    def lane(self, shot, core):
+        return (shot - self.shot_begin) * self.cfg.cores_per_shot + core
+
+    def events(self, shot, core) -> np.ndarray:
+        """structured events of one lane: t, qclk, env_word, cfg, kind, phase, freq, amp"""
+        L = self.lane(shot, core)
+        n = min(int(self.summary['n_events'][L]), self.cfg.event_cap)
+        ev = self.arrays['ev_main'][:n, L]
+        amp = self.arrays['ev_amp'][:n, L] if 'ev_amp' in self.arrays else np.zeros(n, np.uint16)
+        out = np.zeros(n, dtype=[('t', 'u4'), ('qclk', 'u4'), ('env_word', 'u4'), ('cfg', 'u1'),
+                                 ('kind', 'u1'), ('phase', 'u4'), ('freq', 'u2'), ('amp', 'u2')])
+        out['t'], out['qclk'] = ev[:, 0], ev[:, 1]
+        out['env_word'] = ev[:, 2] & 0xFFFFFF
+        out['cfg'] = (ev[:, 2] >> 24) & 0xF
+        out['kind'] = ev[:, 2] >> 28
+        out['phase'] = ev[:, 3] & 0x1FFFF
+        out['freq'] = ev[:, 3] >> 17
+        out['amp'] = amp
+        return out
+
+    def status_counts(self):
+        st, n = np.unique(self.summary['status'], return_counts=True)
+        return {_abi.STATUS_NAMES.get(int(s), str(s)): int(c) for s, c in zip(st, n)}
+
+    @property
+    def histogram(self):
+        return self.arrays.get('hist')
+
+
+class Emulator:
+    """One context per GPU (one process per device)."""
+
+    def __init__(self, device: int = 0):
+        self._L = load_library()
+        h = C.c_void_p()
+        rc = self._L.dpemu_create(int(device), C.byref(h))
+        if rc != 0:
+            raise DpemuError('dpemu_create(device={}) failed ({}): no usable HIP device'.format(device, rc))
+        self._h = h
+        self.device = device
+        self.programs: Optional[ProgramSet] = None
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.dpemu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -------------------------------------------------------------- programs
+    def load(self, programs, cores_per_shot: Optional[int] = None) -> ProgramSet:
+        ps = programs if isinstance(programs, ProgramSet) else ProgramSet(programs, cores_per_shot)
+        rc = self._L.dpemu_load_programs(self._h, ps.words.ctypes.data, ps.offsets.ctypes.data,
+                                         ps.n_instr.ctypes.data, ps.n_programs, ps.table.ctypes.data,
+                                         ps.n_groups, ps.cores_per_shot)
+        check(self._h, rc, 'dpemu_load_programs')
+        self.programs = ps
+        return ps
+
+    def config(self, **kw) -> _abi.Config:
+        if self.programs is None:
+            raise DpemuError('load() programs first')
+        kw.setdefault('n_groups', self.programs.n_groups)
+        return _abi.make_config(self.programs.cores_per_shot, **kw)
+
+    # -------------------------------------------------------------- running
+    def run(self, n_shots: int, shot_begin: int = 0, cfg: Optional[_abi.Config] = None,
+            outputs: Iterable[str] = ('summary', 'ev_main', 'ev_amp', 'meas', 'hist'),
+            **cfg_kw) -> EmulationResult:
+        """Emulate shots [shot_begin, shot_begin + n_shots); results copied to host."""
+        cfg = cfg or self.config(**cfg_kw)
+        want = set(outputs) | {'summary'}
+        arrays = _abi.alloc_host_outputs(cfg, n_shots, want)
+        o = _abi.outputs_struct(arrays)
+        rc = self._L.dpemu_run_host(self._h, C.addressof(cfg), int(shot_begin), int(n_shots), C.addressof(o))
+        check(self._h, rc, 'dpemu_run_host')
+        return EmulationResult(cfg, n_shots, shot_begin, arrays)
+
+    def run_device(self, cfg: _abi.Config, n_shots: int, shot_begin: int, outputs: dict,
+                   stream=None):
+        """Asynchronous run into caller-owned device buffers (e.g. torch tensors:
+        pass {name: tensor}); stream: torch.cuda.Stream / raw handle / None."""
+        o = _abi.Outputs()
+        for name, _ in _abi.Outputs._fields_:
+            t = outputs.get(name)
+            setattr(o, name, None if t is None else (t.data_ptr() if hasattr(t, 'data_ptr') else int(t)))
+        s = getattr(stream, 'cuda_stream', stream)
+        rc = self._L.dpemu_run(self._h, C.addressof(cfg), int(shot_begin), int(n_shots), C.addressof(o),
+                               C.c_void_p(s) if s else None)
+        check(self._h, rc, 'dpemu_run')
+
+
+def alloc_device_outputs(cfg: _abi.Config, n_shots: int, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'),
+                         device='cuda'):
+    """torch device tensors laid out as dpemu_outputs."""
+    import torch
+    n_lanes = int(n_shots) * cfg.cores_per_shot
+    shapes = {'summary': ((n_lanes, 8), torch.int32), 'ev_main': ((cfg.event_cap, n_lanes, 4), torch.int32),
+              'ev_amp': ((cfg.event_cap, n_lanes), torch.int16),
+              'trace': ((cfg.trace_cap, n_lanes, 4), torch.int32),
+              'meas': ((cfg.meas_cap, n_lanes, 2), torch.int32), 'regs': ((16, n_lanes), torch.int32),
+              'hist': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64)}
+    out = {}
+    for k in want:
+        shp, dt = shapes[k]
+        if k == 'hist':
+            if cfg.cores_per_shot > 12:
+                continue
+            out[k] = torch.zeros(shp, dtype=dt, device=device)
+        elif 0 not in shp:
+            out[k] = torch.empty(shp, dtype=dt, device=device)
+    return out

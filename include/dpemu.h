@@ -57,6 +57,7 @@ extern "C" {
 #define DPEMU_F_MEAS_OVF      0x08 /* more measurements than meas_cap                       */
 #define DPEMU_F_DOUBLE_STROBE 0x10 /* trig at the first decode with cmd_time 0: the reset
                                       hold keeps qclk at 0 two cycles -> two cstrobes      */
+#define DPEMU_F_GUARD         0x20 /* internal error: interpreter iteration guard tripped    */
 
 /* ---- fproc back ends --------------------------------------------------*/
 #define DPEMU_FPROC_MEAS 0        /* hdl/fproc_meas.sv: latest stored bit, ready at D+2   */
@@ -71,6 +72,9 @@ extern "C" {
 #define DPEMU_TRACE_QCLK_RST  17  /* SYNC reset qclk (value 0 at t)                       */
 
 #define DPEMU_MAX_CORES 64
+#define DPEMU_MEAS_LOOKUP 16      /* a core's first 16 measurements are visible to fproc;
+                                     later ones set DPEMU_F_MEAS_OVF and are invisible  */
+#define DPEMU_LUT_FIRE_CAP 16     /* meas_lut fires recorded per shot (later fires lost) */
 
 /*
  * Timebase: cycle t = 0 is the first DECODE after reset.  qclk(0) = qclk(1) = 0

@@ -31,7 +31,8 @@
 #include <omp.h>
 #endif
 
-#define MEAS_LOOKUP 16          /* DPEMU_MEAS_LOOKUP: measurements visible to fproc */
+#define MEAS_LOOKUP DPEMU_MEAS_LOOKUP   /* measurements per core visible to fproc */
+#define LUT_FIRE_CAP DPEMU_LUT_FIRE_CAP /* meas_lut fires recorded per shot */
 #define INF32 0xFFFFFFFFu
 
 enum { M_RUN = 0, M_SYNC = 1, M_LUT = 2, M_FIN = 3 };
@@ -62,7 +63,7 @@ typedef struct {
     uint32_t lut_done_until;         /* events with valid <= this applied */
     int lut_any;
     uint32_t lut_cursor[DPEMU_MAX_CORES];
-    uint32_t nfire; uint32_t fire_t[256]; uint64_t fire_out[256];
+    uint32_t nfire; uint32_t fire_t[LUT_FIRE_CAP]; uint64_t fire_out[LUT_FIRE_CAP];
     flane L[DPEMU_MAX_CORES];
 } fshot;
 
@@ -200,7 +201,8 @@ static void lut_apply_cycle(fshot *s, uint32_t tv, uint64_t valid, uint64_t meas
     uint64_t v = s->lut_valid | valid, a = s->lut_addr | (valid & meas);
     if ((cfg->lut_mask & v) == cfg->lut_mask) {
         s->lut_last_fire = tv; s->lut_ready_next = 1;
-        if (s->nfire < 256) { s->fire_t[s->nfire] = tv; s->fire_out[s->nfire] = cfg->lut_table[a & 0xFF]; s->nfire++; }
+        if (s->nfire < LUT_FIRE_CAP) { s->fire_t[s->nfire] = tv; s->fire_out[s->nfire] = cfg->lut_table[a & 0xFF]; }
+        s->nfire++;
         s->lut_valid = 0; s->lut_addr = 0;
     } else { s->lut_valid = v; s->lut_addr = a; }
 }
@@ -262,7 +264,7 @@ static int lut_resolve(fshot *s)
     for (uint32_t c = 0; c < s->C; c++) {
         flane *l = &s->L[c];
         if (l->mode != M_LUT) continue;
-        for (uint32_t k = 0; k < s->nfire; k++) {
+        for (uint32_t k = 0; k < s->nfire && k < LUT_FIRE_CAP; k++) {
             if (s->fire_t[k] >= l->wait_d + 1) {
                 uint32_t R = s->fire_t[k];
                 if (R > s->cfg->max_cycles) { finish(l, DPEMU_ST_MAX_CYCLES, l->wait_d); }

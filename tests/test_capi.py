@@ -1,0 +1,65 @@
+"""The C-ABI library: builds, loads, exports every entry point of
+include/dpemu.h, and fails loudly (no CPU fallback) when no GPU is present.
+No compute call is made here."""
+
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from distributed_processor_amd import _abi, _native
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    with open(os.path.join(REPO, 'include', 'dpemu.h')) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r'\b(dpemu_[a-z_0-9]+)\s*\(', txt)))
+
+
+def test_header_symbols_exported():
+    names = header_functions()
+    assert set(names) == set(_native.EXPORTS)
+    L = _native.load_library()
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_abi_version_and_struct_sizes():
+    L = _native.load_library()
+    assert L.dpemu_abi_version() == _abi.ABI_VERSION
+    # dpemu_config: 12 u32 + 2 u64 + 2 u32 + 64 u32 + 256 u64
+    assert C.sizeof(_abi.Config) == 12 * 4 + 16 + 8 + 64 * 4 + 256 * 8
+    assert C.sizeof(_abi.Outputs) == 7 * 8
+
+
+def test_sin_lut_symmetry():
+    L = _native.load_library()
+    buf = (C.c_int16 * 4096)()
+    assert L.dpemu_dds_sin_lut(buf) == 0
+    v = list(buf)
+    assert v[0] == 0 and v[1024] == 32767 and v[2048] == 0 and v[3072] == -32767
+    for i in range(1, 1024):
+        assert v[i] == v[2048 - i] == -v[2048 + i] == -v[4096 - i]
+
+
+def test_create_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from distributed_processor_amd.emulator import Emulator
+    with pytest.raises(_native.DpemuError):
+        Emulator(0)
+
+
+def test_config_validation():
+    with pytest.raises(ValueError):
+        _abi.make_config(3)
+    with pytest.raises(ValueError):
+        _abi.make_config(4, max_cycles=2 ** 31)
+    with pytest.raises(ValueError):
+        _abi.make_config(4, lut_mask=0)
+    cfg = _abi.make_config(8, p1=[0.0, 1.0, 0.5])
+    assert cfg.p1_threshold[0] == 0 and cfg.p1_threshold[1] == 0xFFFFFFFF and cfg.p1_threshold[2] == 2 ** 31

@@ -1,0 +1,168 @@
+"""HIP interpreter (libdpemu.so, through the C ABI) vs oracle_fast, bit for bit.
+
+oracle_fast is itself pinned to the per-clock RTL restatement
+(tests/test_fast_vs_rtl.py), which is pinned to the reference's cocotb
+known-answer tests (tests/test_rtl_kat.py).  Every output array -- lane
+summaries, events, amplitudes, register/qclk traces, measurements, final
+registers, histograms -- must be identical.  At full BASELINE sizes the
+checks are size-independent properties (sharding invariance, histogram
+totals, per-group determinism).
+"""
+
+import numpy as np
+import pytest
+
+import oracle
+from distributed_processor_amd import _abi, workloads
+from distributed_processor_amd.emulator import Emulator, ProgramSet
+from tests.progfuzz import pack_programs, random_case
+
+pytestmark = pytest.mark.gpu
+
+ALL_OUT = ('summary', 'ev_main', 'ev_amp', 'trace', 'meas', 'regs', 'hist')
+
+
+@pytest.fixture(scope='module')
+def emu():
+    e = Emulator(0)
+    yield e
+    e.close()
+
+
+def compare_all(gpu, ref, ctx=''):
+    for k in ALL_OUT:
+        if k in ref:
+            assert k in gpu, k
+            a, b = np.asarray(gpu[k]), np.asarray(ref[k])
+            if not np.array_equal(a, b):
+                bad = np.argwhere(a != b)
+                raise AssertionError('{} {}: {} mismatches, first at {}: gpu {} ref {}'.format(
+                    ctx, k, len(bad), bad[0].tolist(), a[tuple(bad[0])], b[tuple(bad[0])]))
+
+
+def run_pair(emu, ps, cfg, n_shots, shot0=0):
+    emu.load(ps)
+    g = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
+    f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n_shots, want=ALL_OUT)
+    return g.arrays, f
+
+
+@pytest.mark.parametrize('seed', range(40))
+def test_fuzz_gpu_vs_fast(emu, seed):
+    case = random_case(seed, ncores=[1, 2, 4, 8][seed % 4])
+    mode = _abi.FPROC_MEAS if case['mode'] == 'meas' else _abi.FPROC_LUT
+    C = case['ncores']
+    groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
+    ps = ProgramSet(groups, cores_per_shot=C)
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=6000, event_cap=64, trace_cap=64,
+                           meas_cap=16, fproc_mode=mode, meas_latency=1 + seed % 23,
+                           sync_latency=1 + seed % 3, sync_mask=(0b0111 if seed % 5 == 0 and C == 4 else 0),
+                           seed=seed)
+    n_shots = 333
+    g, f = run_pair(emu, ps, cfg, n_shots, shot0=seed * 1000)
+    compare_all(g, f, 'seed {}'.format(seed))
+
+
+@pytest.mark.parametrize('C', [1, 2, 4, 8, 16, 32, 64])
+def test_fuzz_all_group_sizes(emu, C):
+    case = random_case(500 + C, ncores=C, mode='meas', allow_late=True, allow_hang=True)
+    groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
+    ps = ProgramSet(groups, cores_per_shot=C)
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=5000, event_cap=48, trace_cap=48,
+                           meas_cap=16, meas_latency=7, seed=C)
+    g, f = run_pair(emu, ps, cfg, 4096 // C + 3)
+    if C > 12:
+        f.pop('hist', None)
+    compare_all(g, f, 'C={}'.format(C))
+
+
+def test_config1_golden_program(emu, golden_dir):
+    """the reference's own machine-code golden (test_linear_compile_globalasm core 0)"""
+    import json
+    import os
+    with open(os.path.join(golden_dir, 'cmd_buf_golden.json')) as fh:
+        gold = json.load(fh)
+    ps = ProgramSet([{0: bytes.fromhex(gold['cores']['0']['cmd_buf'])}])
+    cfg = _abi.make_config(1, max_cycles=10000, event_cap=8, trace_cap=8, meas_cap=4)
+    g, f = run_pair(emu, ps, cfg, 10000)
+    compare_all(g, f)
+    s = _abi.unpack_summary(g['summary'])
+    assert (s['status'] == _abi.ST_DONE).all()
+    assert (s['n_events'] == 4).all()            # pulse_reset + 3 strobes
+    ev = g['ev_main'][:, 0]
+    assert [int(e[0]) for e in ev[:4]] == [0, 8, 24, 324]     # reset @0; cstrobe at cmd_time + 3 (qclk = t - 1)
+    assert [int(e[1]) for e in ev[1:4]] == [7, 23, 323]       # qclk at cstrobe = cmd_time + 2
+
+
+def test_config1_dds_element(emu):
+    ps = ProgramSet(workloads.config1_linear())
+    cfg = _abi.make_config(1, max_cycles=10000, event_cap=8, trace_cap=8, meas_cap=4)
+    g, f = run_pair(emu, ps, cfg, 50000, shot0=123)
+    compare_all(g, f)
+
+
+def test_config2_ramsey(emu):
+    ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
+    cfg = _abi.make_config(8, n_groups=100, max_cycles=20000, event_cap=8, trace_cap=4, meas_cap=4)
+    g, f = run_pair(emu, ps, cfg, 3000)
+    compare_all(g, f)
+    assert (_abi.unpack_summary(g['summary'])['status'] == _abi.ST_DONE).all()
+
+
+def test_config3_active_reset(emu):
+    ps = ProgramSet(workloads.config3_active_reset(8))
+    cfg = _abi.make_config(8, max_cycles=50000, event_cap=16, trace_cap=16, meas_cap=4,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, p1=0.5)
+    g, f = run_pair(emu, ps, cfg, 4000, shot0=10 ** 9)
+    compare_all(g, f)
+    s = _abi.unpack_summary(g['summary'])
+    assert (s['status'] == _abi.ST_DONE).all()
+    # the conditional X180 ran exactly for first outcomes of 1
+    flip = (s['meas_bits'] & 1).astype(bool)
+    assert (s['n_events'][flip] == s['n_events'][~flip].min() + 2).all()
+    assert 0.45 < flip.mean() < 0.55
+
+
+def test_config4_rb(emu):
+    ps = ProgramSet(workloads.config4_rb(n_seq=24, depth=40))
+    cfg = _abi.make_config(2, n_groups=24, shots_per_group=5, max_cycles=200000, event_cap=160,
+                           trace_cap=256, meas_cap=4)
+    g, f = run_pair(emu, ps, cfg, 24 * 5)
+    compare_all(g, f)
+
+
+@pytest.mark.parametrize('mode', ['meas', 'lut'])
+def test_lut_and_meas_fuzz_many_shots(emu, mode):
+    for seed in range(6):
+        case = random_case(7000 + seed, ncores=4, mode=mode, allow_late=False, allow_hang=False)
+        groups = [[case['progs'][case['table'][g * 4 + c]] for c in range(4)] for g in range(case['n_groups'])]
+        ps = ProgramSet(groups, cores_per_shot=4)
+        cfg = _abi.make_config(4, n_groups=ps.n_groups, max_cycles=8000, event_cap=64, trace_cap=64,
+                               meas_cap=16, fproc_mode=_abi.FPROC_LUT if mode == 'lut' else _abi.FPROC_MEAS,
+                               meas_latency=3 + seed, seed=seed)
+        g, f = run_pair(emu, ps, cfg, 2048)
+        compare_all(g, f, 'seed {}'.format(seed))
+
+
+# ---------------------------------------------------------------- full-size properties
+def test_ramsey_full_size_sharding_invariant(emu):
+    """config 2 at 10^6 shots: per-shard results equal the single run (RNG keyed
+    by global shot index), histogram totals, and per-group determinism."""
+    ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
+    emu.load(ps)
+    cfg = _abi.make_config(8, n_groups=100, max_cycles=20000, event_cap=8, meas_cap=2)
+    N = 10 ** 6
+    full = emu.run(N, 0, cfg=cfg, outputs=('summary', 'hist'))
+    assert int(full.arrays['hist'].sum()) == N
+    assert (full.summary['status'] == _abi.ST_DONE).all()
+    half = [emu.run(N // 2, s, cfg=cfg, outputs=('summary', 'hist')) for s in (0, N // 2)]
+    assert np.array_equal(np.concatenate([h.arrays['summary'] for h in half]), full.arrays['summary'])
+    assert np.array_equal(half[0].arrays['hist'] + half[1].arrays['hist'], full.arrays['hist'])
+    t_end = full.summary['t_end'].reshape(N, 8)
+    grp = np.arange(N) % 100
+    for k in (0, 37, 99):
+        rows = t_end[grp == k]
+        assert (rows == rows[0]).all()
+    # P(1) = 0.5 per core: each histogram bin near uniform over 256 keys
+    h = full.arrays['hist'].sum(axis=0)
+    assert abs(h.mean() - N / 256) < 1e-9 and h.min() > 0.8 * N / 256
