@@ -8,6 +8,11 @@ timeline, lane summaries, measurement records and the outcome histogram to
 HBM; with N > 1 ranks the histograms are all-reduced over RCCL (the path's
 only exchange).  Shots shard by global index (weak scaling).
 
+DDS leg (config 5, reported under "dds" on the same line): the config-4 RB
+timelines (8 cores, depth 200) synthesised to int16 I/Q on 16 channels per
+sequence at 16 samples/clk; GSamples/s (whole job) and the DDS kernel's HBM
+write roofline.
+
 Metric: emulated core-shots/s (whole job).  Also reported: emulated qclk
 cycles/s and instructions/s, the interpreter's HBM roofline fraction, and
 the CPU baseline (oracle_fast, the event-driven C restatement, on the host
@@ -69,6 +74,103 @@ def cpu_baseline(ps, cfg, target_s=12.0):
                       'restatement, OpenMP) in {}-shot chunks, {:.1f} s'.format(done, cfg.cores_per_shot, chunk, dt)}
 
 
+def dds_workload(n_seq):
+    """config 5: the config-4 RB timelines (8 cores, depth 200) synthesised on
+    16 channels per sequence (8 cores x {qdrv, rdrv}) at 16 samples/clk"""
+    from distributed_processor_amd import workloads
+    from distributed_processor_amd.emulator import ProgramSet
+    return ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
+
+
+def dds_cpu_baseline(plan, host_ev, n_samples, target_s=8.0):
+    """oracle_dds (scalar C restatement, OpenMP over channels) on whole
+    channels of the same timelines until ~target_s of CPU work"""
+    import oracle
+    threads = min(len(os.sched_getaffinity(0)), 16)
+    per = max(threads, 16)
+    done = 0
+    t0 = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t0 < target_s and i < plan.n_channels:
+        d = plan.desc[i:i + per]
+        oracle.dds(d, host_ev['summary'], host_ev['ev_main'], host_ev['ev_amp'], plan.env, plan.freq,
+                   n_samples, plan.event_cap, threads)
+        done += len(d) * n_samples
+        i += per
+    dt = time.perf_counter() - t0
+    return {'value': done / dt / 1e9, 'unit': 'GSamples/s', 'cores': threads, 'kind': 'port',
+            'sample': '{} channels x {} samples of the config-5 timelines, oracle_dds (scalar C '
+                      'restatement, OpenMP over channels), {:.1f} s'.format(done // n_samples, n_samples, dt)}
+
+
+def dds_leg(emu, args, world, rank, stream):
+    """time K synthesis steps of config 5; returns the 'dds' sub-object"""
+    import torch
+    import torch.distributed as dist
+    from distributed_processor_amd import _abi, workloads
+    from distributed_processor_amd.dds import ChannelPlan
+    from distributed_processor_amd.emulator import alloc_device_outputs
+    ps = dds_workload(args.dds_seqs)
+    emu.load(ps)
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=512, meas_cap=4,
+                           meas_latency=64, seed=0x5EED)
+    n = args.dds_seqs
+    shot0 = rank * n
+    ev = alloc_device_outputs(cfg, n, want=('summary', 'ev_main', 'ev_amp'))
+    emu.run_device(cfg, n, shot0, ev, stream)
+    torch.cuda.synchronize()
+    summ = ev['summary'].cpu().numpy().view(np.uint32)
+    s = _abi.unpack_summary(summ)
+    assert (s['status'] == _abi.ST_DONE).all() and (s['n_events'] <= cfg.event_cap).all()
+    n_cyc = int(s['t_end'].max()) + 8
+    n_samples = (n_cyc * 16 + 3) // 4 * 4
+    params = {i: (e['samples_per_clk'], e['interp_ratio']) for i, e in enumerate(workloads.ELEMS)}
+    chans = [(shot0 + q, c, e) for q in range(n) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
+    plan = ChannelPlan(ps, cfg, shot0, n, chans, params)
+    iq = torch.empty((plan.n_channels, n_samples), dtype=torch.int32, device='cuda')
+    for _ in range(args.warmup):
+        emu.synthesize(plan, ev, n_samples, iq, stream)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        emu.synthesize(plan, ev, n_samples, iq, stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    samples = plan.n_channels * n_samples
+    gbs = samples * 4 / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, 'profiles', 'r01_dds_pmc.json')
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get('hbm_bytes_per_launch')
+    res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
+           'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s',
+           'ms_per_step': dt / args.steps * 1e3, 'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
+           'config': {'workload': 'config5_dds_rb8', 'sequences_per_gpu': n, 'channels_per_gpu': plan.n_channels,
+                      'samples_per_channel': n_samples, 'rb_depth': 200},
+           'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                        'frac': gbs / HBM_PEAK_GBS, 'traffic': traffic, 'bytes_per_launch': samples * 4,
+                        'kernel': 'dpemu::dds_kernel'}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        host_ev = {k: v.cpu().numpy() for k, v in ev.items()}
+        res['cpu_baseline'] = dds_cpu_baseline(plan, host_ev, n_samples, args.cpu_seconds * 2 / 3)
+    del iq
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -77,6 +179,11 @@ def main():
     ap.add_argument('--shots', type=int, default=10 ** 6, help='shots per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--spg', type=int, default=1,
+                    help='shots per delay point run back to back (1: delay k = shot mod 100)')
+    ap.add_argument('--exec-flags', type=int, default=0, help='DPEMU_X_* execution knobs')
+    ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
+    ap.add_argument('--no-dds', action='store_true')
     args = ap.parse_args()
 
     import torch
@@ -95,9 +202,11 @@ def main():
     ps = build_workload()
     emu = Emulator(local)
     emu.load(ps)
-    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, trace_cap=0,
-                           meas_cap=2, meas_latency=64, seed=0x5EED, p1=0.5)
     n = args.shots
+    spg = args.spg
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, shots_per_group=spg, max_cycles=1 << 20, event_cap=8,
+                           trace_cap=0, meas_cap=2, meas_latency=64, seed=0x5EED, p1=0.5,
+                           exec_flags=args.exec_flags)
     out = alloc_device_outputs(cfg, n, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'))
     stream = torch.cuda.current_stream()
     shot0 = rank * n
@@ -169,6 +278,7 @@ def main():
         'dtype': 'u32',
         'data': 'synthetic (assembled Ramsey programs, Philox outcomes p=0.5)',
         'config': {'workload': 'config2_ramsey_8core_100pt', 'shots_per_gpu': n, 'cores_per_shot': 8,
+                   'shots_per_delay_point': spg,
                    'global_shots_per_step': n * world, 'parallelism': 'shots sharded, {} GPU(s)'.format(world)},
         'shots_per_s': value / 8,
         'qclk_cycles_per_s': cycles * world * args.steps / dt,
@@ -181,6 +291,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline(ps, cfg, args.cpu_seconds)
+    if not args.no_dds:
+        result['dds'] = dds_leg(emu, args, world, rank, stream)
     if rank == 0:
         print(json.dumps(result), flush=True)
     emu.close()

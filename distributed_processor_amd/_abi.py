@@ -14,6 +14,10 @@ FPROC_MEAS, FPROC_LUT = 0, 1
 EV_STROBE, EV_PULSE_RESET = 0, 1
 TRACE_QCLK_LOAD, TRACE_QCLK_RST = 16, 17
 MAX_CYCLES_LIMIT = 2 ** 31 - 64
+X_PROG_LDS = 0x1
+X_GROUP_MAJOR = 0x2
+X_HIST_DIRECT = 0x4
+X_HIST_REPL = 0x8
 
 STATUS_NAMES = {0: 'running', ST_DONE: 'done', ST_MAX_CYCLES: 'max_cycles',
                 ST_HUNG_OPCODE: 'hung_opcode', ST_DEADLOCK: 'deadlock'}
@@ -24,7 +28,7 @@ class Config(C.Structure):
                 ('shots_per_group', C.c_uint32), ('max_cycles', C.c_uint32),
                 ('event_cap', C.c_uint32), ('trace_cap', C.c_uint32), ('meas_cap', C.c_uint32),
                 ('fproc_mode', C.c_uint32), ('meas_elem', C.c_uint32), ('meas_latency', C.c_uint32),
-                ('sync_latency', C.c_uint32), ('reserved0', C.c_uint32),
+                ('sync_latency', C.c_uint32), ('exec_flags', C.c_uint32),
                 ('sync_mask', C.c_uint64), ('seed', C.c_uint64),
                 ('lut_mask', C.c_uint32), ('reserved1', C.c_uint32),
                 ('p1_threshold', C.c_uint32 * MAX_CORES), ('lut_table', C.c_uint64 * 256)]
@@ -38,7 +42,7 @@ class Outputs(C.Structure):
 
 class DDSChannels(C.Structure):
     _fields_ = [('n_channels', C.c_uint32), ('n_lanes', C.c_uint32), ('n_samples', C.c_uint32),
-                ('reserved', C.c_uint32)] + [(n, C.c_void_p) for n in (
+                ('event_cap', C.c_uint32)] + [(n, C.c_void_p) for n in (
                     'ch_lane', 'ch_elem', 'spc', 'interp', 'env_off', 'env_len', 'freq_off', 'freq_len')]
 
 
@@ -48,7 +52,7 @@ DEFAULT_LUT_TABLE = (0b00000, 0b00100, 0b10000, 0b01000)   # meas_lut.sv:17-20
 def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 20,
                 event_cap=64, trace_cap=0, meas_cap=8, fproc_mode=FPROC_MEAS, meas_elem=2,
                 meas_latency=64, sync_latency=1, sync_mask=0, seed=0x5EED, p1=0.5,
-                lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE):
+                lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE, exec_flags=0):
     """Validated Config.  p1: float or per-core list of P(meas = 1)."""
     C_ = int(cores_per_shot)
     if C_ < 1 or C_ > MAX_CORES or (C_ & (C_ - 1)):
@@ -76,6 +80,7 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
     cfg.sync_mask = int(sync_mask)
     cfg.seed = int(seed) & (2 ** 64 - 1)
     cfg.lut_mask = int(lut_mask)
+    cfg.exec_flags = int(exec_flags)
     ps = list(p1) if isinstance(p1, (list, tuple, np.ndarray)) else [p1] * C_
     for c, p in enumerate(ps):
         cfg.p1_threshold[c] = prob_to_threshold(p)

@@ -25,6 +25,15 @@ def load_library(path=LIB_PATH):
     if not os.path.exists(path):
         raise DpemuError('libdpemu.so not built ({}); run __graft_entry__.build() '
                          '(hipcc --offload-arch=gfx950)'.format(path))
+    # One HIP runtime per process.  PyTorch-ROCm ships its own
+    # libamdhip64.so (soname libamdhip64.so.7) and libhsa-runtime64; loaded
+    # first, it satisfies libdpemu.so's libamdhip64.so.7 dependency, so both
+    # share one runtime and device pointers / streams pass freely.  Loaded
+    # after ours, torch would bring up a second runtime that finds no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(path)
     vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
     L.dpemu_abi_version.restype = C.c_int

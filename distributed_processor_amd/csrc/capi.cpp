@@ -28,6 +28,7 @@ struct dpemu_ctx {
     uint32_t n_programs = 0, n_groups = 0, C = 0;
     uint64_t n_quads = 0;
     bool has_fproc = false, has_sync = false;
+    std::vector<uint64_t> group_len;   // instructions of all C programs of each group
     // run constants
     uint32_t *d_thr = nullptr;
     uint64_t *d_lut = nullptr;
@@ -37,6 +38,11 @@ struct dpemu_ctx {
     int16_t *d_sin = nullptr;
     uint32_t *d_ch = nullptr;
     uint32_t ch_cap = 0;
+    std::vector<uint32_t> ch_cache;
+    int last_feat = -1;
+    // privatised outcome histograms (R replicas, reduced after the interpreter)
+    uint32_t *d_hist_rep = nullptr;
+    uint64_t hist_rep_bytes = 0;
 };
 
 static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...) __attribute__((format(printf, 3, 4)));
@@ -100,6 +106,7 @@ int dpemu_destroy(dpemu_ctx *ctx)
     (void)hipSetDevice(ctx->device);
     free_programs(ctx);
     (void)hipFree(ctx->d_thr); (void)hipFree(ctx->d_lut); (void)hipFree(ctx->d_sin); (void)hipFree(ctx->d_ch);
+    (void)hipFree(ctx->d_hist_rep);
     delete ctx;
     return DPEMU_OK;
 }
@@ -148,6 +155,9 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     ctx->n_quads = quads;
     ctx->has_fproc = fp;
     ctx->has_sync = sy;
+    ctx->group_len.assign(n_groups, 0);
+    for (uint32_t g = 0; g < n_groups; g++)
+        for (uint32_t c = 0; c < C; c++) ctx->group_len[g] += n_instr[prog_table[(uint64_t)g * C + c]];
     return DPEMU_OK;
 }
 
@@ -221,15 +231,88 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.lut_mask = cfg->lut_mask;
     const uint64_t guard = (uint64_t)C * (cfg->max_cycles / 3u + 4u) + 1024u;
     p.iter_guard = guard > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)guard;
+    // thread order and LDS program staging: a workgroup of S = BLOCK / C shots spans at
+    // most w consecutive program groups; stage their programs if they fit
+    const uint32_t S = BLOCK / C, ng = cfg->n_groups;
+    p.shot_order = 0; p.rows = 0;
+    uint64_t w;
+    if ((cfg->exec_flags & DPEMU_X_GROUP_MAJOR) && cfg->shots_per_group == 1 && ng > 1 && n_shots % ng == 0) {
+        p.shot_order = 1;
+        p.rows = (uint32_t)(n_shots / ng);
+        w = (S - 1) / p.rows + 2;
+    } else {
+        w = (ng == 1) ? 1 : (S - 1) / cfg->shots_per_group + 2;
+    }
+    uint64_t footprint = ~0ull;
+    if (w * C <= BLOCK) {
+        const std::vector<uint64_t> &gl = ctx->group_len;
+        uint64_t tot = 0;
+        for (uint64_t x : gl) tot += x;
+        footprint = (w / ng) * tot;
+        const uint64_t r = w % ng;
+        if (r) {
+            uint64_t win = 0, best = 0;
+            for (uint64_t i = 0; i < r; i++) win += gl[i % ng];
+            best = win;
+            for (uint64_t g = 1; g < ng; g++) {
+                win += gl[(g + r - 1) % ng];
+                win -= gl[g - 1];
+                best = std::max(best, win);
+            }
+            footprint += best;
+        }
+    }
+    p.prog_lds_words = 0;
     int feat = 0;
+    if (footprint <= PROG_LDS_MAX && (cfg->exec_flags & DPEMU_X_PROG_LDS)) {
+        feat |= FEAT_PROG_LDS;
+        p.prog_lds_words = (uint32_t)std::max<uint64_t>(16, (footprint + 15) & ~15ull);
+    }
     if (ctx->has_fproc) feat |= (cfg->fproc_mode == DPEMU_FPROC_LUT) ? FEAT_LUT : FEAT_FPROC;
     if (ctx->has_sync) feat |= FEAT_SYNC;
-    if (feat == (FEAT_LUT | FEAT_SYNC) || feat == FEAT_LUT || feat == 0 || feat == FEAT_FPROC ||
-        feat == FEAT_SYNC || feat == (FEAT_FPROC | FEAT_SYNC)) {
-        HIPCHK(ctx, launch_interp(p, feat, stream));
-    } else {
-        return fail(ctx, DPEMU_E_INVALID, "no kernel for feature set %d", feat);
+    // outcome histogram.  Direct: one u64 atomic per shot into out->hist --
+    // cheapest when concurrent shots spread over many bins.  Replicas: R
+    // privatised u32 copies picked by workgroup, then a reduce kernel -- for
+    // few bins hit by every wave at once (e.g. one program, 10^6 shots), where
+    // direct atomics serialise on a few cache lines.  Default: replicas when
+    // the bins a wave population touches concurrently are few.
+    uint64_t bins = 0, hist_stride = 0;
+    uint32_t R = 0;
+    if (out->hist) {
+        bins = (uint64_t)ng << C;
+        const uint64_t spg = std::max<uint64_t>(1, cfg->shots_per_group);
+        // groups live at once across ~64K resident lanes
+        const uint64_t live_groups = std::min<uint64_t>(ng, (65536 / C) / spg + 1);
+        bool repl = (live_groups << C) < 4096;
+        if (cfg->exec_flags & DPEMU_X_HIST_DIRECT) repl = false;
+        if (cfg->exec_flags & DPEMU_X_HIST_REPL) repl = true;
+        p.hist_rep = nullptr;
+        p.hist_lds = 0;
+        if (repl) {
+            const uint64_t stride = (bins + 31) & ~31ull;        // replicas on separate 128-B lines
+            const uint64_t blocks = (p.n_lanes + BLOCK - 1) / BLOCK;
+            R = (uint32_t)std::min<uint64_t>({64, blocks, std::max<uint64_t>(1, (2ull << 20) / (stride * 4))});
+            const uint64_t need = (uint64_t)R * stride * 4;
+            if (need > ctx->hist_rep_bytes) {
+                (void)hipFree(ctx->d_hist_rep);
+                ctx->d_hist_rep = nullptr; ctx->hist_rep_bytes = 0;
+                HIPCHK(ctx, hipMalloc(&ctx->d_hist_rep, need));
+                ctx->hist_rep_bytes = need;
+            }
+            HIPCHK(ctx, hipMemsetAsync(ctx->d_hist_rep, 0, need, stream));
+            p.hist = nullptr;
+            p.hist_rep = ctx->d_hist_rep;
+            p.hist_reps = R;
+            p.hist_stride = stride;
+            p.hist_lds = bins <= HIST_LDS_MAX && (BLOCK / C) >= 4 * bins;   // LDS pre-aggregation pays
+            hist_stride = stride;
+        }
     }
+    HIPCHK(ctx, launch_interp(p, feat, stream));
+    if (out->hist && p.hist_rep)
+        HIPCHK(ctx, launch_hist_reduce(ctx->d_hist_rep, R, hist_stride, bins,
+                                       reinterpret_cast<unsigned long long *>(out->hist), stream));
+    ctx->last_feat = feat;
     return DPEMU_OK;
 }
 
@@ -313,7 +396,45 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
                          const uint32_t *ev_main, const uint16_t *ev_amp, const uint32_t *env_tables,
                          const uint32_t *freq_tables, int16_t *iq_out, void *stream)
 {
-    (void)ch; (void)summary; (void)ev_main; (void)ev_amp; (void)env_tables; (void)freq_tables;
-    (void)iq_out; (void)stream;
-    return fail(ctx, DPEMU_E_INVALID, "dpemu_dds: not built yet");
+    if (!ctx) return DPEMU_E_INVALID;
+    if (!ch || !summary || !ev_main || !ev_amp || !env_tables || !freq_tables || !iq_out)
+        return fail(ctx, DPEMU_E_INVALID, "dpemu_dds: null argument");
+    if (ch->n_samples % 4) return fail(ctx, DPEMU_E_INVALID, "n_samples must be a multiple of 4");
+    if (ch->event_cap > DDS_MAX_EVENTS) return fail(ctx, DPEMU_E_INVALID, "event_cap > %u", DDS_MAX_EVENTS);
+    if (ch->n_channels == 0 || ch->n_samples == 0) return DPEMU_OK;
+    if (ch->n_channels > 65535) return fail(ctx, DPEMU_E_INVALID, "n_channels > 65535");
+    std::vector<uint32_t> desc((size_t)ch->n_channels * DDS_CH_WORDS);
+    for (uint32_t i = 0; i < ch->n_channels; i++) {
+        uint32_t *d = &desc[(size_t)i * DDS_CH_WORDS];
+        d[0] = ch->ch_lane[i]; d[1] = ch->ch_elem[i] & 3u; d[2] = ch->spc[i]; d[3] = ch->interp[i];
+        d[4] = ch->env_off[i]; d[5] = ch->env_len[i]; d[6] = ch->freq_off[i]; d[7] = ch->freq_len[i];
+        if (d[0] >= ch->n_lanes) return fail(ctx, DPEMU_E_INVALID, "channel %u: lane %u >= n_lanes", i, d[0]);
+        if (d[2] < 1 || d[2] > 16) return fail(ctx, DPEMU_E_INVALID, "channel %u: spc %u not in [1, 16]", i, d[2]);
+        if (d[3] < 1) return fail(ctx, DPEMU_E_INVALID, "channel %u: interp must be >= 1", i);
+    }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (desc != ctx->ch_cache) {            // descriptors change rarely: upload only then
+        if (ch->n_channels > ctx->ch_cap) {
+            (void)hipFree(ctx->d_ch);
+            ctx->d_ch = nullptr; ctx->ch_cap = 0;
+            HIPCHK(ctx, hipMalloc(&ctx->d_ch, desc.size() * 4));
+            ctx->ch_cap = ch->n_channels;
+        }
+        HIPCHK(ctx, hipStreamSynchronize(s));   // the previous launch may still read d_ch
+        HIPCHK(ctx, hipMemcpy(ctx->d_ch, desc.data(), desc.size() * 4, hipMemcpyHostToDevice));
+        ctx->ch_cache = desc;
+    }
+    DDSParams p{};
+    p.summary = summary;
+    p.ev_main = reinterpret_cast<const uint4 *>(ev_main);
+    p.ev_amp = ev_amp;
+    p.env = env_tables; p.freq = freq_tables;
+    p.sin_lut = ctx->d_sin;
+    p.ch = ctx->d_ch;
+    p.iq = reinterpret_cast<uint32_t *>(iq_out);
+    p.n_channels = ch->n_channels; p.n_lanes = ch->n_lanes; p.n_samples = ch->n_samples;
+    p.event_cap = ch->event_cap;
+    HIPCHK(ctx, launch_dds(p, s));
+    return DPEMU_OK;
 }

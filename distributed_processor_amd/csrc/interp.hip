@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace dpemu {
@@ -91,12 +93,55 @@ __device__ __forceinline__ void wave_fence()
     __builtin_amdgcn_wave_barrier();
 }
 
+// shot index within the run of the block-linear shot position sp: natural order, or
+// group-major (shot_order 1: shots_per_group 1, n_shots = rows * n_groups) so that a
+// workgroup's shots share their programs
+__device__ __forceinline__ uint32_t shot_of_pos(const KParams &p, uint32_t sp)
+{
+    return p.shot_order ? (sp % p.rows) * p.n_groups + sp / p.rows : sp;
+}
+
+// index of the program-group "step" of shot position sp relative to position sp0
+__device__ __forceinline__ uint32_t group_step(const KParams &p, uint32_t sp, uint32_t sp0)
+{
+    if (p.n_groups == 1) return 0;
+    if (p.shot_order) return sp / p.rows - sp0 / p.rows;
+    const uint64_t a = (p.shot_begin + shot_of_pos(p, sp)) / p.shots_per_group;
+    const uint64_t b = (p.shot_begin + shot_of_pos(p, sp0)) / p.shots_per_group;
+    return (uint32_t)(a - b);
+}
+
+// exclusive block scan of v (BLOCK threads); returns the prefix, *total the sum
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *s_tmp, uint32_t *total)
+{
+    const uint32_t tid = threadIdx.x, wl = tid & 63, wv = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (wl >= (uint32_t)o) x += y;
+    }
+    if (wl == 63) s_tmp[wv] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < BLOCK / 64; k++) {
+        const uint32_t t = s_tmp[k];
+        off += (k < wv) ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + x - v;
+}
+
 template <int FEAT>
 __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 {
     constexpr bool FPROC = (FEAT & FEAT_FPROC) != 0;
     constexpr bool SYNC = (FEAT & FEAT_SYNC) != 0;
     constexpr bool LUT = (FEAT & FEAT_LUT) != 0;
+    constexpr bool PLDS = (FEAT & FEAT_PROG_LDS) != 0;   // programs staged in LDS
     constexpr bool XMEAS = FPROC || LUT;             // measurements readable by other lanes
     constexpr int MT = XMEAS ? MEAS_LOOKUP : 1;
     constexpr int NF = LUT ? LUT_FIRE_CAP : 1;
@@ -107,14 +152,20 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     __shared__ uint32_t s_cur[LUT ? BLOCK : 1];       // merge cursor into lane's s_mt
     __shared__ uint32_t s_fire_t[NF][LUT ? BLOCK : 1];
     __shared__ uint64_t s_fire_o[NF][LUT ? BLOCK : 1];
+    // programs of this workgroup's (group, core) slots: the analogue of each core's cmd_mem
+    __shared__ uint32_t s_pref[PLDS ? BLOCK + 1 : 1];
+    __shared__ uint32_t s_scan[BLOCK / 64];
+    extern __shared__ uint4 s_prog[];
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t lane = blockIdx.x * BLOCK + tid;
     const uint32_t C = p.C;
-    const uint32_t core = lane & (C - 1);
+    const uint32_t pos = blockIdx.x * BLOCK + tid;   // thread position; a shot's cores are adjacent
+    const bool valid = pos < p.n_lanes;
+    const uint32_t core = pos & (C - 1);
+    const uint32_t spos = pos >> p.log2C;
+    const uint32_t lane = (shot_of_pos(p, spos) << p.log2C) | core;   // output lane index
+    const uint64_t shot = p.shot_begin + (lane >> p.log2C);
     const uint32_t wl = tid & 63;                    // lane within the wavefront
-    const bool valid = lane < p.n_lanes;
-    const uint64_t shot = p.shot_begin + (uint64_t)(lane >> p.log2C);
     const uint32_t leader_tid = tid & ~(C - 1);
 
     uint32_t base = 0, nprog = 0, grp = 0;
@@ -123,6 +174,42 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         const uint32_t prog = p.prog_table[(uint64_t)grp * C + core];
         base = p.offsets[prog];
         nprog = p.n_instr[prog];
+    }
+    const uint32_t thr_core = valid ? p.p1_thr[core] : 0u;
+    __shared__ uint32_t s_hist[HIST_LDS_MAX];
+    if (p.hist_lds) {
+        for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
+        __syncthreads();
+    }
+    if constexpr (PLDS) {
+        // slots k = step * C + c over the block's consecutive program groups
+        const uint32_t n_shots = p.n_lanes >> p.log2C;
+        const uint32_t sp0 = (blockIdx.x * BLOCK) >> p.log2C;
+        const uint32_t spl = min(sp0 + (BLOCK >> p.log2C), n_shots) - 1u;
+        const uint32_t g0 = (uint32_t)(((p.shot_begin + shot_of_pos(p, sp0)) / p.shots_per_group) % p.n_groups);
+        const uint32_t nslots = (group_step(p, spl, sp0) + 1u) * C;      // <= BLOCK (host-checked)
+        uint32_t len = 0;
+        if (tid < nslots) {
+            const uint32_t g = (g0 + tid / C) % p.n_groups;
+            len = p.n_instr[p.prog_table[(uint64_t)g * C + (tid & (C - 1))]];
+        }
+        uint32_t total;
+        const uint32_t pre = block_exclusive_scan(len, s_scan, &total);
+        if (tid < nslots) s_pref[tid] = pre;
+        if (tid == 0) s_pref[nslots] = total;
+        __syncthreads();
+        for (uint32_t idx = tid; idx < total; idx += BLOCK) {
+            uint32_t lo = 0, hi = nslots;                // largest k with s_pref[k] <= idx
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pref[mid] <= idx) lo = mid; else hi = mid;
+            }
+            const uint32_t g = (g0 + lo / C) % p.n_groups;
+            const uint32_t prog = p.prog_table[(uint64_t)g * C + (lo & (C - 1))];
+            s_prog[idx] = p.words[p.offsets[prog] + (idx - s_pref[lo])];
+        }
+        __syncthreads();
+        if (valid) base = s_pref[group_step(p, spos, sp0) * C + core];
     }
 #pragma unroll
     for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
@@ -163,7 +250,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         n_ev++;
         if (kind == 0 && p.meas_elem != 0xFFu && ((pe >> 24) & 3u) == p.meas_elem) {
             const uint32_t r = philox_u32(p.seed, shot, core, n_meas);
-            const uint32_t thr = p.p1_thr[core];
+            const uint32_t thr = thr_core;
             const uint32_t bit = (thr == INF32) || (r < thr);
             const uint32_t tv = te + p.meas_latency;
             if constexpr (XMEAS) {
@@ -211,7 +298,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         bool run = (mode == M_RUN);
         if (run && t > p.max_cycles) { finish(ST_MAX_CYCLES, t); run = false; }
         uint4 w = make_uint4(0u, 0u, 0u, 0u);
-        if (run && ip < nprog) w = p.words[base + ip];
+        if (run && ip < nprog) w = PLDS ? s_prog[base + ip] : p.words[base + ip];
         const uint32_t op4 = w.w >> 28;
         const uint32_t alu = (w.w >> 24) & 7u;
         const uint32_t in0_reg = (w.w >> 27) & 1u;
@@ -459,7 +546,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                     const uint32_t tf = s_fire_t[k][leader_tid];
                     if (tf >= wait_d + 1u) {
                         const uint64_t out_bits = s_fire_o[k][leader_tid];
-                        const uint4 w2 = p.words[base + ip];     // the waiting fproc instruction
+                        const uint4 w2 = PLDS ? s_prog[base + ip] : p.words[base + ip];     // the waiting fproc instruction
                         const uint32_t op4b = w2.w >> 28, alub = (w2.w >> 24) & 7u;
                         const uint32_t in0b = ((w2.w >> 27) & 1u) ? s_regs[(w2.w >> 20) & 15u][tid]
                                                                   : ((w2.z >> 24) | (w2.w << 8));
@@ -494,44 +581,83 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         if constexpr (FPROC || XMEAS) wave_fence();
     }
 
-    if (!valid) return;
-    if (p.summary) {
+    if (valid && p.summary) {
         uint4 *s = reinterpret_cast<uint4 *>(p.summary + 8ull * lane);
         s[0] = make_uint4(t_end, (ip_end & 0xFFFFu) | ((status & 0xFFu) << 16) | ((flags & 0xFFu) << 24),
                           n_ev, n_exec);
         s[1] = make_uint4(qclk_end, n_meas, meas_bits, n_tr);
     }
-    if (p.regs_out) {
+    if (valid && p.regs_out) {
 #pragma unroll
         for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = s_regs[r][tid];
     }
-    if (p.hist) {
+    if (p.hist_rep) {
+        // outcome key: bit c = last measurement of core c; one count per shot
         const uint64_t key = group_bits(__ballot(last_bit != 0u), wl, C);
-        if (core == 0u) atomicAdd(&p.hist[(uint64_t)grp * (1ull << C) + key], 1ull);
+        const uint64_t bin = (uint64_t)grp * (1ull << C) + key;
+        uint32_t *rep = p.hist_rep + (uint64_t)(blockIdx.x % p.hist_reps) * p.hist_stride;
+        if (p.hist_lds) {
+            // small histogram: aggregate the workgroup's shots in LDS first
+            if (valid && core == 0u) atomicAdd(&s_hist[bin], 1u);
+            __syncthreads();
+            const uint32_t bins = p.n_groups << C;
+            for (uint32_t i = tid; i < bins; i += BLOCK)
+                if (s_hist[i]) atomicAdd(&rep[i], s_hist[i]);
+        } else if (valid && core == 0u) {
+            atomicAdd(&rep[bin], 1u);
+        }
+    } else if (p.hist) {
+        const uint64_t key = group_bits(__ballot(last_bit != 0u), wl, C);
+        if (valid && core == 0u) atomicAdd(&p.hist[(uint64_t)grp * (1ull << C) + key], 1ull);
     }
 }
 
-#define INSTANTIATE(F) template __global__ void interp_kernel<F>(const KParams p);
-INSTANTIATE(0)
-INSTANTIATE(FEAT_FPROC)
-INSTANTIATE(FEAT_SYNC)
-INSTANTIATE(FEAT_FPROC | FEAT_SYNC)
-INSTANTIATE(FEAT_LUT)
-INSTANTIATE(FEAT_LUT | FEAT_SYNC)
+// out[i] += sum of the R replicas; thread = (bin, slice of 8 replicas), loads independent
+__global__ void __launch_bounds__(BLOCK) hist_reduce_kernel(const uint32_t *rep, uint32_t R, uint64_t stride,
+                                                           uint64_t bins, unsigned long long *hist)
+{
+    const uint32_t slices = (R + 7) / 8;
+    const uint64_t n = bins * slices;
+    for (uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; x < n; x += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t i = x % bins;
+        const uint32_t r0 = (uint32_t)(x / bins) * 8;
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = (r0 + k < R) ? rep[(uint64_t)(r0 + k) * stride + i] : 0u;
+        unsigned long long acc = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc += v[k];
+        if (acc) atomicAdd(&hist[i], acc);
+    }
+}
+
+hipError_t launch_hist_reduce(const uint32_t *rep, uint32_t R, uint64_t stride, uint64_t bins,
+                              unsigned long long *hist, hipStream_t stream)
+{
+    const uint64_t n = bins * ((R + 7) / 8);
+    const uint64_t blocks = std::min<uint64_t>((n + BLOCK - 1) / BLOCK, 8192);
+    hipLaunchKernelGGL(hist_reduce_kernel, dim3((uint32_t)blocks), dim3(BLOCK), 0, stream, rep, R, stride, bins, hist);
+    return hipGetLastError();
+}
+
+template <int F>
+static void launch_one(const KParams &p, uint32_t blocks, size_t shmem, hipStream_t stream)
+{
+    hipLaunchKernelGGL(interp_kernel<F>, dim3(blocks), dim3(BLOCK), shmem, stream, p);
+}
 
 hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
     if (blocks == 0) return hipSuccess;
+    const size_t shmem = (feat & FEAT_PROG_LDS) ? (size_t)p.prog_lds_words * sizeof(uint4) : 0;
     switch (feat) {
-    case 0: hipLaunchKernelGGL(interp_kernel<0>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
-    case FEAT_FPROC: hipLaunchKernelGGL(interp_kernel<FEAT_FPROC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
-    case FEAT_SYNC: hipLaunchKernelGGL(interp_kernel<FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
-    case FEAT_FPROC | FEAT_SYNC:
-        hipLaunchKernelGGL(interp_kernel<FEAT_FPROC | FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
-    case FEAT_LUT: hipLaunchKernelGGL(interp_kernel<FEAT_LUT>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
-    case FEAT_LUT | FEAT_SYNC:
-        hipLaunchKernelGGL(interp_kernel<FEAT_LUT | FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+#define CASE(F) case F: launch_one<F>(p, blocks, shmem, stream); break;
+    CASE(0) CASE(FEAT_FPROC) CASE(FEAT_SYNC) CASE(FEAT_FPROC | FEAT_SYNC) CASE(FEAT_LUT) CASE(FEAT_LUT | FEAT_SYNC)
+    CASE(FEAT_PROG_LDS) CASE(FEAT_PROG_LDS | FEAT_FPROC) CASE(FEAT_PROG_LDS | FEAT_SYNC)
+    CASE(FEAT_PROG_LDS | FEAT_FPROC | FEAT_SYNC) CASE(FEAT_PROG_LDS | FEAT_LUT)
+    CASE(FEAT_PROG_LDS | FEAT_LUT | FEAT_SYNC)
+#undef CASE
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -16,6 +16,8 @@ constexpr uint32_t LUT_FIRE_CAP = DPEMU_LUT_FIRE_CAP;
 constexpr int FEAT_FPROC = 1;   // fproc_meas reads (ALU_FPROC / JUMP_FPROC)
 constexpr int FEAT_SYNC = 2;    // SYNC barriers
 constexpr int FEAT_LUT = 4;     // fproc_lut back end
+constexpr int FEAT_PROG_LDS = 8; // the workgroup's programs staged in LDS (fits PROG_LDS_MAX)
+constexpr uint32_t PROG_LDS_MAX = 1024;   // instructions (16 KiB) of dynamic LDS per workgroup
 
 constexpr uint32_t ST_DONE = DPEMU_ST_DONE, ST_MAX_CYCLES = DPEMU_ST_MAX_CYCLES;
 constexpr uint32_t ST_HUNG_OPCODE = DPEMU_ST_HUNG_OPCODE, ST_DEADLOCK = DPEMU_ST_DEADLOCK;
@@ -46,7 +48,16 @@ struct KParams {
     uint64_t sync_mask, seed;
     uint32_t lut_mask;
     uint32_t iter_guard;
+    uint32_t shot_order, rows;    // 1: group-major thread order (shots_per_group 1, n = rows * n_groups)
+    uint32_t prog_lds_words;      // dynamic LDS instructions (FEAT_PROG_LDS)
+    uint32_t *hist_rep;           // [hist_reps][hist_stride] u32 replicas (128-B aligned rows)
+    uint32_t hist_reps, hist_lds; // hist_lds: n_groups << C <= HIST_LDS_MAX, aggregate in LDS
+    uint64_t hist_stride;
 };
+constexpr uint32_t HIST_LDS_MAX = 1024;
+
+hipError_t launch_hist_reduce(const uint32_t *rep, uint32_t R, uint64_t stride, uint64_t bins,
+                              unsigned long long *hist, hipStream_t stream);
 
 hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
 
@@ -62,6 +73,8 @@ struct DDSParams {
     uint32_t n_channels, n_lanes, n_samples, event_cap;
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
+constexpr uint32_t DDS_MAX_EVENTS = 1024;
+constexpr uint32_t DDS_CHUNK = 1u << 16;   // samples per workgroup
 
 hipError_t launch_dds(const DDSParams &p, hipStream_t stream);
 

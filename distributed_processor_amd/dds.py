@@ -1,0 +1,105 @@
+"""DDS I/Q synthesis from emulated pulse events (hot-path row 4).
+
+The reference stops at the pulse interface: each core drives
+``pulse_iface`` {env_word, phase, freq, amp, cfg} plus ``cstrobe`` into the
+external QubiC DSP (hdl/pulse_iface.sv:2-6, hdl/proc.sv:131-136), and the
+assembler hands that DSP its per-element env / freq buffers
+(assembler.py:472-476, asmparse.py:46-86).  This module plays the emulated
+pulse timelines through a fixed-point DDS on the GPU (``dpemu_dds``,
+csrc/dds.hip) so a caller gets sample-level I/Q per (shot, core, element)
+channel.  The arithmetic is build-defined and pinned
+bit-exactly by oracle/dds_ref.c.
+
+Usage::
+
+    plan = ChannelPlan(programs, cfg, shot_begin, n_shots,
+                       [(shot, core, elem), ...], elem_params={0: (16, 1), 2: (4, 4)})
+    iq = emu.synthesize(plan, device_outputs, n_samples)     # torch int32 [n_ch, n_samples]
+"""
+
+from __future__ import annotations
+
+from typing import Dict, Iterable, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _abi
+
+DESC_FIELDS = ('ch_lane', 'ch_elem', 'spc', 'interp', 'env_off', 'env_len', 'freq_off', 'freq_len')
+
+
+class ChannelPlan:
+    """Channel descriptors and concatenated env / freq tables for one run.
+
+    programs: the ProgramSet that was run (its ``buffers`` hold the
+    assembler's env_buffers / freq_buffers of every (group, core));
+    channels: (absolute shot, core, element) triples, all inside
+    [shot_begin, shot_begin + n_shots); elem_params: element -> (samples per
+    clock, interpolation ratio).  Tables shared by several channels are stored
+    once.
+    """
+
+    def __init__(self, programs, cfg, shot_begin: int, n_shots: int,
+                 channels: Iterable[Tuple[int, int, int]],
+                 elem_params: Dict[int, Tuple[int, int]]):
+        C_ = cfg.cores_per_shot
+        spg, ng = max(int(cfg.shots_per_group), 1), max(int(cfg.n_groups), 1)
+        envs, freqs = [], []
+        env_at: Dict[bytes, Tuple[int, int]] = {}
+        freq_at: Dict[bytes, Tuple[int, int]] = {}
+        n_env = n_freq = 0
+
+        def place(tab, store, at, n):
+            key = tab.tobytes()
+            if key not in at:
+                at[key] = (n, len(tab))
+                store.append(tab)
+                n += len(tab)
+            return at[key], n
+
+        rows = []
+        for shot, core, elem in channels:
+            shot, core, elem = int(shot), int(core), int(elem)
+            if not (shot_begin <= shot < shot_begin + n_shots) or not (0 <= core < C_):
+                raise ValueError('channel ({}, {}, {}) outside the run'.format(shot, core, elem))
+            if elem not in elem_params:
+                raise ValueError('no (spc, interp) for element {}'.format(elem))
+            g = (shot // spg) % ng
+            env_l, freq_l = programs.buffers.get((g, core), ([], []))
+            env = env_l[elem] if elem < len(env_l) else np.zeros(0, np.uint32)
+            frq = freq_l[elem] if elem < len(freq_l) else np.zeros(0, np.uint32)
+            (eo, el), n_env = place(np.ascontiguousarray(env, np.uint32), envs, env_at, n_env)
+            (fo, fl), n_freq = place(np.ascontiguousarray(frq, np.uint32), freqs, freq_at, n_freq)
+            spc, interp = elem_params[elem]
+            rows.append(((shot - shot_begin) * C_ + core, elem, spc, interp, eo, el, fo, fl))
+        self.desc = np.array(rows, np.uint32).reshape(-1, 8)
+        self.env = np.concatenate(envs).astype(np.uint32) if n_env else np.zeros(1, np.uint32)
+        self.freq = np.concatenate(freqs).astype(np.uint32) if n_freq else np.zeros(1, np.uint32)
+        self.n_lanes = int(n_shots) * C_
+        self.event_cap = int(cfg.event_cap)
+        self._cols = {f: np.ascontiguousarray(self.desc[:, i]) for i, f in enumerate(DESC_FIELDS)}
+        self._dev = None
+
+    @property
+    def n_channels(self):
+        return self.desc.shape[0]
+
+    def struct(self, n_samples: int) -> _abi.DDSChannels:
+        s = _abi.DDSChannels(self.n_channels, self.n_lanes, int(n_samples), self.event_cap)
+        for f in DESC_FIELDS:
+            setattr(s, f, self._cols[f].ctypes.data)
+        return s
+
+    def device_tables(self, device='cuda'):
+        """env / freq tables as device tensors (uploaded once per plan)."""
+        if self._dev is None:
+            import torch
+            self._dev = (torch.from_numpy(self.env.view(np.int32)).to(device),
+                         torch.from_numpy(self.freq.view(np.int32)).to(device))
+        return self._dev
+
+
+def split_iq(iq_u32: np.ndarray):
+    """(I, Q) int16 arrays of dpemu_dds output words (I low half, Q high half)."""
+    v = np.asarray(iq_u32).view(np.uint32)
+    return (v & 0xFFFF).astype(np.uint16).view(np.int16), (v >> 16).astype(np.uint16).view(np.int16)

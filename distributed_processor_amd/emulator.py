@@ -38,17 +38,19 @@ def _next_pow2(n: int) -> int:
     return c
 
 
-def _shot_programs(shot) -> Dict[int, np.ndarray]:
-    """one shot's programs: assembler dict {core: {'cmd_buf': ...}}, dict
-    {core: words}, or a list (index = core)."""
-    if isinstance(shot, dict):
-        out = {}
-        for k, v in shot.items():
-            if isinstance(v, dict):
-                v = v['cmd_buf']
-            out[int(k)] = _to_u32(v)
-        return out
-    return {c: _to_u32(p) for c, p in enumerate(shot)}
+def _shot_programs(shot):
+    """one shot's programs: assembler dict {core: {'cmd_buf': ..., 'env_buffers':
+    [...], 'freq_buffers': [...]}}, dict {core: words}, or a list (index = core).
+    Returns ({core: (n, 4) u32}, {core: (env_buffers, freq_buffers)})."""
+    progs, bufs = {}, {}
+    items = shot.items() if isinstance(shot, dict) else enumerate(shot)
+    for k, v in items:
+        if isinstance(v, dict):
+            bufs[int(k)] = ([np.frombuffer(bytes(b), '<u4').astype(np.uint32) for b in v.get('env_buffers', [])],
+                            [np.frombuffer(bytes(b), '<u4').astype(np.uint32) for b in v.get('freq_buffers', [])])
+            v = v['cmd_buf']
+        progs[int(k)] = _to_u32(v)
+    return progs, bufs
 
 
 class ProgramSet:
@@ -62,7 +64,10 @@ class ProgramSet:
     def __init__(self, groups: Sequence, cores_per_shot: Optional[int] = None):
         if isinstance(groups, dict):
             groups = [groups]
-        per_group = [_shot_programs(g) for g in groups]
+        parsed = [_shot_programs(g) for g in groups]
+        per_group = [p for p, _ in parsed]
+        # env / freq buffers of (group, core), when the programs came from an assembler
+        self.buffers = {(g, c): b for g, (_, bs) in enumerate(parsed) for c, b in bs.items()}
         if not per_group:
             raise ValueError('no programs')
         ncore = max((max(g) + 1 if g else 1) for g in per_group)
@@ -208,6 +213,32 @@ class Emulator:
         rc = self._L.dpemu_run(self._h, C.addressof(cfg), int(shot_begin), int(n_shots), C.addressof(o),
                                C.c_void_p(s) if s else None)
         check(self._h, rc, 'dpemu_run')
+
+    def synthesize(self, plan, outputs: dict, n_samples: int, iq=None, stream=None):
+        """DDS I/Q of every channel of ``plan`` (dds.ChannelPlan) from a device
+        run's outputs (summary / ev_main / ev_amp tensors of run_device).
+        Returns (or fills) an int32 device tensor [n_channels, n_samples]
+        whose words hold I in the low and Q in the high 16 bits."""
+        import torch
+        for k in ('summary', 'ev_main', 'ev_amp'):
+            if k not in outputs:
+                raise DpemuError('synthesize needs the run\'s {} output'.format(k))
+        if outputs['ev_main'].shape[:2] != (plan.event_cap, plan.n_lanes):
+            raise DpemuError('event arrays do not match the plan (event_cap, n_lanes)')
+        dev = outputs['summary'].device
+        if iq is None:
+            iq = torch.empty((plan.n_channels, int(n_samples)), dtype=torch.int32, device=dev)
+        elif tuple(iq.shape) != (plan.n_channels, int(n_samples)) or iq.dtype != torch.int32:
+            raise DpemuError('iq must be int32 [n_channels, n_samples]')
+        env, freq = plan.device_tables(dev)
+        ch = plan.struct(n_samples)
+        s = getattr(stream, 'cuda_stream', stream)
+        rc = self._L.dpemu_dds(self._h, C.addressof(ch), outputs['summary'].data_ptr(),
+                               outputs['ev_main'].data_ptr(), outputs['ev_amp'].data_ptr(),
+                               env.data_ptr(), freq.data_ptr(), iq.data_ptr(),
+                               C.c_void_p(s) if s else None)
+        check(self._h, rc, 'dpemu_dds')
+        return iq
 
 
 def alloc_device_outputs(cfg: _abi.Config, n_shots: int, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'),

@@ -71,6 +71,11 @@ extern "C" {
 #define DPEMU_TRACE_QCLK_LOAD 16  /* INC_QCLK loaded qclk (value = qclk at t)             */
 #define DPEMU_TRACE_QCLK_RST  17  /* SYNC reset qclk (value 0 at t)                       */
 
+#define DPEMU_X_PROG_LDS    0x1   /* stage each workgroup's programs in LDS when they fit    */
+#define DPEMU_X_GROUP_MAJOR 0x2   /* group-major thread order (shots_per_group 1, n % n_groups == 0) */
+#define DPEMU_X_HIST_DIRECT 0x4   /* outcome histogram: atomics straight into out->hist       */
+#define DPEMU_X_HIST_REPL   0x8   /* outcome histogram: privatised replicas + reduce          */
+
 #define DPEMU_MAX_CORES 64
 #define DPEMU_MEAS_LOOKUP 16      /* a core's first 16 measurements are visible to fproc;
                                      later ones set DPEMU_F_MEAS_OVF and are invisible  */
@@ -93,7 +98,7 @@ typedef struct dpemu_config {
     uint32_t meas_elem;        /* strobe with (cfg & 3) == meas_elem is a readout; 0xFF none */
     uint32_t meas_latency;     /* readout strobe -> meas_valid, clocks (>= 1)           */
     uint32_t sync_latency;     /* last sync enable -> sync.ready, clocks (>= 1)         */
-    uint32_t reserved0;
+    uint32_t exec_flags;       /* DPEMU_X_* execution knobs (results never depend on them) */
     uint64_t sync_mask;        /* participant cores (bit c); 0 = all C cores             */
     uint64_t seed;             /* Philox4x32-10 key                                      */
     uint32_t lut_mask;         /* meas_lut mask (nonzero), meas_lut.sv:16                */
@@ -161,30 +166,33 @@ int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
                    uint64_t n_shots, const dpemu_outputs *host_out);
 
 /*
- * DDS synthesis (build-defined fixed point).  One channel =
- * one (lane, element) pair.  Channel ch reads the events of lane
- * ch_lane[ch] (slot-major as written by dpemu_run, n_lanes stride, count
- * from the summary) keeping strobes whose cfg & 3 == ch_elem[ch], plus
- * pulse_reset events.  env_tables / freq_tables: concatenated u32 buffers
- * (assembler env_buffers / freq_buffers format), channel ch using
- * env_off[ch] / freq_off[ch] (u32 offsets).  Output iq[ch][n_samples] as
- * int16 {I, Q} pairs (4 B/sample) for samples [0, n_samples) of the
- * channel, sample j at cycle j / spc[ch].  sin_lut: 4096 int16 Q15 (see
- * dpemu_dds_sin_lut).
+ * DDS synthesis (build-defined fixed point; CPU restatement
+ * oracle/dds_ref.c).  One channel = one (lane, element) pair: it plays the
+ * lane's strobes whose cfg & 3 == element, with the lane's pulse_resets as
+ * phase references, from the events dpemu_run wrote (slot-major, n_lanes
+ * stride, count = min(summary n_events, event_cap)).  Env / freq tables are
+ * the assembler's env_buffers / freq_buffers (asmparse.py:46-86 formats),
+ * concatenated; channel c reads env words [env_off, env_off + env_len) and
+ * freq words [freq_off, freq_off + freq_len).  Output: iq[c][n_samples] of
+ * int16 {I, Q} pairs; sample j is at emulated cycle j / spc.
+ *
+ * The dpemu_dds_channels arrays are HOST memory (n_channels entries each);
+ * summary / ev_main / ev_amp / env_tables / freq_tables / iq_out are device
+ * pointers.  n_samples must be a multiple of 4; event_cap <= 1024.
  */
 typedef struct dpemu_dds_channels {
     uint32_t n_channels;
-    uint32_t n_lanes;          /* stride of the event arrays */
-    uint32_t n_samples;        /* samples per channel        */
-    uint32_t reserved;
-    const uint32_t *ch_lane;   /* [n_channels] */
-    const uint32_t *ch_elem;   /* [n_channels] */
-    const uint32_t *spc;       /* [n_channels] samples per clock (1..16) */
-    const uint32_t *interp;    /* [n_channels] output samples per envelope sample (>=1) */
-    const uint32_t *env_off;   /* [n_channels] */
-    const uint32_t *env_len;   /* [n_channels] u32 words available */
-    const uint32_t *freq_off;  /* [n_channels] */
-    const uint32_t *freq_len;  /* [n_channels] u32 words available */
+    uint32_t n_lanes;          /* stride of the event arrays (dpemu_run's n_lanes) */
+    uint32_t n_samples;        /* samples per channel                               */
+    uint32_t event_cap;        /* event slots per lane of the event arrays          */
+    const uint32_t *ch_lane;   /* lane of each channel                               */
+    const uint32_t *ch_elem;   /* element (cfg & 3) of each channel                  */
+    const uint32_t *spc;       /* samples per clock, 1..16                           */
+    const uint32_t *interp;    /* output samples per envelope sample, >= 1           */
+    const uint32_t *env_off;
+    const uint32_t *env_len;
+    const uint32_t *freq_off;
+    const uint32_t *freq_len;
 } dpemu_dds_channels;
 
 int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uint32_t *summary,

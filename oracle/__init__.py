@@ -11,6 +11,7 @@ path (``distributed_processor_amd``) never does.
 * ``rtl_run_shot``  per-clock multi-core shot with the build-defined
                  measurement model and sync controller
 * ``fast_run``   event-driven model, dpemu_run-compatible outputs
+* ``dds``        fixed-point DDS restatement over those outputs
 """
 
 import ctypes as C
@@ -101,8 +102,43 @@ def _setup(L):
     if hasattr(L, 'fast_run'):
         L.fast_run.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
         L.fast_run.restype = C.c_int
-    if hasattr(L, 'oracle_dds'):
-        L.oracle_dds_sin_lut.argtypes = [C.c_void_p]
+    L.oracle_dds_sin_lut.argtypes = [C.c_void_p]
+    L.oracle_dds.argtypes = [C.c_void_p, C.c_int]
+
+
+class DDSArgs(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ('n_channels', 'n_lanes', 'n_samples', 'event_cap')] + [
+        (n, C.c_void_p) for n in ('ch', 'summary', 'ev_main', 'ev_amp', 'env', 'freq', 'iq')]
+
+
+def dds_sin_lut():
+    out = np.zeros(4096, np.int16)
+    lib().oracle_dds_sin_lut(out.ctypes.data)
+    return out
+
+
+def dds(desc, summary, ev_main, ev_amp, env, freq, n_samples, event_cap, threads=0):
+    """oracle_dds: desc (n_ch, 8) u32 [lane, elem, spc, interp, env_off, env_len,
+    freq_off, freq_len]; event arrays in dpemu_run layout (host); returns
+    (n_ch, n_samples) u32 samples, I in the low half, Q in the high half."""
+    desc = np.ascontiguousarray(desc, np.uint32).reshape(-1, 8)
+    summary = np.ascontiguousarray(summary).view(np.uint32)
+    ev_main = np.ascontiguousarray(ev_main).view(np.uint32)
+    ev_amp = np.ascontiguousarray(ev_amp).view(np.uint16)
+    env = np.ascontiguousarray(env, np.uint32)
+    freq = np.ascontiguousarray(freq, np.uint32)
+    if len(env) == 0:
+        env = np.zeros(1, np.uint32)
+    if len(freq) == 0:
+        freq = np.zeros(1, np.uint32)
+    n_lanes = summary.shape[0]
+    assert ev_main.shape[:2] == (event_cap, n_lanes) and ev_amp.shape == (event_cap, n_lanes)
+    iq = np.zeros((desc.shape[0], int(n_samples)), np.uint32)
+    a = DDSArgs(desc.shape[0], n_lanes, int(n_samples), int(event_cap), desc.ctypes.data,
+                summary.ctypes.data, ev_main.ctypes.data, ev_amp.ctypes.data, env.ctypes.data,
+                freq.ctypes.data, iq.ctypes.data)
+    lib().oracle_dds(C.addressof(a), int(threads))
+    return iq
 
 
 def _u128_to_u32x4(word):

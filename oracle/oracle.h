@@ -166,6 +166,16 @@ int fast_run(const dpemu_config *cfg, const uint32_t *words, const uint32_t *off
 
 /* ---- DDS restatement --------------------------------------------------------- */
 void oracle_dds_sin_lut(int16_t *out4096);
+typedef struct {
+    uint32_t n_channels, n_lanes, n_samples, event_cap;
+    const uint32_t *ch;          /* [n_channels][8]: lane, elem, spc, interp, env_off, env_len, freq_off, freq_len */
+    const uint32_t *summary;     /* [n_lanes][8] */
+    const uint32_t *ev_main;     /* [event_cap][n_lanes][4] */
+    const uint16_t *ev_amp;      /* [event_cap][n_lanes] */
+    const uint32_t *env, *freq;
+    uint32_t *iq;                /* [n_channels][n_samples] */
+} oracle_dds_args;
+void oracle_dds(const oracle_dds_args *a, int n_threads);
 
 #ifdef __cplusplus
 }

@@ -11,4 +11,6 @@ rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --cpu-seconds 5 > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
+[ $rc -ne 0 ] && exit $rc
+if [ -n "$AB" ]; then timeout -k 10 300 python -u scripts/ab_interp.py 5 10 > gpurun_out/ab.log 2>&1; rc=$?; echo "ab rc=$rc"; cat gpurun_out/ab.log | grep -v amdgpu.ids; fi
 exit $rc

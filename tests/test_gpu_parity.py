@@ -41,9 +41,17 @@ def compare_all(gpu, ref, ctx=''):
 
 
 def run_pair(emu, ps, cfg, n_shots, shot0=0):
+    """GPU run and oracle; the execution variants (LDS-staged programs,
+    group-major thread order, histogram strategy) must produce the same bytes"""
     emu.load(ps)
     g = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
     f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n_shots, want=ALL_OUT)
+    base = cfg.exec_flags
+    for flags in (_abi.X_PROG_LDS | _abi.X_GROUP_MAJOR | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT):
+        cfg.exec_flags = flags
+        g2 = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
+        compare_all(g2.arrays, g.arrays, 'execution variant {:#x}'.format(flags))
+    cfg.exec_flags = base
     return g.arrays, f
 
 
@@ -58,7 +66,7 @@ def test_fuzz_gpu_vs_fast(emu, seed):
                            meas_cap=16, fproc_mode=mode, meas_latency=1 + seed % 23,
                            sync_latency=1 + seed % 3, sync_mask=(0b0111 if seed % 5 == 0 and C == 4 else 0),
                            seed=seed)
-    n_shots = 333
+    n_shots = 333 if seed % 2 else 100 * ps.n_groups     # odd: natural order; even: group-major
     g, f = run_pair(emu, ps, cfg, n_shots, shot0=seed * 1000)
     compare_all(g, f, 'seed {}'.format(seed))
 
