@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <cstdlib>
 #include <vector>
 
 #include "kernels.h"
@@ -39,6 +40,11 @@ struct dpemu_ctx {
     uint32_t *d_ch = nullptr;
     uint32_t ch_cap = 0;
     std::vector<uint32_t> ch_cache;
+    uint32_t dds_spt8 = 1;                  // DPEMU_DDS_SPT=4 forces 4 samples per thread
+    uint32_t dds_probe = 0;                 // DPEMU_DDS_PROBE: kernel measurement probes
+    uint32_t dds_chunk = DDS_CHUNK;         // DPEMU_DDS_CHUNK: samples per workgroup
+    uint32_t dds_nt = 0;                    // DPEMU_DDS_NT: streaming stores
+    uint32_t dds_ilv = 0;                   // DPEMU_DDS_ILV: interleaved tiles
     int last_feat = -1;
     // privatised outcome histograms (R replicas, reduced after the interpreter)
     uint32_t *d_hist_rep = nullptr;
@@ -84,6 +90,14 @@ int dpemu_create(int device, dpemu_ctx **out)
     if (hipSetDevice(device) != hipSuccess) return DPEMU_E_DEVICE;
     dpemu_ctx *ctx = new dpemu_ctx();
     ctx->device = device;
+    if (const char *e = getenv("DPEMU_DDS_SPT")) ctx->dds_spt8 = atoi(e) == 8;
+    if (const char *e = getenv("DPEMU_DDS_PROBE")) ctx->dds_probe = (uint32_t)atoi(e);
+    if (const char *e = getenv("DPEMU_DDS_CHUNK")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v >= 8 * BLOCK && (v % (8 * BLOCK)) == 0) ctx->dds_chunk = v;
+    }
+    if (const char *e = getenv("DPEMU_DDS_NT")) ctx->dds_nt = atoi(e) != 0;
+    if (const char *e = getenv("DPEMU_DDS_ILV")) ctx->dds_ilv = atoi(e) != 0;
     if (hipMalloc(&ctx->d_thr, DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&ctx->d_lut, 256 * sizeof(uint64_t)) != hipSuccess) {
         delete ctx;
@@ -404,6 +418,7 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     if (ch->n_channels == 0 || ch->n_samples == 0) return DPEMU_OK;
     if (ch->n_channels > 65535) return fail(ctx, DPEMU_E_INVALID, "n_channels > 65535");
     std::vector<uint32_t> desc((size_t)ch->n_channels * DDS_CH_WORDS);
+    uint32_t env_max = 0, freq_max = 0;         // LDS staging sizes: largest tables that fit
     for (uint32_t i = 0; i < ch->n_channels; i++) {
         uint32_t *d = &desc[(size_t)i * DDS_CH_WORDS];
         d[0] = ch->ch_lane[i]; d[1] = ch->ch_elem[i] & 3u; d[2] = ch->spc[i]; d[3] = ch->interp[i];
@@ -411,6 +426,8 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
         if (d[0] >= ch->n_lanes) return fail(ctx, DPEMU_E_INVALID, "channel %u: lane %u >= n_lanes", i, d[0]);
         if (d[2] < 1 || d[2] > 16) return fail(ctx, DPEMU_E_INVALID, "channel %u: spc %u not in [1, 16]", i, d[2]);
         if (d[3] < 1) return fail(ctx, DPEMU_E_INVALID, "channel %u: interp must be >= 1", i);
+        if (d[5] <= DDS_ENV_LDS_MAX) env_max = std::max(env_max, d[5]);
+        if (d[7] <= DDS_FREQ_LDS_MAX) freq_max = std::max(freq_max, d[7]);
     }
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
@@ -435,6 +452,14 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.iq = reinterpret_cast<uint32_t *>(iq_out);
     p.n_channels = ch->n_channels; p.n_lanes = ch->n_lanes; p.n_samples = ch->n_samples;
     p.event_cap = ch->event_cap;
+    p.spt8 = ctx->dds_spt8;
+    p.probe = ctx->dds_probe;
+    p.chunk = ctx->dds_chunk;
+    p.nt = ctx->dds_nt;
+    p.ilv = ctx->dds_ilv;
+    p.ev_lds = std::max<uint32_t>(8, (ch->event_cap + 7) & ~7u);
+    p.env_lds = (env_max + 3) & ~3u;
+    p.freq_lds = (freq_max + 3) & ~3u;
     HIPCHK(ctx, launch_dds(p, s));
     return DPEMU_OK;
 }

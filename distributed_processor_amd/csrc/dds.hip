@@ -3,9 +3,11 @@
 // Spec: DESIGN.md §DDS and oracle/dds_ref.c (CPU restatement, bit-exact).
 // Inputs are the interpreter's outputs in HBM (lane summaries + slot-major
 // event records) and the assembler's env / freq buffers (asmparse.py:46-86
-// formats).  HBM-write-bound by design: 4 B per output sample, everything
-// else is read once per workgroup (events -> LDS) or hits L2 (env / freq
-// tables), so the sample loop is budgeted in VALU ops per sample.
+// formats).  HBM-write-bound by design: 4 B per output sample; everything
+// else is read once per workgroup into LDS (the channel's events, env and
+// freq tables, the sine table), so the sample loop issues no global loads --
+// on gfx950 stores count in vmcnt, and a load in the loop would make every
+// tile wait for the previous tile's stores.
 //
 // Grid: (sample chunks, channels).  A workgroup compacts its channel's
 // events into LDS -- strobes of the channel's element and pulse_resets, both
@@ -15,13 +17,15 @@
 // 1 KiB contiguous).
 //
 // Two sweeps, chosen per channel:
-//  * quad  (spc % 4 == 0, interp 1 or a power of two >= 4, tables 16-B
-//          aligned -- every QubiC element): the 4 samples of a thread share
-//          one emulated cycle, so theta / carrier / amplitude are computed
-//          once per 4 samples and strobe fields once per pulse; env and
-//          rotation words arrive as single 16-B loads.  Per sample: 4
-//          v_dot2_i32_i16, 4 shifts, 4 clamps, 3 packs.
-//  * generic  (anything else the ABI accepts): the per-sample definition.
+//  * quad  (spc % 4 == 0, interp 1 or a power of two >= 4, tables staged in
+//          LDS -- every QubiC element): the 4 (or 8, when 8 | spc) samples
+//          of a thread share one emulated cycle, so theta / carrier /
+//          amplitude are computed once per cycle; strobe fields and the
+//          thread's rotation words (its sub-sample slot never changes) once
+//          per pulse; env words arrive as 16-B LDS reads.  Per sample:
+//          4 v_dot2_i32_i16, 4 shifts, 4 clamps, 3 packs, 1 select.
+//  * generic  (anything else the ABI accepts): the per-sample definition,
+//          reading env / freq tables from global memory.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -32,12 +36,14 @@
 
 namespace dpemu {
 
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-
-// a.lo * b.lo + a.hi * b.hi + c on packed int16 pairs: one v_dot2_i32_i16
+// a.lo * b.lo + a.hi * b.hi + c on packed int16 pairs: one VOP3P
+// v_dot2_i32_i16 with the rounding constant in an SGPR (the builtin lowers to
+// v_dot2c + a v_mov of the accumulator per product)
 __device__ __forceinline__ int32_t dot2(uint32_t a, uint32_t b, int32_t c)
 {
-    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b), c, false);
+    int32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
 }
 
 __device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return min(max(v, lo), hi); }
@@ -61,8 +67,10 @@ struct Carrier {
 __device__ __forceinline__ Carrier carrier(const int16_t *lut, uint32_t theta, int32_t amp)
 {
     const uint32_t idx = theta >> 20;
-    const int32_t ai = (__mul24((int32_t)lut[(idx + 1024) & 4095], amp) + (1 << 15)) >> 16;
-    const int32_t aq = (__mul24((int32_t)lut[idx], amp) + (1 << 15)) >> 16;
+    // |c0| < 2^15, amp < 2^16: v_mad_i32_i24
+    const int32_t a16 = amp & 0xFFFF;
+    const int32_t ai = ((int32_t)lut[(idx + 1024) & 4095] * a16 + (1 << 15)) >> 16;
+    const int32_t aq = ((int32_t)lut[idx] * a16 + (1 << 15)) >> 16;
     return Carrier{pack16(-aq, ai), pack16(ai, aq)};
 }
 
@@ -92,21 +100,138 @@ __device__ __forceinline__ int last_le(const uint32_t *t, int n, uint32_t x)
     return lo - 1;
 }
 
-__device__ __forceinline__ void store4(uint32_t *out, uint32_t j0, uint32_t c_end, const uint32_t v[4])
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void store4(uint32_t *out, uint32_t j0, uint32_t c_end, const uint32_t v[4], bool nt = false)
 {
     if (j0 + 3 < c_end) {
-        *reinterpret_cast<uint4 *>(out + j0) = make_uint4(v[0], v[1], v[2], v[3]);
+        const u32x4 w = {v[0], v[1], v[2], v[3]};
+        if (nt)
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(out + j0));
+        else
+            *reinterpret_cast<u32x4 *>(out + j0) = w;
     } else {
         for (int s = 0; s < 4 && j0 + s < c_end; s++) out[j0 + s] = v[s];
     }
 }
 
+struct QuadArgs {
+    const int16_t *lut;
+    const uint32_t *st_t, *st_env, *st_pf;
+    const uint16_t *st_amp;
+    const uint32_t *rs_t;
+    int n_st, n_rs;
+    uint32_t spc, spc_sh, interp, int_sh;
+    const uint32_t *env;            // channel's env table (LDS)
+    uint32_t env_len;
+    const uint32_t *freq;           // channel's freq table (LDS)
+    uint32_t freq_len;
+    uint32_t *out;
+    uint32_t c_end;                 // end of this workgroup's samples
+    uint32_t tiles_step;            // tile stride: 1 (chunked) or gridDim.x (interleaved)
+    bool nt;
+};
+
+// Quad sweep: a thread's SPT consecutive samples (SPT | spc) share one
+// emulated cycle.  The tile stride SPT * BLOCK is a multiple of spc, so a
+// thread's sub-sample slot k0 is fixed and its SPT rotation words change only
+// with the pulse.
+template <int SPT>
+__device__ __forceinline__ void sweep_quad(const QuadArgs &q, uint32_t j_first)
+{
+    constexpr int NV = SPT / 4;
+    const uint32_t k0 = j_first & (q.spc - 1);
+    int si = last_le(q.st_t, q.n_st, j_first >> q.spc_sh), ri = last_le(q.rs_t, q.n_rs, j_first >> q.spc_sh);
+    int cur = -2;                                   // strobe whose fields are cached
+    bool act = false;                               // strobe plays (freq entry valid)
+    uint32_t base = 0, lim = 0, emask = 0, F0 = 0, ph15 = 0;
+    int32_t amp = 0;
+    uint32_t r[SPT];                                // rotation words R_{k0+s}
+#pragma unroll
+    for (int s = 0; s < SPT; s++) r[s] = 0;
+    const uint32_t *envp = q.env;
+    for (uint32_t j0 = j_first; j0 < q.c_end; j0 += q.tiles_step * (SPT * BLOCK)) {
+        const uint32_t n = j0 >> q.spc_sh;
+        while (si + 1 < q.n_st && q.st_t[si + 1] <= n) si++;
+        while (ri + 1 < q.n_rs && q.rs_t[ri + 1] <= n) ri++;
+        uint32_t v[SPT];
+#pragma unroll
+        for (int s = 0; s < SPT; s++) v[s] = 0;
+        if (si != cur) {                            // new pulse: decode its fields once
+            cur = si;
+            act = false;
+            if (si >= 0) {
+                const uint32_t env_w = q.st_env[si], pf = q.st_pf[si];
+                const uint32_t A = env_w & 0xFFFu, L = (env_w >> 12) & 0xFFFu, fi = pf >> 17;
+                base = q.st_t[si] * q.spc;          // sample index of the strobe
+                // samples d = j - base with env index (d >> int_sh) & emask inside the
+                // pulse and the table: d < lim
+                const uint32_t room = q.env_len > 4 * A ? q.env_len - 4 * A : 0u;
+                if (L) {
+                    emask = 0xFFFFFFFFu;
+                    const uint32_t n_env = min(4 * L, room);
+                    lim = n_env << q.int_sh;
+                    if ((lim >> q.int_sh) != n_env) lim = 0xFFFFFFFFu;   // no overflow past 2^32
+                } else {
+                    emask = 0u;                     // CW: env word 4A forever
+                    lim = room ? 0xFFFFFFFFu : 0u;
+                }
+                envp = q.env + 4 * A;
+                act = 16 * fi + 15 < q.freq_len;
+                if (act) {
+                    const uint32_t *frp = q.freq + 16 * fi;
+                    F0 = frp[0];
+#pragma unroll
+                    for (int h = 0; h < NV; h++) {
+                        const uint4 rw = *reinterpret_cast<const uint4 *>(frp + k0 + 4 * h);
+                        r[4 * h] = rw.x; r[4 * h + 1] = rw.y; r[4 * h + 2] = rw.z; r[4 * h + 3] = rw.w;
+                    }
+                }
+                ph15 = (pf & 0x1FFFFu) << 15;
+                amp = q.st_amp[si];
+            }
+        }
+        if (act) {
+            const uint32_t t_ref = ri >= 0 ? q.rs_t[ri] : 0u;
+            const Carrier a0 = carrier(q.lut, F0 * (n - t_ref) + ph15, amp);
+            uint32_t ew[SPT];
+            const uint32_t d0 = j0 - base;
+            if (q.interp == 1 && d0 + (SPT - 1) < lim && emask) {
+#pragma unroll
+                for (int h = 0; h < NV; h++) {
+                    const uint4 e4 = *reinterpret_cast<const uint4 *>(envp + d0 + 4 * h);
+                    ew[4 * h] = e4.x; ew[4 * h + 1] = e4.y; ew[4 * h + 2] = e4.z; ew[4 * h + 3] = e4.w;
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < SPT; s++)
+                    ew[s] = d0 + s < lim ? envp[((d0 + s) >> q.int_sh) & emask] : 0u;
+            }
+#pragma unroll
+            for (int s = 0; s < SPT; s++) {
+                Carrier a = rotate(a0, r[s]);
+                if (s == 0 && k0 == 0) a = a0;      // sub-sample 0 is the unrotated carrier
+                v[s] = mix(ew[s], a) & (d0 + s < lim ? 0xFFFFFFFFu : 0u);
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < NV; h++) store4(q.out, j0 + 4 * h, q.c_end, v + 4 * h, q.nt);
+    }
+}
+
 __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
 {
-    __shared__ int16_t s_lut[4096];
-    __shared__ uint32_t s_st_t[DDS_MAX_EVENTS], s_st_env[DDS_MAX_EVENTS], s_st_pf[DDS_MAX_EVENTS];
-    __shared__ uint16_t s_st_amp[DDS_MAX_EVENTS];
-    __shared__ uint32_t s_rs_t[DDS_MAX_EVENTS];
+    // dynamic LDS (dds_lds_bytes): sine table | compacted strobes / resets |
+    // staged env table | staged freq table
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    int16_t *s_lut = reinterpret_cast<int16_t *>(s_dyn);
+    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn + 8192);
+    uint32_t *s_st_env = s_st_t + p.ev_lds;
+    uint32_t *s_st_pf = s_st_env + p.ev_lds;
+    uint32_t *s_rs_t = s_st_pf + p.ev_lds;
+    uint32_t *s_env = s_rs_t + p.ev_lds;
+    uint32_t *s_freq = s_env + p.env_lds;
+    uint16_t *s_st_amp = reinterpret_cast<uint16_t *>(s_freq + p.freq_lds);
     __shared__ uint32_t s_tmp[2 * (BLOCK / 64)];
     __shared__ uint32_t s_cnt[2];
 
@@ -117,22 +242,70 @@ __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
     const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
     const uint32_t spc_sh = __ffs(spc) - 1, int_sh = __ffs(interp) - 1;
+    const bool staged = env_len <= p.env_lds && freq_len <= p.freq_lds;
+    if (p.probe == 5) {                         // probe: persistent grid, flattened 4-KiB tiles
+        const uint64_t total = (uint64_t)p.n_channels * p.n_samples;
+        const uint64_t G = (uint64_t)gridDim.x * gridDim.y, wg = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        const u32x4 z = {0, 0, 0, 0};
+        for (uint64_t j = (wg * BLOCK + tid) * 4; j + 3 < total; j += G * BLOCK * 4)
+            *reinterpret_cast<u32x4 *>(p.iq + j) = z;
+        return;
+    }
+    if (p.probe >= 3) {                         // probe: flat zero stores over the whole output,
+        // workgroup-contiguous spans of (probe == 3 ? chunk : 4 * BLOCK) samples
+        const uint64_t total = (uint64_t)p.n_channels * p.n_samples;
+        const uint64_t span = p.probe == 3 ? p.chunk : 4 * BLOCK;
+        const uint64_t wg = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        const u32x4 z = {0, 0, 0, 0};
+        for (uint64_t b = wg * span; b < total; b += (uint64_t)gridDim.x * gridDim.y * span)
+            for (uint64_t j = b + 4 * tid; j < b + span && j + 3 < total; j += 4 * BLOCK)
+                *reinterpret_cast<u32x4 *>(p.iq + j) = z;
+        return;
+    }
+    if (p.probe == 2) {                         // probe: the grid's zero stores alone
+        uint32_t *o = p.iq + (uint64_t)ch * p.n_samples;
+        const uint32_t z[4] = {0, 0, 0, 0};
+        if (p.ilv) {
+            for (uint32_t j0 = blockIdx.x * 4 * BLOCK + 4 * tid; j0 < p.n_samples; j0 += gridDim.x * 4 * BLOCK)
+                store4(o, j0, p.n_samples, z, p.nt);
+        } else {
+            const uint32_t e = min(blockIdx.x * p.chunk + p.chunk, p.n_samples);
+            for (uint32_t j0 = blockIdx.x * p.chunk + 4 * tid; j0 < e; j0 += 4 * BLOCK) store4(o, j0, e, z, p.nt);
+        }
+        return;
+    }
 
-    for (uint32_t i = tid; i < 4096; i += BLOCK) s_lut[i] = p.sin_lut[i];
+    // ---- prologue: issue every global load of the workgroup up front ----
     uint32_t n_ev = p.summary[8ull * lane + 2];
     n_ev = min(n_ev, p.event_cap);
+    constexpr int EV_PASSES = DDS_MAX_EVENTS / BLOCK;
+    uint4 evr[EV_PASSES];
+    uint32_t ampr[EV_PASSES];
+#pragma unroll
+    for (int ps = 0; ps < EV_PASSES; ps++) {
+        const uint32_t e = ps * BLOCK + tid;
+        evr[ps] = make_uint4(0, 0, 0, 0);
+        ampr[ps] = 0;
+        if (e < n_ev) {
+            evr[ps] = p.ev_main[(uint64_t)e * p.n_lanes + lane];
+            ampr[ps] = p.ev_amp[(uint64_t)e * p.n_lanes + lane];
+        }
+    }
+    for (uint32_t i = tid; i < 4096 / 8; i += BLOCK)
+        reinterpret_cast<uint4 *>(s_lut)[i] = reinterpret_cast<const uint4 *>(p.sin_lut)[i];
+    if (staged) {
+        for (uint32_t i = tid; i < env_len; i += BLOCK) s_env[i] = p.env[env_off + i];
+        for (uint32_t i = tid; i < freq_len; i += BLOCK) s_freq[i] = p.freq[freq_off + i];
+    }
     if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; }
     __syncthreads();
 
     // ---- compact this channel's strobes and the lane's pulse_resets into LDS ----
-    for (uint32_t b = 0; b < n_ev; b += BLOCK) {
-        const uint32_t e = b + tid;
-        uint4 ev = make_uint4(0, 0, 0, 0);
-        uint16_t amp = 0;
-        if (e < n_ev) {
-            ev = p.ev_main[(uint64_t)e * p.n_lanes + lane];
-            amp = p.ev_amp[(uint64_t)e * p.n_lanes + lane];
-        }
+#pragma unroll
+    for (int ps = 0; ps < EV_PASSES; ps++) {
+        if ((uint32_t)ps * BLOCK >= n_ev) break;    // uniform
+        const uint32_t e = ps * BLOCK + tid;
+        const uint4 ev = evr[ps];
         const uint32_t kind = ev.z >> 28;
         const bool is_st = e < n_ev && kind == 0u && ((ev.z >> 24) & 3u) == elem;
         const bool is_rs = e < n_ev && kind == 1u;
@@ -149,7 +322,7 @@ __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
         }
         if (is_st) {
             const uint32_t i = os + (uint32_t)__popcll(bs & below);
-            s_st_t[i] = ev.x; s_st_env[i] = ev.z & 0xFFFFFFu; s_st_pf[i] = ev.w; s_st_amp[i] = amp;
+            s_st_t[i] = ev.x; s_st_env[i] = ev.z & 0xFFFFFFu; s_st_pf[i] = ev.w; s_st_amp[i] = (uint16_t)ampr[ps];
         }
         if (is_rs) s_rs_t[orr + (uint32_t)__popcll(br & below)] = ev.x;
         __syncthreads();
@@ -159,85 +332,41 @@ __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
     const int n_st = (int)s_cnt[0], n_rs = (int)s_cnt[1];
 
     uint32_t *out = p.iq + (uint64_t)ch * p.n_samples;
-    const uint32_t c_begin = blockIdx.x * DDS_CHUNK;
-    const uint32_t c_end = min(c_begin + DDS_CHUNK, p.n_samples);
-    // cursors: latest strobe / reset at or before the current cycle.  A
-    // thread's samples only move forward, so after one binary search at the
-    // first sample the cursors advance by a short linear scan per tile.
-    const uint32_t j_first = c_begin + 4 * tid;
-    const uint32_t n_first = spc_p2 ? (j_first >> spc_sh) : j_first / spc;
-    int si = last_le(s_st_t, n_st, n_first), ri = last_le(s_rs_t, n_rs, n_first);
+    // Chunked: workgroup x owns samples [x * chunk, (x + 1) * chunk) and sweeps
+    // them tile by tile.  Interleaved (p.ilv): workgroup x owns tiles x, x + X,
+    // x + 2X, ... of its channel, so the X workgroups of a channel -- dispatched
+    // together -- write one contiguous, advancing window.
+    const uint32_t X = gridDim.x;
+    const uint32_t c_begin = p.ilv ? 0u : blockIdx.x * p.chunk;
+    const uint32_t c_end = p.ilv ? p.n_samples : min(c_begin + p.chunk, p.n_samples);
+    const uint32_t tstep = p.ilv ? X : 1u;
+    // first sample of this thread for SPT samples per thread
+    auto first = [&](uint32_t spt) { return (p.ilv ? blockIdx.x * spt * BLOCK : c_begin) + spt * tid; };
 
-    const bool quad = (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4) &&
-                      (env_off & 3u) == 0 && (freq_off & 3u) == 0 &&
-                      (((uintptr_t)p.env | (uintptr_t)p.freq) & 15u) == 0;
+    if (p.probe == 1) {                         // probe: prologue, then zero stores
+        const uint32_t z[4] = {0, 0, 0, (uint32_t)(n_st + n_rs) & 0u};
+        for (uint32_t j0 = first(4); j0 < c_end; j0 += tstep * 4 * BLOCK) store4(out, j0, c_end, z, p.nt);
+        return;
+    }
+    const bool quad = staged && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
     if (quad) {
-        // ---- quad sweep: one cycle per thread per tile ----
-        int cur = -2;                                   // strobe whose fields are cached
-        bool act = false;                               // strobe plays (freq entry valid)
-        uint32_t base = 0, lim = 0, emask = 0, F0 = 0, ph15 = 0;
-        int32_t amp = 0;
-        const uint32_t *envp = p.env, *frp = p.freq;
-        for (uint32_t j0 = j_first; j0 < c_end; j0 += 4 * BLOCK) {
-            const uint32_t n = j0 >> spc_sh, k0 = j0 & (spc - 1);
-            while (si + 1 < n_st && s_st_t[si + 1] <= n) si++;
-            while (ri + 1 < n_rs && s_rs_t[ri + 1] <= n) ri++;
-            uint32_t v[4] = {0, 0, 0, 0};
-            if (si != cur) {                            // new pulse: decode its fields once
-                cur = si;
-                act = false;
-                if (si >= 0) {
-                    const uint32_t env_w = s_st_env[si], pf = s_st_pf[si];
-                    const uint32_t A = env_w & 0xFFFu, L = (env_w >> 12) & 0xFFFu, fi = pf >> 17;
-                    base = s_st_t[si] * spc;            // sample index of the strobe
-                    // samples d = j - base with env index (d >> int_sh) & emask inside the
-                    // pulse and the table: d < lim
-                    const uint32_t room = env_len > 4 * A ? env_len - 4 * A : 0u;
-                    if (L) {
-                        emask = 0xFFFFFFFFu;
-                        const uint32_t n_env = min(4 * L, room);
-                        lim = n_env << int_sh;
-                        if ((lim >> int_sh) != n_env) lim = 0xFFFFFFFFu;   // no overflow past 2^32
-                    } else {
-                        emask = 0u;                     // CW: env word 4A forever
-                        lim = room ? 0xFFFFFFFFu : 0u;
-                    }
-                    envp = p.env + env_off + 4 * A;
-                    frp = p.freq + freq_off + 16 * fi;
-                    act = 16 * fi + 15 < freq_len;
-                    F0 = act ? frp[0] : 0u;
-                    ph15 = (pf & 0x1FFFFu) << 15;
-                    amp = s_st_amp[si];
-                }
-            }
-            if (act) {
-                const uint32_t t_ref = ri >= 0 ? s_rs_t[ri] : 0u;
-                const Carrier a0 = carrier(s_lut, F0 * (n - t_ref) + ph15, amp);
-                const uint4 rw = *reinterpret_cast<const uint4 *>(frp + k0);
-                const uint32_t d0 = j0 - base;
-                uint32_t ew[4];
-                if (interp == 1 && d0 + 3 < lim && emask) {
-                    const uint4 e4 = *reinterpret_cast<const uint4 *>(envp + d0);
-                    ew[0] = e4.x; ew[1] = e4.y; ew[2] = e4.z; ew[3] = e4.w;
-                } else {
-#pragma unroll
-                    for (int s = 0; s < 4; s++)
-                        ew[s] = d0 + s < lim ? envp[((d0 + s) >> int_sh) & emask] : 0u;
-                }
-                const uint32_t r[4] = {rw.x, rw.y, rw.z, rw.w};
-#pragma unroll
-                for (int s = 0; s < 4; s++) {
-                    const Carrier a = (k0 + s == 0) ? a0 : rotate(a0, r[s]);
-                    v[s] = d0 + s < lim ? mix(ew[s], a) : 0u;
-                }
-            }
-            store4(out, j0, c_end, v);
-        }
+        const QuadArgs q{s_lut, s_st_t, s_st_env, s_st_pf, s_st_amp, s_rs_t, n_st, n_rs, spc, spc_sh, interp, int_sh,
+                         s_env, env_len, s_freq, freq_len, out, c_end, tstep, p.nt != 0};
+        if ((spc & 7u) == 0 && p.spt8)
+            sweep_quad<8>(q, first(8));
+        else
+            sweep_quad<4>(q, first(4));
         return;
     }
 
     // ---- generic sweep: the per-sample definition ----
-    for (uint32_t j0 = j_first; j0 < c_end; j0 += 4 * BLOCK) {
+    // cursors: latest strobe / reset at or before the current cycle.  A
+    // thread's samples only move forward, so after one binary search at the
+    // first sample the cursors advance by a short linear scan per tile.
+    const uint32_t j_first = first(4);
+    const uint32_t n_first = spc_p2 ? (j_first >> spc_sh) : j_first / spc;
+    int si = last_le(s_st_t, n_st, n_first), ri = last_le(s_rs_t, n_rs, n_first);
+    for (uint32_t j0 = j_first; j0 < c_end; j0 += tstep * 4 * BLOCK) {
         uint32_t v[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
@@ -262,15 +391,36 @@ __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
             }
             v[s] = o;
         }
-        store4(out, j0, c_end, v);
+        store4(out, j0, c_end, v, p.nt);
     }
 }
 
 hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    const uint32_t chunks = (p.n_samples + DDS_CHUNK - 1) / DDS_CHUNK;
-    hipLaunchKernelGGL(dds_kernel, dim3(chunks, p.n_channels), dim3(BLOCK), 0, stream, p);
+    const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
+    if (p.probe == 5) {
+        hipLaunchKernelGGL(dds_kernel, dim3(p.chunk / 64, 1), dim3(BLOCK), dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds),
+                           stream, p);
+        return hipGetLastError();
+    }
+    if (p.probe == 4) {                         // probe: fill-like grid, one 16-B store per thread
+        const uint64_t total = (uint64_t)p.n_channels * p.n_samples;
+        const uint64_t blocks = (total + 4 * BLOCK - 1) / (4 * BLOCK);
+        hipLaunchKernelGGL(dds_kernel, dim3(65535, (uint32_t)((blocks + 65534) / 65535)), dim3(BLOCK), 0, stream, p);
+        return hipGetLastError();
+    }
+    const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds);
+    if (lds > 64 * 1024) {
+        static bool attr = false;               // opt in to > 64 KiB of dynamic LDS once
+        if (!attr) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(dds_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+    }
+    hipLaunchKernelGGL(dds_kernel, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
     return hipGetLastError();
 }
 

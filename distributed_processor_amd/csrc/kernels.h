@@ -71,10 +71,26 @@ struct DDSParams {
     const uint32_t *ch;            // per-channel descriptors, DDS_CH_WORDS u32 each
     uint32_t *iq;                  // [n_channels][n_samples] packed {I16 low, Q16 high}
     uint32_t n_channels, n_lanes, n_samples, event_cap;
+    uint32_t spt8;                 // 8 samples per thread when 8 | spc (tuning knob, DPEMU_DDS_SPT)
+    uint32_t ev_lds;               // compacted-event slots in LDS (>= event_cap, multiple of 8)
+    uint32_t env_lds, freq_lds;    // LDS staging capacity for a channel's env / freq table (words)
+    uint32_t probe;                // measurement probes (DPEMU_DDS_PROBE): 1 = prologue + zero
+                                   // stores, 2 = zero stores only; 0 = normal
+    uint32_t chunk;                // samples per workgroup (multiple of 8 * BLOCK)
+    uint32_t nt;                   // non-temporal (streaming) stores
+    uint32_t ilv;                  // interleaved tile order within a channel
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
 constexpr uint32_t DDS_MAX_EVENTS = 1024;
-constexpr uint32_t DDS_CHUNK = 1u << 16;   // samples per workgroup
+constexpr uint32_t DDS_CHUNK = 1u << 15;   // samples per workgroup (A/B: 32K beats 16K / 64K)
+constexpr uint32_t DDS_ENV_LDS_MAX = 8192;   // words: tables up to 32 KiB are staged in LDS
+constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;  // words: 128 freq entries
+
+// dynamic LDS bytes of dds_kernel
+inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_lds)
+{
+    return 4096 * 2 + ev_lds * 18 + (env_lds + freq_lds) * 4;
+}
 
 hipError_t launch_dds(const DDSParams &p, hipStream_t stream);
 

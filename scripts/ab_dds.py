@@ -1,0 +1,74 @@
+"""Interleaved A/B of DDS kernel variants on the config-5 workload, in ONE
+process, next to a pure streaming-store reference (torch fill of the same
+output buffer) that measures the achievable HBM write bandwidth.
+usage: python scripts/ab_dds.py [rounds] [steps] [n_seq]"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_processor_amd import _abi, workloads  # noqa: E402
+from distributed_processor_amd.dds import ChannelPlan  # noqa: E402
+from distributed_processor_amd.emulator import Emulator, ProgramSet, alloc_device_outputs  # noqa: E402
+
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+n_seq = int(sys.argv[3]) if len(sys.argv) > 3 else 128
+
+ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
+ctx = {}
+VARIANTS = [  # name, spt, probe, chunk, nt, ilv
+    ('spt8_c16k', 8, 0, 16384, 0, 0), ('spt8_c32k', 8, 0, 32768, 0, 0), ('spt8_c8k', 8, 0, 8192, 0, 0),
+    ('spt8_ilv_c16k', 8, 0, 16384, 0, 1), ('spt8_ilv_c32k', 8, 0, 32768, 0, 1), ('spt8_ilv_c64k', 8, 0, 65536, 0, 1),
+    ('spt4_ilv_c16k', 4, 0, 16384, 0, 1),
+    ('zero_c16k', 8, 2, 16384, 0, 0), ('zero_ilv_c16k', 8, 2, 16384, 0, 1), ('zero_ilv_c64k', 8, 2, 65536, 0, 1),
+    ('prologue_ilv_c16k', 8, 1, 16384, 0, 1), ('flat_c16k', 8, 3, 16384, 0, 0), ('flat_c4k', 8, 3, 4096, 0, 0),
+    ('flat_fill_like', 8, 4, 16384, 0, 0), ('persist_1792', 8, 5, 1792 * 64, 0, 0),
+    ('persist_3584', 8, 5, 3584 * 64, 0, 0), ('persist_1024', 8, 5, 1024 * 64, 0, 0)]
+for name, spt, probe, chunk, nt, ilv in VARIANTS:
+    os.environ['DPEMU_DDS_SPT'] = str(spt)
+    os.environ['DPEMU_DDS_PROBE'] = str(probe)
+    os.environ['DPEMU_DDS_CHUNK'] = str(chunk)
+    os.environ['DPEMU_DDS_NT'] = str(nt)
+    os.environ['DPEMU_DDS_ILV'] = str(ilv)
+    ctx[name] = Emulator(0)
+emu = ctx['spt8_c16k']
+emu.load(ps)
+cfg = _abi.make_config(8, n_groups=ps.n_groups, event_cap=512, meas_cap=4)
+ev = alloc_device_outputs(cfg, n_seq, want=('summary', 'ev_main', 'ev_amp'))
+emu.run_device(cfg, n_seq, 0, ev)
+torch.cuda.synchronize()
+t_end = int(ev['summary'][:, 0].max().item())
+n_samples = ((t_end + 8) * 16 + 3) // 4 * 4
+params = {i: (e['samples_per_clk'], e['interp_ratio']) for i, e in enumerate(workloads.ELEMS)}
+plan = ChannelPlan(ps, cfg, 0, n_seq, [(q, c, e) for q in range(n_seq) for c in range(8) for e in (0, 1)], params)
+iq = torch.empty((plan.n_channels, n_samples), dtype=torch.int32, device='cuda')
+ref = None
+stream = torch.cuda.current_stream()
+variants = {k: (lambda e=e: e.synthesize(plan, ev, n_samples, iq, stream)) for k, e in ctx.items()}
+variants['store_only_fill'] = lambda: iq.fill_(0x01020304)
+times = {k: [] for k in variants}
+for r in range(rounds):
+    for k, fn in variants.items():
+        fn()
+        torch.cuda.synchronize()
+        if k.startswith('spt'):
+            h = iq[::97].cpu()
+            if ref is None:
+                ref = h
+            assert torch.equal(ref, h), 'variant {} differs'.format(k)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in evs:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize()
+        times[k] += [a.elapsed_time(b) for a, b in evs]
+nbytes = plan.n_channels * n_samples * 4
+res = {k: {'median_ms': round(float(np.median(v)), 4), 'GB/s': round(nbytes / (float(np.median(v)) * 1e-3) / 1e9, 1)}
+       for k, v in times.items()}
+res['bytes'] = nbytes
+print(json.dumps(res, indent=1))
