@@ -107,15 +107,14 @@ def dds_leg(emu, args, world, rank, stream):
     """time K synthesis steps of config 5; returns the 'dds' sub-object"""
     import torch
     import torch.distributed as dist
-    from distributed_processor_amd import _abi, workloads
+    from distributed_processor_amd import _abi, sharding, workloads
     from distributed_processor_amd.dds import ChannelPlan
     from distributed_processor_amd.emulator import alloc_device_outputs
     ps = dds_workload(args.dds_seqs)
     emu.load(ps)
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=512, meas_cap=4,
                            meas_latency=64, seed=0x5EED)
-    n = args.dds_seqs
-    shot0 = rank * n
+    shot0, n = sharding.weak_shard(args.dds_seqs, rank)
     ev = alloc_device_outputs(cfg, n, want=('summary', 'ev_main', 'ev_amp'))
     emu.run_device(cfg, n, shot0, ev, stream)
     torch.cuda.synchronize()
@@ -143,11 +142,7 @@ def dds_leg(emu, args, world, rank, stream):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device='cuda')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     samples = plan.n_channels * n_samples
     gbs = samples * 4 / (kernel_ms * 1e-3) / 1e9
@@ -196,7 +191,7 @@ def main():
         dist.init_process_group('nccl')
     torch.cuda.set_device(local)
 
-    from distributed_processor_amd import _abi
+    from distributed_processor_amd import _abi, sharding
     from distributed_processor_amd.emulator import Emulator, alloc_device_outputs
 
     ps = build_workload()
@@ -209,7 +204,7 @@ def main():
                            exec_flags=args.exec_flags)
     out = alloc_device_outputs(cfg, n, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'))
     stream = torch.cuda.current_stream()
-    shot0 = rank * n
+    shot0, n = sharding.weak_shard(n, rank)
 
     def step(ev_pair=None):
         out['hist'].zero_()
@@ -218,8 +213,7 @@ def main():
         emu.run_device(cfg, n, shot0, out, stream)
         if ev_pair:
             ev_pair[1].record(stream)
-        if world > 1:
-            dist.all_reduce(out['hist'])
+        sharding.allreduce_histogram(out['hist'])     # the path's only exchange (RCCL)
 
     for _ in range(args.warmup):
         step()
@@ -236,11 +230,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device='cuda')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
 
     # accounting from the last step's outputs (identical every step)

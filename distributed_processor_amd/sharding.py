@@ -1,0 +1,100 @@
+"""Multi-GPU sharding of emulated shots.
+
+Shots are independent units: a shot's C cores interact only through fproc
+and sync, which live inside one wavefront (csrc/interp.hip).  So N ranks --
+one process per GPU, ``torch.distributed`` over RCCL/xGMI -- split the
+global shot range with no exchange on the data path.  Every random counter
+is keyed by the *global* shot index (Philox ctr = shot, core, m), so a shard
+produces exactly the lanes the single-GPU run would, for any N.
+
+The path's only collective is the outcome histogram: ``all_reduce(SUM)`` of
+an int64 [n_groups, 2^C] tensor (100 x 256 x 8 B = 200 KB at config 2).  An
+optional validation gather brings a fixed-size sample of lanes (summaries or
+event slots) to every rank with ``all_gather`` -- equal-size tensors, so one
+RCCL ring call rather than per-rank send/recv.
+
+Nothing here depends on the backend: the same calls run under ``gloo`` on
+CPU tensors (tests/test_dist.py) and ``nccl`` (= RCCL on ROCm) on GPU.
+"""
+
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+
+
+def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
+    """(shot_begin, n_shots) of ``rank`` for strong scaling: contiguous
+    blocks, the first ``n_total % world`` ranks one shot longer."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError('rank {} outside world {}'.format(rank, world))
+    if n_total < 0:
+        raise ValueError('n_total must be >= 0')
+    q, r = divmod(int(n_total), int(world))
+    begin = rank * q + min(rank, r)
+    return begin, q + (1 if rank < r else 0)
+
+
+def weak_shard(shots_per_rank: int, rank: int) -> Tuple[int, int]:
+    """(shot_begin, n_shots) for weak scaling: every rank runs the same
+    number of shots, rank r owning global shots [r*n, (r+1)*n)."""
+    return int(rank) * int(shots_per_rank), int(shots_per_rank)
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def world_size(group=None) -> int:
+    dist = _dist()
+    return dist.get_world_size(group) if dist is not None else 1
+
+
+def allreduce_histogram(hist, group=None):
+    """Sum the int64 outcome histogram over ranks, in place (no-op on one
+    rank).  ``hist``: torch.int64 tensor on the backend's device."""
+    import torch
+    if hist.dtype != torch.int64:
+        raise TypeError('histogram must be int64, got {}'.format(hist.dtype))
+    if world_size(group) > 1:
+        dist = _dist()
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+    return hist
+
+
+def gather_sample(t, group=None):
+    """Every rank's equal-shape tensor ``t`` stacked along a new leading rank
+    axis (one all_gather).  Collects a sampled subset of lanes' timelines or
+    summaries for validation."""
+    import torch
+    if world_size(group) == 1:
+        return t.unsqueeze(0)
+    dist = _dist()
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, t.contiguous(), group=group)
+    return torch.stack(parts)
+
+
+def max_over_ranks(value: float, device=None, group=None) -> float:
+    """The largest ``value`` of any rank (bench timing: the job ends when the
+    slowest rank ends)."""
+    import torch
+    if world_size(group) == 1:
+        return float(value)
+    dist = _dist()
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def sample_lanes(n_shots: int, cores_per_shot: int, n_sample: int) -> np.ndarray:
+    """Local lane indices of ``n_sample`` whole shots spread evenly over a
+    shard of ``n_shots`` (every core of each chosen shot).  The same count on
+    every rank keeps gather_sample's tensors equal-shaped."""
+    if n_shots <= 0 or n_sample <= 0:
+        return np.zeros(0, np.int64)
+    k = min(int(n_sample), int(n_shots))
+    shots = (np.arange(k, dtype=np.int64) * n_shots) // k
+    return (shots[:, None] * cores_per_shot + np.arange(cores_per_shot)[None, :]).reshape(-1)

@@ -1,0 +1,114 @@
+"""The N > 1 path on CPU: world-size-2 ``gloo`` process group.
+
+Each rank emulates its shard of the global shot range and the ranks combine
+outcome histograms with ``sharding.allreduce_histogram`` and a sampled lane
+gather with ``sharding.gather_sample`` -- the same calls bench.py makes over
+RCCL on GPUs.  The per-rank emulation here is oracle_fast (the checker: no
+GPU in this container); the GPU kernel is pinned to it bit for bit by
+tests/test_gpu_parity.py, including a sharding-invariance test at 10^6 shots.
+Rank 0 checks the combined result against one unsharded run.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from distributed_processor_amd import _abi, sharding, workloads
+from distributed_processor_amd.emulator import ProgramSet
+
+N_TOTAL = 1001          # odd: uneven shards
+N_SAMPLE = 7
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _workload():
+    ps = ProgramSet(workloads.config3_active_reset(8))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, meas_cap=4,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, p1=0.37, seed=0xABCD)
+    return ps, cfg
+
+
+def _rank_main(rank, world, port, out_dir):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        ps, cfg = _workload()
+        begin, n = sharding.shard_range(N_TOTAL, rank, world)
+        out = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, begin, n, threads=1,
+                              want=('summary', 'hist'))
+        hist = torch.from_numpy(out['hist'].astype(np.int64))
+        sharding.allreduce_histogram(hist)
+        lanes = sharding.sample_lanes(n, cfg.cores_per_shot, N_SAMPLE)
+        sample = torch.from_numpy(out['summary'][lanes].astype(np.int64))
+        gathered = sharding.gather_sample(sample)
+        slowest = sharding.max_over_ranks(float(rank + 1))
+        if rank == 0:
+            np.save(os.path.join(out_dir, 'hist.npy'), hist.numpy())
+            np.save(os.path.join(out_dir, 'gathered.npy'), gathered.numpy())
+            np.save(os.path.join(out_dir, 'slowest.npy'), np.array([slowest]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    for total in (0, 1, 7, 1000, 1001):
+        for world in (1, 2, 3, 8):
+            spans = [sharding.shard_range(total, r, world) for r in range(world)]
+            assert sum(n for _, n in spans) == total
+            pos = 0
+            for b, n in spans:
+                assert b == pos
+                pos += n
+            assert max(n for _, n in spans) - min(n for _, n in spans) <= 1
+    assert sharding.weak_shard(10 ** 6, 3) == (3 * 10 ** 6, 10 ** 6)
+    with pytest.raises(ValueError):
+        sharding.shard_range(10, 2, 2)
+
+
+def test_sample_lanes_whole_shots():
+    lanes = sharding.sample_lanes(100, 8, 5)
+    assert len(lanes) == 40
+    shots = lanes.reshape(5, 8) // 8
+    assert (shots == shots[:, :1]).all() and len(set(shots[:, 0])) == 5
+    assert (lanes.reshape(5, 8) % 8 == np.arange(8)).all()
+    assert len(sharding.sample_lanes(0, 8, 5)) == 0
+
+
+def test_single_rank_collectives_are_identity():
+    h = torch.arange(6, dtype=torch.int64)
+    assert sharding.allreduce_histogram(h) is h and h.tolist() == list(range(6))
+    assert sharding.gather_sample(h).shape == (1, 6)
+    assert sharding.max_over_ranks(2.5) == 2.5
+    with pytest.raises(TypeError):
+        sharding.allreduce_histogram(torch.zeros(3, dtype=torch.int32))
+
+
+def test_two_rank_gloo_matches_unsharded(tmp_path):
+    world = 2
+    mp.start_processes(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method='spawn')
+    ps, cfg = _workload()
+    full = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, N_TOTAL, threads=2,
+                           want=('summary', 'hist'))
+    hist = np.load(tmp_path / 'hist.npy')
+    assert hist.sum() == N_TOTAL
+    np.testing.assert_array_equal(hist, full['hist'].astype(np.int64))
+    gathered = np.load(tmp_path / 'gathered.npy')
+    assert gathered.shape == (world, N_SAMPLE * 8, 8)
+    for r in range(world):
+        begin, n = sharding.shard_range(N_TOTAL, r, world)
+        lanes = begin * 8 + sharding.sample_lanes(n, 8, N_SAMPLE)
+        np.testing.assert_array_equal(gathered[r], full['summary'][lanes].astype(np.int64))
+    assert float(np.load(tmp_path / 'slowest.npy')[0]) == float(world)
