@@ -40,11 +40,10 @@ struct dpemu_ctx {
     uint32_t *d_ch = nullptr;
     uint32_t ch_cap = 0;
     std::vector<uint32_t> ch_cache;
-    uint32_t dds_spt8 = 1;                  // DPEMU_DDS_SPT=4 forces 4 samples per thread
-    uint32_t dds_probe = 0;                 // DPEMU_DDS_PROBE: kernel measurement probes
+    uint32_t dds_rows = 0;                  // DPEMU_DDS_ROWS: quad rows per thread (1, 2, 4; 0 = contiguous 8)
     uint32_t dds_chunk = DDS_CHUNK;         // DPEMU_DDS_CHUNK: samples per workgroup
-    uint32_t dds_nt = 0;                    // DPEMU_DDS_NT: streaming stores
-    uint32_t dds_ilv = 0;                   // DPEMU_DDS_ILV: interleaved tiles
+    uint32_t dds_probe = 0;                 // DPEMU_DDS_PROBE: store-pattern probes (A/B only)
+    uint32_t dds_lds_pad = 0;               // DPEMU_DDS_LDSPAD: occupancy A/B
     int last_feat = -1;
     // privatised outcome histograms (R replicas, reduced after the interpreter)
     uint32_t *d_hist_rep = nullptr;
@@ -90,14 +89,16 @@ int dpemu_create(int device, dpemu_ctx **out)
     if (hipSetDevice(device) != hipSuccess) return DPEMU_E_DEVICE;
     dpemu_ctx *ctx = new dpemu_ctx();
     ctx->device = device;
-    if (const char *e = getenv("DPEMU_DDS_SPT")) ctx->dds_spt8 = atoi(e) == 8;
-    if (const char *e = getenv("DPEMU_DDS_PROBE")) ctx->dds_probe = (uint32_t)atoi(e);
+    if (const char *e = getenv("DPEMU_DDS_ROWS")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v == 0 || v == 1 || v == 2 || v == 4) ctx->dds_rows = v;
+    }
     if (const char *e = getenv("DPEMU_DDS_CHUNK")) {
         const uint32_t v = (uint32_t)atoi(e);
         if (v >= 8 * BLOCK && (v % (8 * BLOCK)) == 0) ctx->dds_chunk = v;
     }
-    if (const char *e = getenv("DPEMU_DDS_NT")) ctx->dds_nt = atoi(e) != 0;
-    if (const char *e = getenv("DPEMU_DDS_ILV")) ctx->dds_ilv = atoi(e) != 0;
+    if (const char *e = getenv("DPEMU_DDS_PROBE")) ctx->dds_probe = (uint32_t)atoi(e);
+    if (const char *e = getenv("DPEMU_DDS_LDSPAD")) ctx->dds_lds_pad = (uint32_t)atoi(e) & ~15u;
     if (hipMalloc(&ctx->d_thr, DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&ctx->d_lut, 256 * sizeof(uint64_t)) != hipSuccess) {
         delete ctx;
@@ -107,7 +108,7 @@ int dpemu_create(int device, dpemu_ctx **out)
     dpemu_dds_sin_lut(lut.data());
     if (hipMalloc(&ctx->d_sin, 4096 * sizeof(int16_t)) != hipSuccess ||
         hipMemcpy(ctx->d_sin, lut.data(), 4096 * sizeof(int16_t), hipMemcpyHostToDevice) != hipSuccess) {
-        delete ctx;
+        dpemu_destroy(ctx);
         return DPEMU_E_NOMEM;
     }
     *out = ctx;
@@ -452,14 +453,13 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.iq = reinterpret_cast<uint32_t *>(iq_out);
     p.n_channels = ch->n_channels; p.n_lanes = ch->n_lanes; p.n_samples = ch->n_samples;
     p.event_cap = ch->event_cap;
-    p.spt8 = ctx->dds_spt8;
-    p.probe = ctx->dds_probe;
-    p.chunk = ctx->dds_chunk;
-    p.nt = ctx->dds_nt;
-    p.ilv = ctx->dds_ilv;
     p.ev_lds = std::max<uint32_t>(8, (ch->event_cap + 7) & ~7u);
     p.env_lds = (env_max + 3) & ~3u;
     p.freq_lds = (freq_max + 3) & ~3u;
+    p.chunk = ctx->dds_chunk;
+    p.rows = ctx->dds_rows;
+    p.probe = ctx->dds_probe;
+    p.lds_pad = ctx->dds_lds_pad;
     HIPCHK(ctx, launch_dds(p, s));
     return DPEMU_OK;
 }

@@ -1,31 +1,32 @@
 // dds.hip -- fixed-point DDS I/Q synthesis from emulated pulse events (gfx950).
 //
-// Spec: DESIGN.md §DDS and oracle/dds_ref.c (CPU restatement, bit-exact).
+// Spec: DESIGN.md §4.3 and oracle/dds_ref.c (CPU restatement, bit-exact).
 // Inputs are the interpreter's outputs in HBM (lane summaries + slot-major
 // event records) and the assembler's env / freq buffers (asmparse.py:46-86
-// formats).  HBM-write-bound by design: 4 B per output sample; everything
-// else is read once per workgroup into LDS (the channel's events, env and
-// freq tables, the sine table), so the sample loop issues no global loads --
-// on gfx950 stores count in vmcnt, and a load in the loop would make every
-// tile wait for the previous tile's stores.
+// formats).  HBM-write-bound by design: 4 B per output sample.
 //
 // Grid: (sample chunks, channels).  A workgroup compacts its channel's
 // events into LDS -- strobes of the channel's element and pulse_resets, both
-// time-sorted because a core emits them in time order -- then sweeps its
-// chunk in 1024-sample tiles; a thread produces 4 consecutive samples per
-// tile and stores them with one 16-byte global_store_dwordx4 (a wave writes
-// 1 KiB contiguous).
+// time-sorted because a core emits them in time order -- stages the sine
+// table and the channel's env / freq tables there, then sweeps its chunk
+// with no global loads in the loop: on gfx950 stores count in vmcnt, and a
+// load in the loop would make every tile wait for the previous tile's
+// stores.  Everything a pulse needs (env pointer, phase, amp, rotation words)
+// is decoded once per pulse; the carrier once per quad of samples.
 //
-// Two sweeps, chosen per channel:
-//  * quad  (spc % 4 == 0, interp 1 or a power of two >= 4, tables staged in
-//          LDS -- every QubiC element): the 4 (or 8, when 8 | spc) samples
-//          of a thread share one emulated cycle, so theta / carrier /
-//          amplitude are computed once per cycle; strobe fields and the
-//          thread's rotation words (its sub-sample slot never changes) once
-//          per pulse; env words arrive as 16-B LDS reads.  Per sample:
-//          4 v_dot2_i32_i16, 4 shifts, 4 clamps, 3 packs, 1 select.
-//  * generic  (anything else the ABI accepts): the per-sample definition,
-//          reading env / freq tables from global memory.
+// Store layout: thread-contiguous 8 samples (sweep_quad<8>, the default:
+// one carrier per 8 samples) or rows (sweep_rows<R>, DPEMU_DDS_ROWS=R): a
+// thread's quads sit 1024 samples apart, so each store instruction of a
+// wave is 1 KiB dense.  A/B history (scripts/ab_dds.py, config 5, 1.72 GB
+// per launch):
+//   * rows vs contiguous: +5-7 % on bare stores (5.7-5.8 vs 5.45 TB/s), but
+//     -10..-25 % on the real kernel, which is VALU-heavy (~24 VALU lane-ops
+//     per sample before v_cvt_pk_i16_i32) and pays a carrier per quad;
+//   * a two-kernel design -- per-channel pulse-segment tables, then one short
+//     fill-like workgroup per 1-8 KiB tile -- lost (3.2-3.5 TB/s): every tile
+//     paid a chain of dependent table lookups that 8 resident workgroups per
+//     CU cannot hide, while a torch fill of the same buffer reaches 6.9 TB/s;
+//   * 2..7 resident workgroups per CU: within 2 % on bare stores.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,8 +38,7 @@
 namespace dpemu {
 
 // a.lo * b.lo + a.hi * b.hi + c on packed int16 pairs: one VOP3P
-// v_dot2_i32_i16 with the rounding constant in an SGPR (the builtin lowers to
-// v_dot2c + a v_mov of the accumulator per product)
+// v_dot2_i32_i16 with the rounding constant in an SGPR
 __device__ __forceinline__ int32_t dot2(uint32_t a, uint32_t b, int32_t c)
 {
     int32_t r;
@@ -58,20 +58,25 @@ __device__ __forceinline__ uint32_t pack16(int32_t lo, int32_t hi)
 // half.  With X = {lo: -bq, hi: bi} and Y = {lo: bi, hi: bq}:
 //   (a (x) b).re = ai*bi - aq*bq = dot2(a, X),  .im = ai*bq + aq*bi = dot2(a, Y).
 // bq is never -32768 here (table and rotated carriers are symmetric), so -bq
-// fits in int16, and every sum stays inside int32 (DESIGN.md §DDS).
+// fits in int16, and every sum stays inside int32 (DESIGN.md §4.3).
 struct Carrier {
     uint32_t X, Y;
 };
 
-// a0 = (c0 * amp + 2^15) >> 16 from the Q15 table at theta >> 20
+// a0 = (c0 * amp + 2^15) >> 16 from the carrier (cos, sin) = table entries
+__device__ __forceinline__ Carrier carrier_cs(int32_t c, int32_t s, int32_t amp)
+{
+    const int32_t a16 = amp & 0xFFFF;           // |c0| < 2^15, amp < 2^16: v_mad_i32_i24
+    const int32_t ai = (c * a16 + (1 << 15)) >> 16;
+    const int32_t aq = (s * a16 + (1 << 15)) >> 16;
+    return Carrier{pack16(-aq, ai), pack16(ai, aq)};
+}
+
+// from the Q15 table at theta >> 20
 __device__ __forceinline__ Carrier carrier(const int16_t *lut, uint32_t theta, int32_t amp)
 {
     const uint32_t idx = theta >> 20;
-    // |c0| < 2^15, amp < 2^16: v_mad_i32_i24
-    const int32_t a16 = amp & 0xFFFF;
-    const int32_t ai = ((int32_t)lut[(idx + 1024) & 4095] * a16 + (1 << 15)) >> 16;
-    const int32_t aq = ((int32_t)lut[idx] * a16 + (1 << 15)) >> 16;
-    return Carrier{pack16(-aq, ai), pack16(ai, aq)};
+    return carrier_cs(lut[(idx + 1024) & 4095], lut[idx], amp);
 }
 
 // a = symsat((a0 (x) R_k + 2^14) >> 15)
@@ -82,11 +87,14 @@ __device__ __forceinline__ Carrier rotate(Carrier a0, uint32_t rw)
     return Carrier{pack16(-cq, cr), pack16(cr, cq)};
 }
 
-// sat16((env (x) a + 2^14) >> 15), packed {I low, Q high}
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
+// sat16((env (x) a + 2^14) >> 15), packed {I low, Q high}: the two
+// saturations and the pack are one v_cvt_pk_i16_i32
 __device__ __forceinline__ uint32_t mix(uint32_t ew, Carrier a)
 {
-    return pack16(clampi(dot2(ew, a.X, 1 << 14) >> 15, -32768, 32767),
-                  clampi(dot2(ew, a.Y, 1 << 14) >> 15, -32768, 32767));
+    const short2_t r = __builtin_amdgcn_cvt_pk_i16(dot2(ew, a.X, 1 << 14) >> 15, dot2(ew, a.Y, 1 << 14) >> 15);
+    return __builtin_bit_cast(uint32_t, r);
 }
 
 // last index i < n with t[i] <= x, or -1
@@ -102,19 +110,81 @@ __device__ __forceinline__ int last_le(const uint32_t *t, int n, uint32_t x)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void store4(uint32_t *out, uint32_t j0, uint32_t c_end, const uint32_t v[4], bool nt = false)
+__device__ __forceinline__ void store4(uint32_t *out, uint32_t j0, uint32_t c_end, const uint32_t v[4])
 {
     if (j0 + 3 < c_end) {
         const u32x4 w = {v[0], v[1], v[2], v[3]};
-        if (nt)
-            __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(out + j0));
-        else
-            *reinterpret_cast<u32x4 *>(out + j0) = w;
+        *reinterpret_cast<u32x4 *>(out + j0) = w;
     } else {
         for (int s = 0; s < 4 && j0 + s < c_end; s++) out[j0 + s] = v[s];
     }
 }
 
+// ---------------------------------------------------------------------------
+// Event compaction: the channel's strobes (kind 0, cfg & 3 ==
+// elem) and the lane's pulse_resets, in event (= time) order, into LDS.
+// Every global load of the events is issued before the first barrier.
+// ---------------------------------------------------------------------------
+struct Compacted {
+    uint32_t *st_t, *st_env, *st_pf, *rs_t;
+    uint16_t *st_amp;
+};
+
+__device__ __forceinline__ void compact_events(const DDSParams &p, uint32_t lane, uint32_t elem, const Compacted &c,
+                                               uint32_t *s_tmp, uint32_t *s_cnt, int *n_st, int *n_rs)
+{
+    const uint32_t tid = threadIdx.x, wl = tid & 63, wv = tid >> 6;
+    uint32_t n_ev = min(p.summary[8ull * lane + 2], p.event_cap);
+    constexpr int EV_PASSES = DDS_MAX_EVENTS / BLOCK;
+    uint4 evr[EV_PASSES];
+    uint32_t ampr[EV_PASSES];
+#pragma unroll
+    for (int ps = 0; ps < EV_PASSES; ps++) {
+        const uint32_t e = ps * BLOCK + tid;
+        evr[ps] = make_uint4(0, 0, 0, 0);
+        ampr[ps] = 0;
+        if (e < n_ev) {
+            evr[ps] = p.ev_main[(uint64_t)e * p.n_lanes + lane];
+            ampr[ps] = p.ev_amp[(uint64_t)e * p.n_lanes + lane];
+        }
+    }
+    if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; }
+    __syncthreads();
+#pragma unroll
+    for (int ps = 0; ps < EV_PASSES; ps++) {
+        if ((uint32_t)ps * BLOCK >= n_ev) break;    // uniform
+        const uint32_t e = ps * BLOCK + tid;
+        const uint4 ev = evr[ps];
+        const uint32_t kind = ev.z >> 28;
+        const bool is_st = e < n_ev && kind == 0u && ((ev.z >> 24) & 3u) == elem;
+        const bool is_rs = e < n_ev && kind == 1u;
+        const uint64_t bs = __ballot(is_st), br = __ballot(is_rs);
+        const uint64_t below = (wl == 0) ? 0ull : (~0ull >> (64 - wl));
+        if (wl == 0) { s_tmp[wv] = (uint32_t)__popcll(bs); s_tmp[BLOCK / 64 + wv] = (uint32_t)__popcll(br); }
+        __syncthreads();
+        uint32_t os = s_cnt[0], orr = s_cnt[1], ts = 0, tr = 0;
+        for (uint32_t k = 0; k < BLOCK / 64; k++) {
+            os += (k < wv) ? s_tmp[k] : 0u;
+            orr += (k < wv) ? s_tmp[BLOCK / 64 + k] : 0u;
+            ts += s_tmp[k];
+            tr += s_tmp[BLOCK / 64 + k];
+        }
+        if (is_st) {
+            const uint32_t i = os + (uint32_t)__popcll(bs & below);
+            c.st_t[i] = ev.x; c.st_env[i] = ev.z & 0xFFFFFFu; c.st_pf[i] = ev.w; c.st_amp[i] = (uint16_t)ampr[ps];
+        }
+        if (is_rs) c.rs_t[orr + (uint32_t)__popcll(br & below)] = ev.x;
+        __syncthreads();
+        if (tid == 0) { s_cnt[0] += ts; s_cnt[1] += tr; }
+        __syncthreads();
+    }
+    *n_st = (int)s_cnt[0];
+    *n_rs = (int)s_cnt[1];
+}
+
+// ===========================================================================
+// Chunk path
+// ===========================================================================
 struct QuadArgs {
     const int16_t *lut;
     const uint32_t *st_t, *st_env, *st_pf;
@@ -128,8 +198,6 @@ struct QuadArgs {
     uint32_t freq_len;
     uint32_t *out;
     uint32_t c_end;                 // end of this workgroup's samples
-    uint32_t tiles_step;            // tile stride: 1 (chunked) or gridDim.x (interleaved)
-    bool nt;
 };
 
 // Quad sweep: a thread's SPT consecutive samples (SPT | spc) share one
@@ -150,7 +218,7 @@ __device__ __forceinline__ void sweep_quad(const QuadArgs &q, uint32_t j_first)
 #pragma unroll
     for (int s = 0; s < SPT; s++) r[s] = 0;
     const uint32_t *envp = q.env;
-    for (uint32_t j0 = j_first; j0 < q.c_end; j0 += q.tiles_step * (SPT * BLOCK)) {
+    for (uint32_t j0 = j_first; j0 < q.c_end; j0 += SPT * BLOCK) {
         const uint32_t n = j0 >> q.spc_sh;
         while (si + 1 < q.n_st && q.st_t[si + 1] <= n) si++;
         while (ri + 1 < q.n_rs && q.rs_t[ri + 1] <= n) ri++;
@@ -211,15 +279,125 @@ __device__ __forceinline__ void sweep_quad(const QuadArgs &q, uint32_t j_first)
             for (int s = 0; s < SPT; s++) {
                 Carrier a = rotate(a0, r[s]);
                 if (s == 0 && k0 == 0) a = a0;      // sub-sample 0 is the unrotated carrier
-                v[s] = mix(ew[s], a) & (d0 + s < lim ? 0xFFFFFFFFu : 0u);
+                v[s] = mix(ew[s], a);
+            }
+            if (d0 + (SPT - 1) >= lim) {            // the pulse ends inside these samples
+#pragma unroll
+                for (int s = 0; s < SPT; s++) v[s] = d0 + s < lim ? v[s] : 0u;
             }
         }
 #pragma unroll
-        for (int h = 0; h < NV; h++) store4(q.out, j0 + 4 * h, q.c_end, v + 4 * h, q.nt);
+        for (int h = 0; h < NV; h++) store4(q.out, j0 + 4 * h, q.c_end, v + 4 * h);
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
+// Row sweep: per tile iteration a thread produces R quads, quad h at
+// j0 + h * ROW (ROW = 4 * BLOCK samples, a multiple of spc), so every store
+// instruction of a wave writes 1 KiB contiguous -- measured 5-7 % faster
+// for bare stores than the thread-contiguous 32 B of sweep_quad<8>, whose
+// two store instructions each leave every other 16 B of a line for the
+// other (scripts/ab_dds.py probes).  Each row keeps its own pulse cursor.
+struct RowCursor {
+    int si, ri, cur;
+    bool act;
+    uint32_t base, lim, emask, F0, ph15, amp;
+    uint32_t r[4];                  // rotation words R_{k0 .. k0+3}
+    const uint32_t *envp;
+};
+
+__device__ __forceinline__ void row_init(const QuadArgs &q, RowCursor &c, uint32_t j_first)
+{
+    c.si = last_le(q.st_t, q.n_st, j_first >> q.spc_sh);
+    c.ri = last_le(q.rs_t, q.n_rs, j_first >> q.spc_sh);
+    c.cur = -2;
+    c.act = false;
+    c.base = c.lim = c.emask = c.F0 = c.ph15 = c.amp = 0;
+#pragma unroll
+    for (int s = 0; s < 4; s++) c.r[s] = 0;
+    c.envp = q.env;
+}
+
+__device__ __forceinline__ void row_step(const QuadArgs &q, RowCursor &c, uint32_t j0, uint32_t k0, uint32_t v[4])
+{
+    const uint32_t n = j0 >> q.spc_sh;
+    while (c.si + 1 < q.n_st && q.st_t[c.si + 1] <= n) c.si++;
+    while (c.ri + 1 < q.n_rs && q.rs_t[c.ri + 1] <= n) c.ri++;
+#pragma unroll
+    for (int s = 0; s < 4; s++) v[s] = 0;
+    if (c.si != c.cur) {                            // new pulse: decode its fields once
+        c.cur = c.si;
+        c.act = false;
+        if (c.si >= 0) {
+            const uint32_t env_w = q.st_env[c.si], pf = q.st_pf[c.si];
+            const uint32_t A = env_w & 0xFFFu, L = (env_w >> 12) & 0xFFFu, fi = pf >> 17;
+            c.base = q.st_t[c.si] * q.spc;
+            const uint32_t room = q.env_len > 4 * A ? q.env_len - 4 * A : 0u;
+            if (L) {
+                c.emask = 0xFFFFFFFFu;
+                const uint32_t n_env = min(4 * L, room);
+                c.lim = n_env << q.int_sh;
+                if ((c.lim >> q.int_sh) != n_env) c.lim = 0xFFFFFFFFu;
+            } else {
+                c.emask = 0u;
+                c.lim = room ? 0xFFFFFFFFu : 0u;
+            }
+            c.envp = q.env + 4 * A;
+            c.act = 16 * fi + 15 < q.freq_len;
+            if (c.act) {
+                const uint32_t *frp = q.freq + 16 * fi;
+                c.F0 = frp[0];
+                const uint4 rw = *reinterpret_cast<const uint4 *>(frp + k0);
+                c.r[0] = rw.x; c.r[1] = rw.y; c.r[2] = rw.z; c.r[3] = rw.w;
+            }
+            c.ph15 = (pf & 0x1FFFFu) << 15;
+            c.amp = q.st_amp[c.si];
+        }
+    }
+    if (c.act) {
+        const uint32_t t_ref = c.ri >= 0 ? q.rs_t[c.ri] : 0u;
+        const Carrier a0 = carrier(q.lut, c.F0 * (n - t_ref) + c.ph15, (int32_t)c.amp);
+        uint32_t ew[4];
+        const uint32_t d0 = j0 - c.base;
+        if (q.interp == 1 && d0 + 3 < c.lim && c.emask) {
+            const uint4 e4 = *reinterpret_cast<const uint4 *>(c.envp + d0);
+            ew[0] = e4.x; ew[1] = e4.y; ew[2] = e4.z; ew[3] = e4.w;
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; s++) ew[s] = d0 + s < c.lim ? c.envp[((d0 + s) >> q.int_sh) & c.emask] : 0u;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            Carrier a = rotate(a0, c.r[s]);
+            if (s == 0 && k0 == 0) a = a0;          // sub-sample 0 is the unrotated carrier
+            v[s] = mix(ew[s], a);
+        }
+        if (d0 + 3 >= c.lim) {
+#pragma unroll
+            for (int s = 0; s < 4; s++) v[s] = d0 + s < c.lim ? v[s] : 0u;
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void sweep_rows(const QuadArgs &q, uint32_t c_begin)
+{
+    constexpr uint32_t ROW = 4 * BLOCK;
+    const uint32_t j_first = c_begin + 4 * threadIdx.x;
+    const uint32_t k0 = j_first & (q.spc - 1);      // the same in every row and tile
+    RowCursor c[R];
+#pragma unroll
+    for (int h = 0; h < R; h++) row_init(q, c[h], j_first + h * ROW);
+    for (uint32_t j0 = j_first; j0 < q.c_end; j0 += R * ROW) {
+        uint32_t v[R][4];
+#pragma unroll
+        for (int h = 0; h < R; h++) row_step(q, c[h], j0 + h * ROW, k0, v[h]);
+#pragma unroll
+        for (int h = 0; h < R; h++)
+            if (j0 + h * ROW < q.c_end) store4(q.out, j0 + h * ROW, q.c_end, v[h]);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
 {
     // dynamic LDS (dds_lds_bytes): sine table | compacted strobes / resets |
     // staged env table | staged freq table
@@ -235,7 +413,7 @@ __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
     __shared__ uint32_t s_tmp[2 * (BLOCK / 64)];
     __shared__ uint32_t s_cnt[2];
 
-    const uint32_t tid = threadIdx.x, wl = tid & 63, wv = tid >> 6;
+    const uint32_t tid = threadIdx.x;
     const uint32_t ch = blockIdx.y;
     const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
     const uint32_t lane = d[0], elem = d[1], spc = d[2], interp = d[3] ? d[3] : 1u;
@@ -243,119 +421,49 @@ __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
     const uint32_t spc_sh = __ffs(spc) - 1, int_sh = __ffs(interp) - 1;
     const bool staged = env_len <= p.env_lds && freq_len <= p.freq_lds;
-    if (p.probe == 5) {                         // probe: persistent grid, flattened 4-KiB tiles
-        const uint64_t total = (uint64_t)p.n_channels * p.n_samples;
-        const uint64_t G = (uint64_t)gridDim.x * gridDim.y, wg = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
-        const u32x4 z = {0, 0, 0, 0};
-        for (uint64_t j = (wg * BLOCK + tid) * 4; j + 3 < total; j += G * BLOCK * 4)
-            *reinterpret_cast<u32x4 *>(p.iq + j) = z;
-        return;
-    }
-    if (p.probe >= 3) {                         // probe: flat zero stores over the whole output,
-        // workgroup-contiguous spans of (probe == 3 ? chunk : 4 * BLOCK) samples
-        const uint64_t total = (uint64_t)p.n_channels * p.n_samples;
-        const uint64_t span = p.probe == 3 ? p.chunk : 4 * BLOCK;
-        const uint64_t wg = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
-        const u32x4 z = {0, 0, 0, 0};
-        for (uint64_t b = wg * span; b < total; b += (uint64_t)gridDim.x * gridDim.y * span)
-            for (uint64_t j = b + 4 * tid; j < b + span && j + 3 < total; j += 4 * BLOCK)
-                *reinterpret_cast<u32x4 *>(p.iq + j) = z;
-        return;
-    }
-    if (p.probe == 2) {                         // probe: the grid's zero stores alone
-        uint32_t *o = p.iq + (uint64_t)ch * p.n_samples;
-        const uint32_t z[4] = {0, 0, 0, 0};
-        if (p.ilv) {
-            for (uint32_t j0 = blockIdx.x * 4 * BLOCK + 4 * tid; j0 < p.n_samples; j0 += gridDim.x * 4 * BLOCK)
-                store4(o, j0, p.n_samples, z, p.nt);
-        } else {
-            const uint32_t e = min(blockIdx.x * p.chunk + p.chunk, p.n_samples);
-            for (uint32_t j0 = blockIdx.x * p.chunk + 4 * tid; j0 < e; j0 += 4 * BLOCK) store4(o, j0, e, z, p.nt);
-        }
-        return;
-    }
 
-    // ---- prologue: issue every global load of the workgroup up front ----
-    uint32_t n_ev = p.summary[8ull * lane + 2];
-    n_ev = min(n_ev, p.event_cap);
-    constexpr int EV_PASSES = DDS_MAX_EVENTS / BLOCK;
-    uint4 evr[EV_PASSES];
-    uint32_t ampr[EV_PASSES];
-#pragma unroll
-    for (int ps = 0; ps < EV_PASSES; ps++) {
-        const uint32_t e = ps * BLOCK + tid;
-        evr[ps] = make_uint4(0, 0, 0, 0);
-        ampr[ps] = 0;
-        if (e < n_ev) {
-            evr[ps] = p.ev_main[(uint64_t)e * p.n_lanes + lane];
-            ampr[ps] = p.ev_amp[(uint64_t)e * p.n_lanes + lane];
-        }
-    }
+    // prologue: every global load of the workgroup up front (compact_events
+    // issues the event loads before its first barrier)
     for (uint32_t i = tid; i < 4096 / 8; i += BLOCK)
         reinterpret_cast<uint4 *>(s_lut)[i] = reinterpret_cast<const uint4 *>(p.sin_lut)[i];
     if (staged) {
         for (uint32_t i = tid; i < env_len; i += BLOCK) s_env[i] = p.env[env_off + i];
         for (uint32_t i = tid; i < freq_len; i += BLOCK) s_freq[i] = p.freq[freq_off + i];
     }
-    if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; }
-    __syncthreads();
-
-    // ---- compact this channel's strobes and the lane's pulse_resets into LDS ----
-#pragma unroll
-    for (int ps = 0; ps < EV_PASSES; ps++) {
-        if ((uint32_t)ps * BLOCK >= n_ev) break;    // uniform
-        const uint32_t e = ps * BLOCK + tid;
-        const uint4 ev = evr[ps];
-        const uint32_t kind = ev.z >> 28;
-        const bool is_st = e < n_ev && kind == 0u && ((ev.z >> 24) & 3u) == elem;
-        const bool is_rs = e < n_ev && kind == 1u;
-        const uint64_t bs = __ballot(is_st), br = __ballot(is_rs);
-        const uint64_t below = (wl == 0) ? 0ull : (~0ull >> (64 - wl));
-        if (wl == 0) { s_tmp[wv] = (uint32_t)__popcll(bs); s_tmp[BLOCK / 64 + wv] = (uint32_t)__popcll(br); }
-        __syncthreads();
-        uint32_t os = s_cnt[0], orr = s_cnt[1], ts = 0, tr = 0;
-        for (uint32_t k = 0; k < BLOCK / 64; k++) {
-            os += (k < wv) ? s_tmp[k] : 0u;
-            orr += (k < wv) ? s_tmp[BLOCK / 64 + k] : 0u;
-            ts += s_tmp[k];
-            tr += s_tmp[BLOCK / 64 + k];
-        }
-        if (is_st) {
-            const uint32_t i = os + (uint32_t)__popcll(bs & below);
-            s_st_t[i] = ev.x; s_st_env[i] = ev.z & 0xFFFFFFu; s_st_pf[i] = ev.w; s_st_amp[i] = (uint16_t)ampr[ps];
-        }
-        if (is_rs) s_rs_t[orr + (uint32_t)__popcll(br & below)] = ev.x;
-        __syncthreads();
-        if (tid == 0) { s_cnt[0] += ts; s_cnt[1] += tr; }
-        __syncthreads();
-    }
-    const int n_st = (int)s_cnt[0], n_rs = (int)s_cnt[1];
+    int n_st, n_rs;
+    compact_events(p, lane, elem, Compacted{s_st_t, s_st_env, s_st_pf, s_rs_t, s_st_amp}, s_tmp, s_cnt,
+                   &n_st, &n_rs);
 
     uint32_t *out = p.iq + (uint64_t)ch * p.n_samples;
-    // Chunked: workgroup x owns samples [x * chunk, (x + 1) * chunk) and sweeps
-    // them tile by tile.  Interleaved (p.ilv): workgroup x owns tiles x, x + X,
-    // x + 2X, ... of its channel, so the X workgroups of a channel -- dispatched
-    // together -- write one contiguous, advancing window.
-    const uint32_t X = gridDim.x;
-    const uint32_t c_begin = p.ilv ? 0u : blockIdx.x * p.chunk;
-    const uint32_t c_end = p.ilv ? p.n_samples : min(c_begin + p.chunk, p.n_samples);
-    const uint32_t tstep = p.ilv ? X : 1u;
-    // first sample of this thread for SPT samples per thread
-    auto first = [&](uint32_t spt) { return (p.ilv ? blockIdx.x * spt * BLOCK : c_begin) + spt * tid; };
-
-    if (p.probe == 1) {                         // probe: prologue, then zero stores
+    const uint32_t c_begin = blockIdx.x * p.chunk;
+    const uint32_t c_end = min(c_begin + p.chunk, p.n_samples);
+    if (p.probe >= 3) {          // probes: zero stores of the sweep, 8 samples per thread per tile
         const uint32_t z[4] = {0, 0, 0, (uint32_t)(n_st + n_rs) & 0u};
-        for (uint32_t j0 = first(4); j0 < c_end; j0 += tstep * 4 * BLOCK) store4(out, j0, c_end, z, p.nt);
+        if (p.probe == 3) {      // thread-contiguous 32 B (two half-dense store instructions)
+            for (uint32_t j0 = c_begin + 8 * tid; j0 < c_end; j0 += 8 * BLOCK) {
+                store4(out, j0, c_end, z);
+                store4(out, j0 + 4, c_end, z);
+            }
+        } else {                 // rows: each store instruction dense (1 KiB per wave)
+            for (uint32_t j0 = c_begin + 4 * tid; j0 < c_end; j0 += 8 * BLOCK) {
+                store4(out, j0, c_end, z);
+                store4(out, j0 + 4 * BLOCK, c_end, z);
+            }
+        }
         return;
     }
     const bool quad = staged && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
     if (quad) {
         const QuadArgs q{s_lut, s_st_t, s_st_env, s_st_pf, s_st_amp, s_rs_t, n_st, n_rs, spc, spc_sh, interp, int_sh,
-                         s_env, env_len, s_freq, freq_len, out, c_end, tstep, p.nt != 0};
-        if ((spc & 7u) == 0 && p.spt8)
-            sweep_quad<8>(q, first(8));
-        else
-            sweep_quad<4>(q, first(4));
+                         s_env, env_len, s_freq, freq_len, out, c_end};
+        switch (p.rows) {
+        case 1: sweep_rows<1>(q, c_begin); break;
+        case 2: sweep_rows<2>(q, c_begin); break;
+        case 4: sweep_rows<4>(q, c_begin); break;
+        default:
+            if ((spc & 7u) == 0) sweep_quad<8>(q, c_begin + 8 * tid);
+            else sweep_quad<4>(q, c_begin + 4 * tid);
+        }
         return;
     }
 
@@ -363,10 +471,10 @@ __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
     // cursors: latest strobe / reset at or before the current cycle.  A
     // thread's samples only move forward, so after one binary search at the
     // first sample the cursors advance by a short linear scan per tile.
-    const uint32_t j_first = first(4);
+    const uint32_t j_first = c_begin + 4 * tid;
     const uint32_t n_first = spc_p2 ? (j_first >> spc_sh) : j_first / spc;
     int si = last_le(s_st_t, n_st, n_first), ri = last_le(s_rs_t, n_rs, n_first);
-    for (uint32_t j0 = j_first; j0 < c_end; j0 += tstep * 4 * BLOCK) {
+    for (uint32_t j0 = j_first; j0 < c_end; j0 += 4 * BLOCK) {
         uint32_t v[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
@@ -391,36 +499,28 @@ __global__ void __launch_bounds__(BLOCK) dds_kernel(const DDSParams p)
             }
             v[s] = o;
         }
-        store4(out, j0, c_end, v, p.nt);
+        store4(out, j0, c_end, v);
     }
+}
+
+// dynamic LDS above 64 KiB needs an opt-in per kernel, raised as requests grow
+static hipError_t opt_in_lds(const void *fn, uint32_t bytes, uint32_t *granted)
+{
+    if (bytes <= 64 * 1024 || bytes <= *granted) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) *granted = bytes;
+    return e;
 }
 
 hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
     const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
-    if (p.probe == 5) {
-        hipLaunchKernelGGL(dds_kernel, dim3(p.chunk / 64, 1), dim3(BLOCK), dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds),
-                           stream, p);
-        return hipGetLastError();
-    }
-    if (p.probe == 4) {                         // probe: fill-like grid, one 16-B store per thread
-        const uint64_t total = (uint64_t)p.n_channels * p.n_samples;
-        const uint64_t blocks = (total + 4 * BLOCK - 1) / (4 * BLOCK);
-        hipLaunchKernelGGL(dds_kernel, dim3(65535, (uint32_t)((blocks + 65534) / 65535)), dim3(BLOCK), 0, stream, p);
-        return hipGetLastError();
-    }
-    const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds);
-    if (lds > 64 * 1024) {
-        static bool attr = false;               // opt in to > 64 KiB of dynamic LDS once
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(dds_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
-    }
-    hipLaunchKernelGGL(dds_kernel, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
+    const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) + p.lds_pad;
+    static uint32_t granted = 0;
+    const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_chunk_kernel), lds, &granted);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(dds_chunk_kernel, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
     return hipGetLastError();
 }
 

@@ -111,30 +111,6 @@ __device__ __forceinline__ uint32_t group_step(const KParams &p, uint32_t sp, ui
     return (uint32_t)(a - b);
 }
 
-// exclusive block scan of v (BLOCK threads); returns the prefix, *total the sum
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *s_tmp, uint32_t *total)
-{
-    const uint32_t tid = threadIdx.x, wl = tid & 63, wv = tid >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-        if (wl >= (uint32_t)o) x += y;
-    }
-    if (wl == 63) s_tmp[wv] = x;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < BLOCK / 64; k++) {
-        const uint32_t t = s_tmp[k];
-        off += (k < wv) ? t : 0u;
-        tot += t;
-    }
-    __syncthreads();
-    *total = tot;
-    return off + x - v;
-}
-
 template <int FEAT>
 __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 {

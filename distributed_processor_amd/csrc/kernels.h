@@ -12,6 +12,30 @@ constexpr uint32_t BLOCK = 256;                 // 4 wavefronts per workgroup
 constexpr uint32_t MEAS_LOOKUP = DPEMU_MEAS_LOOKUP;
 constexpr uint32_t LUT_FIRE_CAP = DPEMU_LUT_FIRE_CAP;
 
+// exclusive block scan of v (BLOCK threads); returns the prefix, *total the sum
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *s_tmp, uint32_t *total)
+{
+    const uint32_t tid = threadIdx.x, wl = tid & 63, wv = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (wl >= (uint32_t)o) x += y;
+    }
+    if (wl == 63) s_tmp[wv] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < BLOCK / 64; k++) {
+        const uint32_t t = s_tmp[k];
+        off += (k < wv) ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + x - v;
+}
+
 // kernel specialisations, chosen per run from the opcodes the programs use
 constexpr int FEAT_FPROC = 1;   // fproc_meas reads (ALU_FPROC / JUMP_FPROC)
 constexpr int FEAT_SYNC = 2;    // SYNC barriers
@@ -67,26 +91,25 @@ struct DDSParams {
     const uint4 *ev_main;
     const uint16_t *ev_amp;
     const uint32_t *env, *freq;
-    const int16_t *sin_lut;
+    const int16_t *sin_lut;        // Q15 sine table [4096]
     const uint32_t *ch;            // per-channel descriptors, DDS_CH_WORDS u32 each
     uint32_t *iq;                  // [n_channels][n_samples] packed {I16 low, Q16 high}
     uint32_t n_channels, n_lanes, n_samples, event_cap;
-    uint32_t spt8;                 // 8 samples per thread when 8 | spc (tuning knob, DPEMU_DDS_SPT)
     uint32_t ev_lds;               // compacted-event slots in LDS (>= event_cap, multiple of 8)
     uint32_t env_lds, freq_lds;    // LDS staging capacity for a channel's env / freq table (words)
-    uint32_t probe;                // measurement probes (DPEMU_DDS_PROBE): 1 = prologue + zero
-                                   // stores, 2 = zero stores only; 0 = normal
     uint32_t chunk;                // samples per workgroup (multiple of 8 * BLOCK)
-    uint32_t nt;                   // non-temporal (streaming) stores
-    uint32_t ilv;                  // interleaved tile order within a channel
+    uint32_t rows;                 // quad rows per thread per tile (1, 2, 4); 0 = 8 contiguous samples
+    uint32_t probe;                // measurement probes (DPEMU_DDS_PROBE): 3 / 4 = bare stores,
+                                   // thread-contiguous / rows layout; 0 = normal
+    uint32_t lds_pad;              // extra dynamic LDS per workgroup (DPEMU_DDS_LDSPAD, occupancy A/B)
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
 constexpr uint32_t DDS_MAX_EVENTS = 1024;
-constexpr uint32_t DDS_CHUNK = 1u << 15;   // samples per workgroup (A/B: 32K beats 16K / 64K)
+constexpr uint32_t DDS_CHUNK = 1u << 15;   // samples per workgroup
 constexpr uint32_t DDS_ENV_LDS_MAX = 8192;   // words: tables up to 32 KiB are staged in LDS
 constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;  // words: 128 freq entries
 
-// dynamic LDS bytes of dds_kernel
+// dynamic LDS bytes of dds_chunk_kernel
 inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_lds)
 {
     return 4096 * 2 + ev_lds * 18 + (env_lds + freq_lds) * 4;

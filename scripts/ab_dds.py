@@ -1,6 +1,6 @@
-"""Interleaved A/B of DDS kernel variants on the config-5 workload, in ONE
-process, next to a pure streaming-store reference (torch fill of the same
-output buffer) that measures the achievable HBM write bandwidth.
+"""Interleaved A/B of the DDS paths on the config-5 workload, in ONE process,
+next to a pure streaming-store reference (torch fill of the same output
+buffer) that measures the achievable HBM write bandwidth.
 usage: python scripts/ab_dds.py [rounds] [steps] [n_seq]"""
 import json
 import os
@@ -20,22 +20,17 @@ n_seq = int(sys.argv[3]) if len(sys.argv) > 3 else 128
 
 ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
 ctx = {}
-VARIANTS = [  # name, spt, probe, chunk, nt, ilv
-    ('spt8_c16k', 8, 0, 16384, 0, 0), ('spt8_c32k', 8, 0, 32768, 0, 0), ('spt8_c8k', 8, 0, 8192, 0, 0),
-    ('spt8_ilv_c16k', 8, 0, 16384, 0, 1), ('spt8_ilv_c32k', 8, 0, 32768, 0, 1), ('spt8_ilv_c64k', 8, 0, 65536, 0, 1),
-    ('spt4_ilv_c16k', 4, 0, 16384, 0, 1),
-    ('zero_c16k', 8, 2, 16384, 0, 0), ('zero_ilv_c16k', 8, 2, 16384, 0, 1), ('zero_ilv_c64k', 8, 2, 65536, 0, 1),
-    ('prologue_ilv_c16k', 8, 1, 16384, 0, 1), ('flat_c16k', 8, 3, 16384, 0, 0), ('flat_c4k', 8, 3, 4096, 0, 0),
-    ('flat_fill_like', 8, 4, 16384, 0, 0), ('persist_1792', 8, 5, 1792 * 64, 0, 0),
-    ('persist_3584', 8, 5, 3584 * 64, 0, 0), ('persist_1024', 8, 5, 1024 * 64, 0, 0)]
-for name, spt, probe, chunk, nt, ilv in VARIANTS:
-    os.environ['DPEMU_DDS_SPT'] = str(spt)
+VARIANTS = [  # name, rows, chunk, probe, lds pad
+    ('contig8_c32k_default', 0, 32768, 0, 0), ('rows1_c32k', 1, 32768, 0, 0),
+    ('contig8_c16k', 0, 16384, 0, 0), ('contig8_c64k', 0, 65536, 0, 0),
+    ('probe_rows_stores', 2, 32768, 4, 0), ('probe_contig_stores', 2, 32768, 3, 0)]
+for name, rows, chunk, probe, pad in VARIANTS:
+    os.environ['DPEMU_DDS_LDSPAD'] = str(pad)
     os.environ['DPEMU_DDS_PROBE'] = str(probe)
+    os.environ['DPEMU_DDS_ROWS'] = str(rows)
     os.environ['DPEMU_DDS_CHUNK'] = str(chunk)
-    os.environ['DPEMU_DDS_NT'] = str(nt)
-    os.environ['DPEMU_DDS_ILV'] = str(ilv)
     ctx[name] = Emulator(0)
-emu = ctx['spt8_c16k']
+emu = ctx['contig8_c32k_default']
 emu.load(ps)
 cfg = _abi.make_config(8, n_groups=ps.n_groups, event_cap=512, meas_cap=4)
 ev = alloc_device_outputs(cfg, n_seq, want=('summary', 'ev_main', 'ev_amp'))
@@ -55,7 +50,7 @@ for r in range(rounds):
     for k, fn in variants.items():
         fn()
         torch.cuda.synchronize()
-        if k.startswith('spt'):
+        if not k.startswith(('store_only', 'probe')):
             h = iq[::97].cpu()
             if ref is None:
                 ref = h

@@ -19,12 +19,9 @@ lin = ProgramSet(workloads.config1_linear())
 rst = ProgramSet(workloads.config3_active_reset(8))
 OUT = ('summary', 'ev_main', 'ev_amp', 'meas', 'hist')
 variants = {
-    'ramsey_spg1': (ramsey, dict(n_groups=100), OUT),
-    'ramsey_spg1_nohist': (ramsey, dict(n_groups=100), OUT[:-1]),
-    'ramsey_spg1_repl': (ramsey, dict(n_groups=100, exec_flags=_abi.X_HIST_REPL), OUT),
-    'ramsey_spg1_lds_gm': (ramsey, dict(n_groups=100, exec_flags=_abi.X_PROG_LDS | _abi.X_GROUP_MAJOR), OUT),
-    'ramsey_spg1e4': (ramsey, dict(n_groups=100, shots_per_group=10000), OUT),
-    'ramsey_spg1e4_direct': (ramsey, dict(n_groups=100, shots_per_group=10000, exec_flags=_abi.X_HIST_DIRECT), OUT),
+    'ramsey': (ramsey, dict(n_groups=100), OUT),
+    'ramsey_nohist': (ramsey, dict(n_groups=100), OUT[:-1]),
+    'ramsey_summary_only': (ramsey, dict(n_groups=100), ('summary',)),
     'config1_linear_8e6': (lin, dict(), OUT),
     'config3_reset': (rst, dict(meas_latency=workloads.CONFIG3_MEAS_LATENCY, max_cycles=1 << 16, event_cap=16,
                                 meas_cap=4), OUT),

@@ -27,6 +27,28 @@ def emu():
     e.close()
 
 
+def make_emu(rows):
+    """an Emulator whose DDS sweep uses `rows` quad rows per thread (0 = eight
+    contiguous samples); DPEMU_DDS_ROWS is read once, at dpemu_create"""
+    import os
+    old = os.environ.get('DPEMU_DDS_ROWS')
+    os.environ['DPEMU_DDS_ROWS'] = str(rows)
+    try:
+        return Emulator(0)
+    finally:
+        if old is None:
+            os.environ.pop('DPEMU_DDS_ROWS', None)
+        else:
+            os.environ['DPEMU_DDS_ROWS'] = old
+
+
+@pytest.fixture(scope='module', params=[0, 1, 2, 4], ids=lambda r: 'rows{}'.format(r))
+def emu_path(request):
+    e = make_emu(request.param)
+    yield e
+    e.close()
+
+
 def host(t):
     return t.cpu().numpy()
 
@@ -148,3 +170,91 @@ def test_bad_arguments_fail_loudly(emu):
     plan._cols['spc'] = np.ascontiguousarray(plan.desc[:, 2])
     with pytest.raises(DpemuError):
         emu.synthesize(plan, out, 1024)               # spc out of range
+
+
+def synthetic_timelines(rng, n_lanes, cap, n_cycles, env_len, n_freq):
+    """random, time-sorted event arrays: strobes on elements 0-3 (some CW, some
+    past the window), pulse_resets (some inside pulses), ragged counts, an
+    overflowed lane and an empty lane"""
+    summary = np.zeros((n_lanes, 8), np.uint32)
+    ev = np.zeros((cap, n_lanes, 4), np.uint32)
+    amp = np.zeros((cap, n_lanes), np.uint16)
+    for L in range(1, n_lanes):                     # lane 0 stays empty
+        n = cap if L == 2 else cap - 2 * L
+        t = np.sort(rng.integers(0, n_cycles, n)).astype(np.uint32)
+        t[-2:] = n_cycles + np.array([5, 10 ** 6], np.uint32)      # past the window
+        kind = (rng.random(n) < 0.2).astype(np.uint32)
+        A = rng.integers(0, env_len // 4 + 2, n)                  # some past the table end
+        Ln = rng.integers(0, 6, n)                                # 0 = CW
+        envw = (A | (Ln << 12)).astype(np.uint32)
+        cfgw = rng.integers(0, 4, n).astype(np.uint32)
+        ev[:n, L, 0] = t
+        ev[:n, L, 1] = t
+        ev[:n, L, 2] = envw | (cfgw << 24) | (kind << 28)
+        ev[:n, L, 3] = (rng.integers(0, 1 << 17, n).astype(np.uint32)
+                        | (rng.integers(0, n_freq + 1, n).astype(np.uint32) << 17))   # n_freq: no entry
+        amp[:n, L] = rng.integers(0, 65536, n)
+        summary[L, 2] = n + (7 if L == 2 else 0)    # lane 2 overflowed: count > cap
+    return summary, ev, amp
+
+
+def plan_from(desc, env_tab, freq_tab, n_lanes, cap):
+    plan = ChannelPlan.__new__(ChannelPlan)
+    plan.desc, plan.env, plan.freq = desc, env_tab, freq_tab
+    plan.n_lanes, plan.event_cap, plan._dev = n_lanes, cap, None
+    plan._cols = {f: np.ascontiguousarray(desc[:, i]) for i, f in
+                  enumerate(('ch_lane', 'ch_elem', 'spc', 'interp', 'env_off', 'env_len', 'freq_off', 'freq_len'))}
+    return plan
+
+
+@pytest.mark.parametrize('spcs', [(16, 16, 16, 16), (16, 8, 4, 16)], ids=['spc16', 'spc_mixed'])
+def test_sweep_edges(emu_path, spcs):
+    """every pulse rule against oracle_dds on every sweep variant: CW, pulse
+    end inside a thread's samples (odd env lengths), non-power-of-two interp
+    (generic sweep), resets inside pulses, odd env / freq offsets, missing
+    freq entries, env words past the table, ragged tail, overflowed and empty
+    lanes"""
+    import torch
+    rng = np.random.default_rng(11)
+    cap, n_lanes, n_cycles = 48, 6, 9000
+    env_tab = pack_iq16(np.exp(1j * rng.uniform(0, 2 * np.pi, 301)) * rng.uniform(0, 1, 301))
+    freq_tab = np.concatenate([np.zeros(3, np.uint32)] + [DDSElementConfig(samples_per_clk=16).get_freq_buffer([f])
+                              for f in (91.7e6, -13.1e6, 250e6)])
+    summary, ev, amp = synthetic_timelines(rng, n_lanes, cap, n_cycles, 280, 3)
+    desc = []
+    for L in range(n_lanes):
+        for e, spc in enumerate(spcs):
+            interp = (1, 3, 16, 2)[e]
+            env_off = (0, 1, 5, 2)[e]                       # odd offsets: unaligned env reads
+            env_len = (280, 279, 290, 301 - 2)[e]           # not multiples of 4
+            desc.append((L, e, spc, interp, env_off, env_len, 3 if e % 2 else 1, len(freq_tab) - 3))
+    desc = np.array(desc, np.uint32)
+    n_samples = 16 * n_cycles + 4 * 37                   # ragged last tile
+    ref = oracle.dds(desc, summary, ev, amp, env_tab, freq_tab, n_samples, cap)
+    dev = {'summary': torch.from_numpy(summary.view(np.int32)).cuda(),
+           'ev_main': torch.from_numpy(ev.view(np.int32)).cuda(),
+           'ev_amp': torch.from_numpy(amp.view(np.int16)).cuda()}
+    iq = emu_path.synthesize(plan_from(desc, env_tab, freq_tab, n_lanes, cap), dev, n_samples)
+    torch.cuda.synchronize()
+    check_equal(host(iq), ref, 'sweep edges')
+    assert (ref != 0).sum() > 10000
+
+
+def test_paths_agree_on_config5_slice(emu_path):
+    """the bench's config-5 shape (RB timelines, qdrv + rdrv at 16 samples/clk)
+    on a few sequences, full length, against oracle_dds"""
+    ps = ProgramSet(workloads.config4_rb(n_seq=4, depth=200, n_cores=8))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, event_cap=512, meas_cap=4)
+    ch = [(q, c, e) for q in range(4) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
+    import torch
+    emu_path.load(ps)
+    out = alloc_device_outputs(cfg, 4, want=('summary', 'ev_main', 'ev_amp'))
+    emu_path.run_device(cfg, 4, 0, out)
+    torch.cuda.synchronize()
+    n_samples = ((int(out['summary'][:, 0].max().item()) + 8) * 16 + 3) // 4 * 4
+    plan = ChannelPlan(ps, cfg, 0, 4, ch, ELEM_PARAMS)
+    iq = emu_path.synthesize(plan, out, n_samples)
+    torch.cuda.synchronize()
+    ref = oracle.dds(plan.desc, host(out['summary']), host(out['ev_main']), host(out['ev_amp']),
+                     plan.env, plan.freq, n_samples, cfg.event_cap, threads=8)
+    check_equal(host(iq), ref, 'config5 slice')
