@@ -18,6 +18,7 @@ X_PROG_LDS = 0x1
 X_GROUP_MAJOR = 0x2
 X_HIST_DIRECT = 0x4
 X_HIST_REPL = 0x8
+X_PROG_MAJOR = 0x10
 
 STATUS_NAMES = {0: 'running', ST_DONE: 'done', ST_MAX_CYCLES: 'max_cycles',
                 ST_HUNG_OPCODE: 'hung_opcode', ST_DEADLOCK: 'deadlock'}

@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(HERE, 'libdpemu.so')
 EXPORTS = ('dpemu_abi_version', 'dpemu_create', 'dpemu_destroy', 'dpemu_last_error',
            'dpemu_load_programs', 'dpemu_run', 'dpemu_run_host', 'dpemu_dds', 'dpemu_dds_sin_lut')
 
-_lib = None
+_libs = {}
 
 
 class DpemuError(RuntimeError):
@@ -19,9 +19,9 @@ class DpemuError(RuntimeError):
 
 
 def load_library(path=LIB_PATH):
-    global _lib
-    if _lib is not None:
-        return _lib
+    """the ctypes handle of libdpemu.so (another build's path for A/B runs)"""
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise DpemuError('libdpemu.so not built ({}); run __graft_entry__.build() '
                          '(hipcc --offload-arch=gfx950)'.format(path))
@@ -50,12 +50,12 @@ def load_library(path=LIB_PATH):
     if L.dpemu_abi_version() != _abi.ABI_VERSION:
         raise DpemuError('ABI version mismatch: library {} vs host {}'.format(
             L.dpemu_abi_version(), _abi.ABI_VERSION))
-    _lib = L
+    _libs[path] = L
     return L
 
 
-def check(ctx_handle, rc, what):
+def check(ctx_handle, rc, what, L=None):
     if rc != 0:
-        L = load_library()
+        L = L or load_library()
         msg = L.dpemu_last_error(ctx_handle)
         raise DpemuError('{} failed ({}): {}'.format(what, rc, msg.decode() if msg else ''))

@@ -25,10 +25,11 @@ struct dpemu_ctx {
     std::string err;
     // programs
     uint4 *d_words = nullptr;
+    uint4 *d_words_t = nullptr;             // command-major copy (KParams::fetch), or null
     uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
     uint32_t n_programs = 0, n_groups = 0, C = 0;
     uint64_t n_quads = 0;
-    bool has_fproc = false, has_sync = false;
+    bool has_fproc = false, has_sync = false, straight = false;
     std::vector<uint64_t> group_len;   // instructions of all C programs of each group
     // run constants
     uint32_t *d_thr = nullptr;
@@ -71,8 +72,8 @@ static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...)
 
 static void free_programs(dpemu_ctx *ctx)
 {
-    (void)hipFree(ctx->d_words); (void)hipFree(ctx->d_offsets); (void)hipFree(ctx->d_ninstr); (void)hipFree(ctx->d_table);
-    ctx->d_words = nullptr; ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
+    (void)hipFree(ctx->d_words); (void)hipFree(ctx->d_words_t); (void)hipFree(ctx->d_offsets); (void)hipFree(ctx->d_ninstr); (void)hipFree(ctx->d_table);
+    ctx->d_words = nullptr; ctx->d_words_t = nullptr; ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
     ctx->n_programs = 0;
 }
 
@@ -139,7 +140,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1)))
         return fail(ctx, DPEMU_E_INVALID, "cores_per_shot %u is not a power of two in [1, 64]", C);
     uint64_t quads = 0;
-    bool fp = false, sy = false;
+    bool fp = false, sy = false, straight = true;
     for (uint32_t i = 0; i < n_programs; i++) {
         if (n_instr[i] > 65536u)
             return fail(ctx, DPEMU_E_INVALID, "program %u: %u commands exceed the 2^16-deep cmd_mem", i, n_instr[i]);
@@ -150,6 +151,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
             const uint32_t op4 = words[4 * ((uint64_t)offsets[i] + k) + 3] >> 28;
             fp |= (op4 == 4 || op4 == 5);
             sy |= (op4 == 7);
+            straight &= !(op4 >= 1 && op4 <= 7);
         }
     for (uint64_t i = 0; i < (uint64_t)n_groups * C; i++)
         if (prog_table[i] >= n_programs)
@@ -161,6 +163,18 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     HIPCHK(ctx, hipMalloc(&ctx->d_ninstr, n_programs * 4));
     HIPCHK(ctx, hipMalloc(&ctx->d_table, (uint64_t)n_groups * C * 4));
     if (quads) HIPCHK(ctx, hipMemcpy(ctx->d_words, words, quads * 16, hipMemcpyHostToDevice));
+    // command-major copy when the padding stays small (at most 4x the programs, 1 GiB)
+    uint32_t max_len = 0;
+    for (uint32_t i = 0; i < n_programs; i++) max_len = std::max(max_len, n_instr[i]);
+    const uint64_t t_quads = (uint64_t)max_len * n_programs;
+    if (max_len && t_quads <= std::max<uint64_t>(4 * quads, 4096) && t_quads * 16 <= (1ull << 30)) {
+        std::vector<uint32_t> wt(t_quads * 4, 0u);
+        for (uint32_t pr = 0; pr < n_programs; pr++)
+            for (uint32_t k = 0; k < n_instr[pr]; k++)
+                memcpy(&wt[4 * ((uint64_t)k * n_programs + pr)], words + 4 * ((uint64_t)offsets[pr] + k), 16);
+        HIPCHK(ctx, hipMalloc(&ctx->d_words_t, t_quads * 16));
+        HIPCHK(ctx, hipMemcpy(ctx->d_words_t, wt.data(), t_quads * 16, hipMemcpyHostToDevice));
+    }
     HIPCHK(ctx, hipMemcpy(ctx->d_offsets, offsets, n_programs * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->d_ninstr, n_instr, n_programs * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->d_table, prog_table, (uint64_t)n_groups * C * 4, hipMemcpyHostToDevice));
@@ -170,6 +184,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     ctx->n_quads = quads;
     ctx->has_fproc = fp;
     ctx->has_sync = sy;
+    ctx->straight = straight;
     ctx->group_len.assign(n_groups, 0);
     for (uint32_t g = 0; g < n_groups; g++)
         for (uint32_t c = 0; c < C; c++) ctx->group_len[g] += n_instr[prog_table[(uint64_t)g * C + c]];
@@ -219,6 +234,9 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     }
     KParams p{};
     p.words = ctx->d_words;
+    const bool cmd_major = ctx->d_words_t && !(cfg->exec_flags & DPEMU_X_PROG_MAJOR);
+    p.fetch = cmd_major ? ctx->d_words_t : ctx->d_words;
+    p.fetch_stride = cmd_major ? ctx->n_programs : 1u;
     p.offsets = ctx->d_offsets; p.n_instr = ctx->d_ninstr; p.prog_table = ctx->d_table;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
     p.summary = out->summary;
@@ -285,6 +303,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     }
     if (ctx->has_fproc) feat |= (cfg->fproc_mode == DPEMU_FPROC_LUT) ? FEAT_LUT : FEAT_FPROC;
     if (ctx->has_sync) feat |= FEAT_SYNC;
+    if (ctx->straight) feat |= FEAT_STRAIGHT;
     // outcome histogram.  Direct: one u64 atomic per shot into out->hist --
     // cheapest when concurrent shots spread over many bins.  Replicas: R
     // privatised u32 copies picked by workgroup, then a reduce kernel -- for

@@ -118,11 +118,13 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     constexpr bool SYNC = (FEAT & FEAT_SYNC) != 0;
     constexpr bool LUT = (FEAT & FEAT_LUT) != 0;
     constexpr bool PLDS = (FEAT & FEAT_PROG_LDS) != 0;   // programs staged in LDS
+    // pulse / idle / done only: no ALU writes, so every register reads 0
+    constexpr bool STRAIGHT = (FEAT & FEAT_STRAIGHT) != 0;
     constexpr bool XMEAS = FPROC || LUT;             // measurements readable by other lanes
     constexpr int MT = XMEAS ? MEAS_LOOKUP : 1;
     constexpr int NF = LUT ? LUT_FIRE_CAP : 1;
 
-    __shared__ uint32_t s_regs[16][BLOCK];
+    __shared__ uint32_t s_regs[STRAIGHT ? 1 : 16][STRAIGHT ? 1 : BLOCK];
     __shared__ uint32_t s_mt[MT][BLOCK];
     // meas_lut per shot (slots indexed by the shot leader's tid)
     __shared__ uint32_t s_cur[LUT ? BLOCK : 1];       // merge cursor into lane's s_mt
@@ -144,13 +146,15 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     const uint32_t wl = tid & 63;                    // lane within the wavefront
     const uint32_t leader_tid = tid & ~(C - 1);
 
-    uint32_t base = 0, nprog = 0, grp = 0;
+    uint32_t base = 0, nprog = 0, grp = 0, prog = 0;
     if (valid) {
         grp = (uint32_t)((shot / p.shots_per_group) % p.n_groups);
-        const uint32_t prog = p.prog_table[(uint64_t)grp * C + core];
+        prog = p.prog_table[(uint64_t)grp * C + core];
         base = p.offsets[prog];
         nprog = p.n_instr[prog];
     }
+    // command ip of this lane's program in the fetch image (KParams::fetch)
+    const uint32_t fetch_off = p.fetch_stride == 1u ? base : prog;
     const uint32_t thr_core = valid ? p.p1_thr[core] : 0u;
     __shared__ uint32_t s_hist[HIST_LDS_MAX];
     if (p.hist_lds) {
@@ -187,8 +191,10 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         __syncthreads();
         if (valid) base = s_pref[group_step(p, spos, sp0) * C + core];
     }
+    if constexpr (!STRAIGHT) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
+        for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
+    }
     if constexpr (XMEAS) {
 #pragma unroll
         for (int m = 0; m < MT; m++) s_mt[m][tid] = INF32;
@@ -201,7 +207,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     uint32_t pe = 0, pp = 0, pa = 0;                 // pulse regs: env|cfg<<24, phase|freq<<17, amp
     uint32_t wait_d = 0, status = 0, flags = 0;
     uint32_t n_ev = 0, n_tr = 0, n_meas = 0, n_exec = 0, meas_bits = 0, last_bit = 0;
-    uint32_t t_end = 0, ip_end = 0, qclk_end = 0;
+    uint32_t t_end = 0;
     // leader-only meas_lut state
     uint64_t lut_valid = 0, lut_addr = 0;
     uint32_t lut_last_fire = INF32, nfire = 0;
@@ -209,9 +215,10 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     const uint64_t n_lanes = p.n_lanes;
     const bool is_part = SYNC ? (((p.sync_mask >> core) & 1ull) != 0) : false;
 
+    // a finished lane's ip and qclk anchor never change again: ip and qclk at
+    // t_end are read when the summary is written
     auto finish = [&](uint32_t st, uint32_t at) {
-        status = st; mode = M_FIN; t_end = at; ip_end = ip;
-        qclk_end = (at < qa_t) ? 0u : qa_q + (at - qa_t);
+        status = st; mode = M_FIN; t_end = at;
     };
 
     auto emit_event = [&](uint32_t te, uint32_t kind) {
@@ -274,14 +281,14 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         bool run = (mode == M_RUN);
         if (run && t > p.max_cycles) { finish(ST_MAX_CYCLES, t); run = false; }
         uint4 w = make_uint4(0u, 0u, 0u, 0u);
-        if (run && ip < nprog) w = PLDS ? s_prog[base + ip] : p.words[base + ip];
+        if (run && ip < nprog) w = PLDS ? s_prog[base + ip] : p.fetch[(uint64_t)ip * p.fetch_stride + fetch_off];
         const uint32_t op4 = w.w >> 28;
         const uint32_t alu = (w.w >> 24) & 7u;
         const uint32_t in0_reg = (w.w >> 27) & 1u;
         const uint32_t rs0 = (w.w >> 20) & 15u;
         const uint32_t rs1 = (w.z >> 20) & 15u;
-        const uint32_t reg0 = s_regs[rs0][tid];
-        const uint32_t reg1 = s_regs[rs1][tid];
+        const uint32_t reg0 = STRAIGHT ? 0u : s_regs[rs0][tid];
+        const uint32_t reg1 = STRAIGHT ? 0u : s_regs[rs1][tid];
         const uint32_t imm = (w.z >> 24) | (w.w << 8);
         const uint32_t in0 = in0_reg ? reg0 : imm;
         const uint32_t qD = (t < qa_t) ? 0u : qa_q + (t - qa_t);
@@ -342,7 +349,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                 executed = true;
                 n_exec++;
                 const uint32_t D = t;
-                switch (op4) {
+                switch (STRAIGHT && op4 >= 0x1 && op4 <= 0x7 ? 0xFu : op4) {   // not reached if STRAIGHT
                 case 0x0: case 0xA:
                     finish(ST_DONE, D);
                     break;
@@ -558,14 +565,15 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     }
 
     if (valid && p.summary) {
+        const uint32_t qclk_end = (t_end < qa_t) ? 0u : qa_q + (t_end - qa_t);
         uint4 *s = reinterpret_cast<uint4 *>(p.summary + 8ull * lane);
-        s[0] = make_uint4(t_end, (ip_end & 0xFFFFu) | ((status & 0xFFu) << 16) | ((flags & 0xFFu) << 24),
+        s[0] = make_uint4(t_end, (ip & 0xFFFFu) | ((status & 0xFFu) << 16) | ((flags & 0xFFu) << 24),
                           n_ev, n_exec);
         s[1] = make_uint4(qclk_end, n_meas, meas_bits, n_tr);
     }
     if (valid && p.regs_out) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = s_regs[r][tid];
+        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = STRAIGHT ? 0u : s_regs[r][tid];
     }
     if (p.hist_rep) {
         // outcome key: bit c = last measurement of core c; one count per shot
@@ -629,6 +637,7 @@ hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream)
     const size_t shmem = (feat & FEAT_PROG_LDS) ? (size_t)p.prog_lds_words * sizeof(uint4) : 0;
     switch (feat) {
 #define CASE(F) case F: launch_one<F>(p, blocks, shmem, stream); break;
+    CASE(FEAT_STRAIGHT) CASE(FEAT_STRAIGHT | FEAT_PROG_LDS)
     CASE(0) CASE(FEAT_FPROC) CASE(FEAT_SYNC) CASE(FEAT_FPROC | FEAT_SYNC) CASE(FEAT_LUT) CASE(FEAT_LUT | FEAT_SYNC)
     CASE(FEAT_PROG_LDS) CASE(FEAT_PROG_LDS | FEAT_FPROC) CASE(FEAT_PROG_LDS | FEAT_SYNC)
     CASE(FEAT_PROG_LDS | FEAT_FPROC | FEAT_SYNC) CASE(FEAT_PROG_LDS | FEAT_LUT)

@@ -41,6 +41,7 @@ constexpr int FEAT_FPROC = 1;   // fproc_meas reads (ALU_FPROC / JUMP_FPROC)
 constexpr int FEAT_SYNC = 2;    // SYNC barriers
 constexpr int FEAT_LUT = 4;     // fproc_lut back end
 constexpr int FEAT_PROG_LDS = 8; // the workgroup's programs staged in LDS (fits PROG_LDS_MAX)
+constexpr int FEAT_STRAIGHT = 16; // only pulse / idle / done / hang opcodes: no register file
 constexpr uint32_t PROG_LDS_MAX = 1024;   // instructions (16 KiB) of dynamic LDS per workgroup
 
 constexpr uint32_t ST_DONE = DPEMU_ST_DONE, ST_MAX_CYCLES = DPEMU_ST_MAX_CYCLES;
@@ -52,7 +53,12 @@ constexpr uint32_t TRACE_QCLK_LOAD = DPEMU_TRACE_QCLK_LOAD, TRACE_QCLK_RST = DPE
 
 struct KParams {
     // programs
-    const uint4 *words;
+    const uint4 *words;           // program-major: program p's command i at offsets[p] + i
+    const uint4 *fetch;           // the image the loop fetches from: command i of program p at
+    uint32_t fetch_stride;        //   i * fetch_stride + (stride 1 ? offsets[p] : p); stride = the
+                                  //   program count selects the command-major copy (zero past a
+                                  //   program's end), where adjacent lanes -- adjacent programs --
+                                  //   fetch adjacent words
     const uint32_t *offsets, *n_instr, *prog_table;
     const uint32_t *p1_thr;
     const uint64_t *lut_table;

@@ -145,8 +145,8 @@ class EmulationResult:
 class Emulator:
     """One context per GPU (one process per device)."""
 
-    def __init__(self, device: int = 0):
-        self._L = load_library()
+    def __init__(self, device: int = 0, lib_path: Optional[str] = None):
+        self._L = load_library(lib_path) if lib_path else load_library()
         h = C.c_void_p()
         rc = self._L.dpemu_create(int(device), C.byref(h))
         if rc != 0:
@@ -178,7 +178,7 @@ class Emulator:
         rc = self._L.dpemu_load_programs(self._h, ps.words.ctypes.data, ps.offsets.ctypes.data,
                                          ps.n_instr.ctypes.data, ps.n_programs, ps.table.ctypes.data,
                                          ps.n_groups, ps.cores_per_shot)
-        check(self._h, rc, 'dpemu_load_programs')
+        check(self._h, rc, 'dpemu_load_programs', self._L)
         self.programs = ps
         return ps
 
@@ -198,7 +198,7 @@ class Emulator:
         arrays = _abi.alloc_host_outputs(cfg, n_shots, want)
         o = _abi.outputs_struct(arrays)
         rc = self._L.dpemu_run_host(self._h, C.addressof(cfg), int(shot_begin), int(n_shots), C.addressof(o))
-        check(self._h, rc, 'dpemu_run_host')
+        check(self._h, rc, 'dpemu_run_host', self._L)
         return EmulationResult(cfg, n_shots, shot_begin, arrays)
 
     def run_device(self, cfg: _abi.Config, n_shots: int, shot_begin: int, outputs: dict,
@@ -212,7 +212,7 @@ class Emulator:
         s = getattr(stream, 'cuda_stream', stream)
         rc = self._L.dpemu_run(self._h, C.addressof(cfg), int(shot_begin), int(n_shots), C.addressof(o),
                                C.c_void_p(s) if s else None)
-        check(self._h, rc, 'dpemu_run')
+        check(self._h, rc, 'dpemu_run', self._L)
 
     def synthesize(self, plan, outputs: dict, n_samples: int, iq=None, stream=None):
         """DDS I/Q of every channel of ``plan`` (dds.ChannelPlan) from a device
@@ -237,7 +237,7 @@ class Emulator:
                                outputs['ev_main'].data_ptr(), outputs['ev_amp'].data_ptr(),
                                env.data_ptr(), freq.data_ptr(), iq.data_ptr(),
                                C.c_void_p(s) if s else None)
-        check(self._h, rc, 'dpemu_dds')
+        check(self._h, rc, 'dpemu_dds', self._L)
         return iq
 
 

@@ -33,7 +33,9 @@ def raw(op4, in0_reg=0, alu_op=0, imm=0, rs0=0, rs1=0, rd=0, target=0, fproc_id=
 
 
 class Gen:
-    def __init__(self, rng, ncores, mode='meas', allow_late=False, allow_hang=False, meas_latency=20):
+    def __init__(self, rng, ncores, mode='meas', allow_late=False, allow_hang=False, meas_latency=20,
+                 straight=False):
+        self.straight = straight          # pulse / idle / pulse_reset / done only
         self.rng = rng
         self.ncores = ncores
         self.mode = mode
@@ -63,7 +65,7 @@ class Gen:
         i = 0
         while i < n:
             kind = r.choices(['trig', 'pw', 'idle', 'prst', 'alu', 'incq', 'jc', 'ji', 'loop', 'fproc'],
-                             [10, 3, 2, 1, 6, 2, 2, 1, 1, 2])[0]
+                             [10, 3, 2, 1, 0, 0, 0, 0, 0, 0] if self.straight else [10, 3, 2, 1, 6, 2, 2, 1, 1, 2])[0]
             if kind == 'trig':
                 if self.allow_late and r.random() < 0.05:
                     t = (q - r.randint(1, 4)) & 0xFFFFFFFF
@@ -183,13 +185,13 @@ def pack_programs(progs):
     return words, np.array(offsets, np.uint32), np.array(n_instr, np.uint32)
 
 
-def random_case(seed, ncores=None, mode=None, allow_late=True, allow_hang=True, n_groups=None):
+def random_case(seed, ncores=None, mode=None, allow_late=True, allow_hang=True, n_groups=None, straight=False):
     rng = random.Random(seed)
     ncores = ncores or rng.choice([1, 2, 4])
     mode = mode or rng.choice(['meas', 'meas', 'lut'])
     n_groups = n_groups or rng.choice([1, 2])
-    n_sync = rng.choice([0, 0, 1, 2]) if ncores > 1 else rng.choice([0, 1])
-    g = Gen(rng, ncores, mode, allow_late, allow_hang)
+    n_sync = 0 if straight else (rng.choice([0, 0, 1, 2]) if ncores > 1 else rng.choice([0, 1]))
+    g = Gen(rng, ncores, mode, allow_late, allow_hang, straight=straight)
     body = rng.randint(3, 14)
     progs = [g.program(n_sync, body) for _ in range(n_groups * ncores)]
     table = np.arange(n_groups * ncores, dtype=np.uint32)

@@ -47,7 +47,7 @@ def run_pair(emu, ps, cfg, n_shots, shot0=0):
     g = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
     f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n_shots, want=ALL_OUT)
     base = cfg.exec_flags
-    for flags in (_abi.X_PROG_LDS | _abi.X_GROUP_MAJOR | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT):
+    for flags in (_abi.X_PROG_LDS | _abi.X_GROUP_MAJOR | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT | _abi.X_PROG_MAJOR):
         cfg.exec_flags = flags
         g2 = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
         compare_all(g2.arrays, g.arrays, 'execution variant {:#x}'.format(flags))
@@ -68,6 +68,21 @@ def test_fuzz_gpu_vs_fast(emu, seed):
                            seed=seed)
     n_shots = 333 if seed % 2 else 100 * ps.n_groups     # odd: natural order; even: group-major
     g, f = run_pair(emu, ps, cfg, n_shots, shot0=seed * 1000)
+    compare_all(g, f, 'seed {}'.format(seed))
+
+
+@pytest.mark.parametrize('seed', range(12))
+def test_fuzz_straight_programs(emu, seed):
+    """pulse / idle / pulse_reset / done / hang programs (the register-free
+    kernel specialisation): register-sourced pulse fields read 0, late
+    triggers, the reset-hold double strobe"""
+    C = [1, 2, 4, 8][seed % 4]
+    case = random_case(9000 + seed, ncores=C, mode='meas', allow_late=True, allow_hang=True, straight=True)
+    groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
+    ps = ProgramSet(groups, cores_per_shot=C)
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=6000, event_cap=64, trace_cap=16,
+                           meas_cap=16, meas_latency=1 + seed, seed=seed)
+    g, f = run_pair(emu, ps, cfg, 777, shot0=seed * 31)
     compare_all(g, f, 'seed {}'.format(seed))
 
 
