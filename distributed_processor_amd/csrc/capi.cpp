@@ -24,8 +24,8 @@ struct dpemu_ctx {
     int device = 0;
     std::string err;
     // programs
-    uint4 *d_words = nullptr;
-    uint4 *d_words_t = nullptr;             // command-major copy (KParams::fetch), or null
+    uint4 *d_uops = nullptr;                // decode_cmd words, program-major (KParams::uops)
+    uint4 *d_uops_t = nullptr;              // command-major copy (KParams::fetch), or null
     uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
     uint32_t n_programs = 0, n_groups = 0, C = 0;
     uint64_t n_quads = 0;
@@ -72,8 +72,8 @@ static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...)
 
 static void free_programs(dpemu_ctx *ctx)
 {
-    (void)hipFree(ctx->d_words); (void)hipFree(ctx->d_words_t); (void)hipFree(ctx->d_offsets); (void)hipFree(ctx->d_ninstr); (void)hipFree(ctx->d_table);
-    ctx->d_words = nullptr; ctx->d_words_t = nullptr; ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
+    (void)hipFree(ctx->d_uops); (void)hipFree(ctx->d_uops_t); (void)hipFree(ctx->d_offsets); (void)hipFree(ctx->d_ninstr); (void)hipFree(ctx->d_table);
+    ctx->d_uops = nullptr; ctx->d_uops_t = nullptr; ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
     ctx->n_programs = 0;
 }
 
@@ -158,22 +158,26 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
             return fail(ctx, DPEMU_E_INVALID, "prog_table[%llu] = %u >= n_programs", (unsigned long long)i, prog_table[i]);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     free_programs(ctx);
-    HIPCHK(ctx, hipMalloc(&ctx->d_words, std::max<uint64_t>(quads, 1) * 16));
     HIPCHK(ctx, hipMalloc(&ctx->d_offsets, n_programs * 4));
     HIPCHK(ctx, hipMalloc(&ctx->d_ninstr, n_programs * 4));
     HIPCHK(ctx, hipMalloc(&ctx->d_table, (uint64_t)n_groups * C * 4));
-    if (quads) HIPCHK(ctx, hipMemcpy(ctx->d_words, words, quads * 16, hipMemcpyHostToDevice));
-    // command-major copy when the padding stays small (at most 4x the programs, 1 GiB)
+    // every command pre-decoded once (kernels.h decode_cmd), program-major ...
+    std::vector<uint32_t> uops(std::max<uint64_t>(quads, 1) * 4, 0u);
+    for (uint64_t i = 0; i < quads; i++) decode_cmd(words + 4 * i, &uops[4 * i]);
+    HIPCHK(ctx, hipMalloc(&ctx->d_uops, uops.size() * 4));
+    HIPCHK(ctx, hipMemcpy(ctx->d_uops, uops.data(), uops.size() * 4, hipMemcpyHostToDevice));
+    // ... and command-major (zero = DONE past a program's end) when the padding
+    // stays small: at most 4x the programs, 1 GiB
     uint32_t max_len = 0;
     for (uint32_t i = 0; i < n_programs; i++) max_len = std::max(max_len, n_instr[i]);
-    const uint64_t t_quads = (uint64_t)max_len * n_programs;
-    if (max_len && t_quads <= std::max<uint64_t>(4 * quads, 4096) && t_quads * 16 <= (1ull << 30)) {
-        std::vector<uint32_t> wt(t_quads * 4, 0u);
+    const uint64_t t_cmds = (uint64_t)max_len * n_programs;
+    if (max_len && t_cmds <= std::max<uint64_t>(4 * quads, 4096) && t_cmds * 16 <= (1ull << 30)) {
+        std::vector<uint32_t> ut(t_cmds * 4, 0u);
         for (uint32_t pr = 0; pr < n_programs; pr++)
             for (uint32_t k = 0; k < n_instr[pr]; k++)
-                memcpy(&wt[4 * ((uint64_t)k * n_programs + pr)], words + 4 * ((uint64_t)offsets[pr] + k), 16);
-        HIPCHK(ctx, hipMalloc(&ctx->d_words_t, t_quads * 16));
-        HIPCHK(ctx, hipMemcpy(ctx->d_words_t, wt.data(), t_quads * 16, hipMemcpyHostToDevice));
+                memcpy(&ut[4 * ((uint64_t)k * n_programs + pr)], &uops[4 * ((uint64_t)offsets[pr] + k)], 16);
+        HIPCHK(ctx, hipMalloc(&ctx->d_uops_t, t_cmds * 16));
+        HIPCHK(ctx, hipMemcpy(ctx->d_uops_t, ut.data(), t_cmds * 16, hipMemcpyHostToDevice));
     }
     HIPCHK(ctx, hipMemcpy(ctx->d_offsets, offsets, n_programs * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->d_ninstr, n_instr, n_programs * 4, hipMemcpyHostToDevice));
@@ -200,6 +204,7 @@ static int validate(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t n_shots, b
     if (cfg->n_groups != ctx->n_groups)
         return fail(ctx, DPEMU_E_INVALID, "n_groups %u != loaded %u", cfg->n_groups, ctx->n_groups);
     if (cfg->shots_per_group == 0) return fail(ctx, DPEMU_E_INVALID, "shots_per_group == 0");
+    if (cfg->n_groups > 0x80000000u) return fail(ctx, DPEMU_E_INVALID, "n_groups > 2^31");
     if (cfg->max_cycles == 0 || cfg->max_cycles > 0x7FFFFFC0u)
         return fail(ctx, DPEMU_E_INVALID, "max_cycles must be in (0, 2^31 - 64]");
     if (cfg->meas_latency < 1 || cfg->meas_latency > (1u << 20) || cfg->sync_latency < 1 ||
@@ -233,9 +238,9 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
         ctx->lut_cache = lut;
     }
     KParams p{};
-    p.words = ctx->d_words;
-    const bool cmd_major = ctx->d_words_t && !(cfg->exec_flags & DPEMU_X_PROG_MAJOR);
-    p.fetch = cmd_major ? ctx->d_words_t : ctx->d_words;
+    p.uops = ctx->d_uops;
+    const bool cmd_major = ctx->d_uops_t && !(cfg->exec_flags & DPEMU_X_PROG_MAJOR);
+    p.fetch = cmd_major ? ctx->d_uops_t : ctx->d_uops;
     p.fetch_stride = cmd_major ? ctx->n_programs : 1u;
     p.offsets = ctx->d_offsets; p.n_instr = ctx->d_ninstr; p.prog_table = ctx->d_table;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
@@ -252,6 +257,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.log2C = 0;
     while ((1u << p.log2C) < C) p.log2C++;
     p.n_groups = cfg->n_groups; p.shots_per_group = cfg->shots_per_group;
+    p.grp_g0 = (uint32_t)((shot_begin / cfg->shots_per_group) % cfg->n_groups);
+    p.grp_r0 = (uint32_t)(shot_begin % cfg->shots_per_group);
     p.max_cycles = cfg->max_cycles;
     p.event_cap = out->ev_main || out->ev_amp ? cfg->event_cap : 0;
     p.trace_cap = out->trace ? cfg->trace_cap : 0;

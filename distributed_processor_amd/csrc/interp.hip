@@ -53,6 +53,19 @@ __device__ __forceinline__ uint32_t alu_op(uint32_t op, uint32_t a, uint32_t b)
     return r;
 }
 
+// pulse_reg.sv:59-97 for a pre-decoded pulse command (decode_cmd): each field
+// with its write enable takes its immediate (register-sourced fields are
+// zero here and ORed in by the caller)
+__device__ __forceinline__ void pulse_write(const uint4 u, uint32_t &pe, uint32_t &pp, uint32_t &pa)
+{
+    const uint32_t we = u.z >> 26;                  // env cfg phase freq amp
+    const uint32_t clr_e = (we & 1u ? 0x00FFFFFFu : 0u) | (we & 2u ? 0x0F000000u : 0u);
+    const uint32_t clr_p = (we & 4u ? 0x0001FFFFu : 0u) | (we & 8u ? 0x03FE0000u : 0u);
+    pe = (pe & ~clr_e) | (u.y & clr_e);
+    pp = (pp & ~clr_p) | (u.z & clr_p);
+    pa = (we & 16u) ? (u.w & 0xFFFFu) : pa;
+}
+
 // Philox4x32-10, output word 0 (counter = shot_lo, shot_hi, core, m; key = seed)
 __device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m)
 {
@@ -148,7 +161,14 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 
     uint32_t base = 0, nprog = 0, grp = 0, prog = 0;
     if (valid) {
-        grp = (uint32_t)((shot / p.shots_per_group) % p.n_groups);
+        // group of the shot, (shot / spg) % n_groups, from the run's first shot
+        // (g0, r0 from the host) in 32-bit arithmetic: a u64 division would cost
+        // ~150 VALU instructions per lane
+        const uint32_t sl = lane >> p.log2C;                 // shot within the run (< 2^31)
+        const uint64_t num = (uint64_t)p.grp_r0 + sl;
+        const uint32_t q = (num >> 32) ? (uint32_t)(num / p.shots_per_group) : (uint32_t)num / p.shots_per_group;
+        const uint32_t g = p.grp_g0 + q % p.n_groups;       // < 2 n_groups <= 2^32
+        grp = g >= p.n_groups ? g - p.n_groups : g;
         prog = p.prog_table[(uint64_t)grp * C + core];
         base = p.offsets[prog];
         nprog = p.n_instr[prog];
@@ -186,7 +206,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
             }
             const uint32_t g = (g0 + lo / C) % p.n_groups;
             const uint32_t prog = p.prog_table[(uint64_t)g * C + (lo & (C - 1))];
-            s_prog[idx] = p.words[p.offsets[prog] + (idx - s_pref[lo])];
+            s_prog[idx] = p.uops[p.offsets[prog] + (idx - s_pref[lo])];
         }
         __syncthreads();
         if (valid) base = s_pref[group_step(p, spos, sp0) * C + core];
@@ -280,17 +300,13 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         // ---------------- fetch + decode (RUN lanes) ----------------
         bool run = (mode == M_RUN);
         if (run && t > p.max_cycles) { finish(ST_MAX_CYCLES, t); run = false; }
-        uint4 w = make_uint4(0u, 0u, 0u, 0u);
-        if (run && ip < nprog) w = PLDS ? s_prog[base + ip] : p.fetch[(uint64_t)ip * p.fetch_stride + fetch_off];
-        const uint32_t op4 = w.w >> 28;
-        const uint32_t alu = (w.w >> 24) & 7u;
-        const uint32_t in0_reg = (w.w >> 27) & 1u;
-        const uint32_t rs0 = (w.w >> 20) & 15u;
-        const uint32_t rs1 = (w.z >> 20) & 15u;
-        const uint32_t reg0 = STRAIGHT ? 0u : s_regs[rs0][tid];
-        const uint32_t reg1 = STRAIGHT ? 0u : s_regs[rs1][tid];
-        const uint32_t imm = (w.z >> 24) | (w.w << 8);
-        const uint32_t in0 = in0_reg ? reg0 : imm;
+        uint4 u = make_uint4(0u, 0u, 0u, 0u);             // past the program: op4 0 = DONE
+        if (run && ip < nprog) u = PLDS ? s_prog[base + ip] : p.fetch[(uint64_t)ip * p.fetch_stride + fetch_off];
+        const uint32_t op4 = u.y >> 28;
+        const uint32_t alu = u.y & 7u;
+        const uint32_t reg0 = STRAIGHT ? 0u : s_regs[(u.w >> 20) & 15u][tid];
+        const uint32_t reg1 = STRAIGHT ? 0u : s_regs[(u.y >> 4) & 15u][tid];
+        const uint32_t in0 = (u.y & 8u) ? reg0 : u.x;
         const uint32_t qD = (t < qa_t) ? 0u : qa_q + (t - qa_t);
         const bool is_fproc = run && (op4 == 4u || op4 == 5u);
 
@@ -336,7 +352,44 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 
         // ---------------- execute ----------------
         bool executed = false;
-        if (run) {
+        if constexpr (STRAIGHT) {
+            // pulse / idle / pulse_reset / done / hang only: the timing of ctrl.v in
+            // closed form with few state merges (the generic switch below costs ~2x
+            // the VALU instructions per command)
+            if (run) {
+                n_exec++;
+                const uint32_t D = t;
+                const bool pw = op4 == 0x8u || op4 == 0x9u;
+                const bool waits = op4 == 0x9u || op4 == 0xCu;
+                const bool pulse_cls = pw || op4 == 0xBu || op4 == 0xCu;
+                const uint32_t T = u.x;
+                uint32_t wait = T - qD;
+                bool dbl = false, big = false;
+                if (D < qa_t) {            // reset hold: qclk(0) = qclk(1) = 0 (proc.sv:125-136)
+                    dbl = T == 0u;
+                    const uint64_t wl = dbl ? 0ull : (uint64_t)(qa_t - D) + (uint32_t)(T - qa_q);
+                    wait = (uint32_t)wl;
+                    big = (wl >> 32) != 0ull;
+                }
+                if (waits && (big || wait >= 0x80000000u)) flags |= F_LATE;
+                const bool over = waits && (big || wait > p.max_cycles - D);
+                const uint32_t tT = D + (waits ? wait : 0u);
+                if (!pulse_cls || over) {
+                    finish(over ? ST_MAX_CYCLES : (op4 >= 0xDu ? ST_HUNG_OPCODE : ST_DONE), D);
+                } else {
+                    if (pw) {
+                        // pulse_reg.sv:59-97 with reg_in = 0
+                        pulse_write(u, pe, pp, pa);
+                    }
+                    if (op4 == 0x9u || op4 == 0xBu) {
+                        emit_event(op4 == 0xBu ? D : tT + 2u, op4 == 0xBu ? 1u : 0u);
+                        if (dbl && op4 == 0x9u) { emit_event(tT + 3u, 0u); flags |= F_DOUBLE_STROBE; }
+                    }
+                    ip = (ip + 1u) & 0xFFFFu;
+                    t = tT + 3u;
+                }
+            }
+        } else if (run) {
             bool stall = false;
             if constexpr (FPROC) {
                 // fproc_meas read at D = t needs every meas_valid <= D known
@@ -365,7 +418,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                     uint32_t tT = D;
                     bool dbl = false;
                     if (op4 != 0x8) {
-                        const uint32_t T = (w.x >> 5) | (w.y << 27);
+                        const uint32_t T = u.x;
                         uint64_t wait;
                         if (D < qa_t) { dbl = (T == 0u); wait = dbl ? 0ull : (uint64_t)(qa_t - D) + (uint32_t)(T - qa_q); }
                         else wait = (uint32_t)(T - qD);
@@ -374,17 +427,14 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                         else tT = D + (uint32_t)wait;
                     }
                     if (go && op4 != 0xC) {
-                        // pulse_reg.sv:59-97
-                        const uint32_t env_i = ((w.z >> 26) | (w.w << 6)) & 0xFFFFFFu;
-                        const uint32_t ph_i = (w.z >> 7) & 0x1FFFFu;
-                        const uint32_t fr_i = ((w.y >> 28) | (w.z << 4)) & 0x1FFu;
-                        const uint32_t amp_i = (w.y >> 10) & 0xFFFFu;
-                        const uint32_t cfg_i = (w.y >> 5) & 0xFu;
-                        if ((w.w >> 19) & 1u) pe = (pe & 0xFF000000u) | (((w.w >> 18) & 1u) ? (reg0 & 0xFFFFFFu) : env_i);
-                        if ((w.z >> 25) & 1u) pp = (pp & 0xFFFE0000u) | (((w.z >> 24) & 1u) ? (reg0 & 0x1FFFFu) : ph_i);
-                        if ((w.z >> 6) & 1u) pp = (pp & 0x1FFFFu) | ((((w.z >> 5) & 1u) ? (reg0 & 0x1FFu) : fr_i) << 17);
-                        if ((w.y >> 27) & 1u) pa = ((w.y >> 26) & 1u) ? (reg0 & 0xFFFFu) : amp_i;
-                        if ((w.y >> 9) & 1u) pe = (pe & 0xFFFFFFu) | (cfg_i << 24);
+                        // pulse_reg.sv:59-97: immediates, then reg[rs0] into register-sourced fields
+                        pulse_write(u, pe, pp, pa);
+                        if (u.z >> 31) {
+                            if (u.w & UOP_RS_ENV) pe |= reg0 & 0xFFFFFFu;
+                            if (u.w & UOP_RS_PH) pp |= reg0 & 0x1FFFFu;
+                            if (u.w & UOP_RS_FR) pp |= (reg0 & 0x1FFu) << 17;
+                            if (u.w & UOP_RS_AMP) pa = reg0 & 0xFFFFu;
+                        }
                     }
                     if (go) {
                         if (op4 == 0x9) {
@@ -398,18 +448,18 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                 }
                 case 0x1: {
                     const uint32_t out = alu_op(alu, in0, reg1);
-                    const uint32_t rd = (w.z >> 16) & 15u;
+                    const uint32_t rd = (u.y >> 8) & 15u;
                     s_regs[rd][tid] = out;
                     emit_trace(D + 3u, rd, out);
                     ip = (ip + 1u) & 0xFFFFu; t = D + 4u;
                     break;
                 }
                 case 0x2:
-                    ip = (w.z >> 4) & 0xFFFFu; t = D + 4u;
+                    ip = u.z & 0xFFFFu; t = D + 4u;
                     break;
                 case 0x3: {
                     const uint32_t out = alu_op(alu, in0, reg1);
-                    ip = (out & 1u) ? ((w.z >> 4) & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                    ip = (out & 1u) ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
                     t = D + 6u;
                     break;
                 }
@@ -425,7 +475,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                     else { finish(ST_DEADLOCK, D); }   // not reached: host selects SYNC kernels
                     break;
                 case 0x4: case 0x5: {
-                    const uint32_t id = (w.y >> 20) & 0xFFu;
+                    const uint32_t id = (u.z >> 16) & 0xFFu;
                     bool have = false;
                     uint32_t R = 0, data = 0;
                     if constexpr (XMEAS) {
@@ -452,12 +502,12 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                         else {
                             const uint32_t out = alu_op(alu, in0, data);
                             if (op4 == 4u) {
-                                const uint32_t rd = (w.z >> 16) & 15u;
+                                const uint32_t rd = (u.y >> 8) & 15u;
                                 s_regs[rd][tid] = out;
                                 emit_trace(R + 3u, rd, out);
                                 ip = (ip + 1u) & 0xFFFFu; t = R + 4u;
                             } else {
-                                ip = (out & 1u) ? ((w.z >> 4) & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                                ip = (out & 1u) ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
                                 t = R + 6u;
                             }
                         }
@@ -529,20 +579,20 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                     const uint32_t tf = s_fire_t[k][leader_tid];
                     if (tf >= wait_d + 1u) {
                         const uint64_t out_bits = s_fire_o[k][leader_tid];
-                        const uint4 w2 = PLDS ? s_prog[base + ip] : p.words[base + ip];     // the waiting fproc instruction
-                        const uint32_t op4b = w2.w >> 28, alub = (w2.w >> 24) & 7u;
-                        const uint32_t in0b = ((w2.w >> 27) & 1u) ? s_regs[(w2.w >> 20) & 15u][tid]
-                                                                  : ((w2.z >> 24) | (w2.w << 8));
+                        // the waiting fproc command
+                        const uint4 u2 = PLDS ? s_prog[base + ip] : p.uops[base + ip];
+                        const uint32_t op4b = u2.y >> 28, alub = u2.y & 7u;
+                        const uint32_t in0b = (u2.y & 8u) ? s_regs[(u2.w >> 20) & 15u][tid] : u2.x;
                         if (tf > p.max_cycles) { finish(ST_MAX_CYCLES, wait_d); }
                         else {
                             const uint32_t out = alu_op(alub, in0b, (uint32_t)((out_bits >> core) & 1ull));
                             if (op4b == 4u) {
-                                const uint32_t rd = (w2.z >> 16) & 15u;
+                                const uint32_t rd = (u2.y >> 8) & 15u;
                                 s_regs[rd][tid] = out;
                                 emit_trace(tf + 3u, rd, out);
                                 ip = (ip + 1u) & 0xFFFFu; t = tf + 4u;
                             } else {
-                                ip = (out & 1u) ? ((w2.z >> 4) & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                                ip = (out & 1u) ? (u2.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
                                 t = tf + 6u;
                             }
                             mode = M_RUN;

@@ -42,7 +42,7 @@ constexpr int FEAT_SYNC = 2;    // SYNC barriers
 constexpr int FEAT_LUT = 4;     // fproc_lut back end
 constexpr int FEAT_PROG_LDS = 8; // the workgroup's programs staged in LDS (fits PROG_LDS_MAX)
 constexpr int FEAT_STRAIGHT = 16; // only pulse / idle / done / hang opcodes: no register file
-constexpr uint32_t PROG_LDS_MAX = 1024;   // instructions (16 KiB) of dynamic LDS per workgroup
+constexpr uint32_t PROG_LDS_MAX = 1024;   // commands (16 KiB) of dynamic LDS per workgroup
 
 constexpr uint32_t ST_DONE = DPEMU_ST_DONE, ST_MAX_CYCLES = DPEMU_ST_MAX_CYCLES;
 constexpr uint32_t ST_HUNG_OPCODE = DPEMU_ST_HUNG_OPCODE, ST_DEADLOCK = DPEMU_ST_DEADLOCK;
@@ -51,14 +51,55 @@ constexpr uint32_t F_TRACE_OVF = DPEMU_F_TRACE_OVF, F_MEAS_OVF = DPEMU_F_MEAS_OV
 constexpr uint32_t F_DOUBLE_STROBE = DPEMU_F_DOUBLE_STROBE, F_GUARD = DPEMU_F_GUARD;
 constexpr uint32_t TRACE_QCLK_LOAD = DPEMU_TRACE_QCLK_LOAD, TRACE_QCLK_RST = DPEMU_TRACE_QCLK_RST;
 
+// Pre-decoded command: dpemu_load_programs re-packs every 128-bit cmd_mem
+// word (decode_cmd) so the interpreter reads fields at fixed 32-bit
+// positions instead of slicing hdl/proc.sv:89-107's layout (the same 16
+// bytes per command):
+//   x  cmd_time (cmd[36:5]) for pulse / idle; ALU immediate in0 (cmd[119:88])
+//   y  op4[31:28]; pulse writes: env[23:0] cfg[27:24] immediates (zero when the
+//      field is not written or register-sourced); other ops: alu[2:0]
+//      in0_reg[3] rs1[7:4] rd[11:8]
+//   z  pulse writes: phase[16:0] freq[25:17] immediates, write enables
+//      env[26] cfg[27] phase[28] freq[29] amp[30], any register-sourced[31]
+//      (hdl/pulse_reg.sv:38-97); other ops: target[15:0] fproc_id[23:16]
+//   w  rs0[23:20] (cmd[119:116]); pulse writes: amp[15:0] immediate,
+//      register-sourced env[16] phase[17] freq[18] amp[19]
+constexpr uint32_t UOP_RS_ENV = 1u << 16, UOP_RS_PH = 1u << 17, UOP_RS_FR = 1u << 18, UOP_RS_AMP = 1u << 19;
+
+__host__ __device__ inline void decode_cmd(const uint32_t w[4], uint32_t u[4])
+{
+    const uint32_t op4 = w[3] >> 28;
+    const uint32_t rs0 = (w[3] >> 20) & 15u;
+    u[0] = (op4 == 0x9 || op4 == 0xC) ? ((w[0] >> 5) | (w[1] << 27)) : ((w[2] >> 24) | (w[3] << 8));
+    u[1] = (op4 << 28) | ((w[3] >> 24) & 7u) | (((w[3] >> 27) & 1u) << 3) | (((w[2] >> 20) & 15u) << 4) |
+           (((w[2] >> 16) & 15u) << 8);
+    u[2] = ((w[2] >> 4) & 0xFFFFu) | (((w[1] >> 20) & 0xFFu) << 16);
+    u[3] = rs0 << 20;
+    if (op4 == 0x8 || op4 == 0x9) {
+        const uint32_t env_i = ((w[2] >> 26) | (w[3] << 6)) & 0xFFFFFFu, ph_i = (w[2] >> 7) & 0x1FFFFu;
+        const uint32_t fr_i = ((w[1] >> 28) | (w[2] << 4)) & 0x1FFu, amp_i = (w[1] >> 10) & 0xFFFFu;
+        const uint32_t cfg_i = (w[1] >> 5) & 0xFu;
+        const uint32_t env_we = (w[3] >> 19) & 1u, env_rs = (w[3] >> 18) & 1u;
+        const uint32_t ph_we = (w[2] >> 25) & 1u, ph_rs = (w[2] >> 24) & 1u;
+        const uint32_t fr_we = (w[2] >> 6) & 1u, fr_rs = (w[2] >> 5) & 1u;
+        const uint32_t amp_we = (w[1] >> 27) & 1u, amp_rs = (w[1] >> 26) & 1u;
+        const uint32_t cfg_we = (w[1] >> 9) & 1u;
+        const uint32_t rs = (env_we & env_rs) | ((ph_we & ph_rs) << 1) | ((fr_we & fr_rs) << 2) | ((amp_we & amp_rs) << 3);
+        u[1] = (op4 << 28) | (env_we && !env_rs ? env_i : 0u) | (cfg_we ? cfg_i << 24 : 0u);
+        u[2] = (ph_we && !ph_rs ? ph_i : 0u) | (fr_we && !fr_rs ? fr_i << 17 : 0u) | (env_we << 26) |
+               (cfg_we << 27) | (ph_we << 28) | (fr_we << 29) | (amp_we << 30) | ((rs ? 1u : 0u) << 31);
+        u[3] = (rs0 << 20) | (amp_we && !amp_rs ? amp_i : 0u) | (rs << 16);
+    }
+}
+
 struct KParams {
-    // programs
-    const uint4 *words;           // program-major: program p's command i at offsets[p] + i
+    // programs, as decode_cmd words (16 B per command)
+    const uint4 *uops;            // program-major: program p's command i at offsets[p] + i
     const uint4 *fetch;           // the image the loop fetches from: command i of program p at
     uint32_t fetch_stride;        //   i * fetch_stride + (stride 1 ? offsets[p] : p); stride = the
                                   //   program count selects the command-major copy (zero past a
                                   //   program's end), where adjacent lanes -- adjacent programs --
-                                  //   fetch adjacent words
+                                  //   fetch adjacent commands
     const uint32_t *offsets, *n_instr, *prog_table;
     const uint32_t *p1_thr;
     const uint64_t *lut_table;
@@ -73,13 +114,14 @@ struct KParams {
     // run
     uint64_t shot_begin;
     uint32_t n_lanes, C, log2C, n_groups, shots_per_group;
+    uint32_t grp_g0, grp_r0;      // (shot_begin / spg) % n_groups, shot_begin % spg
     uint32_t max_cycles, event_cap, trace_cap, meas_cap;
     uint32_t fproc_mode, meas_elem, meas_latency, sync_latency;
     uint64_t sync_mask, seed;
     uint32_t lut_mask;
     uint32_t iter_guard;
     uint32_t shot_order, rows;    // 1: group-major thread order (shots_per_group 1, n = rows * n_groups)
-    uint32_t prog_lds_words;      // dynamic LDS instructions (FEAT_PROG_LDS)
+    uint32_t prog_lds_words;      // dynamic LDS commands (FEAT_PROG_LDS)
     uint32_t *hist_rep;           // [hist_reps][hist_stride] u32 replicas (128-B aligned rows)
     uint32_t hist_reps, hist_lds; // hist_lds: n_groups << C <= HIST_LDS_MAX, aggregate in LDS
     uint64_t hist_stride;

@@ -2,8 +2,8 @@
 
 usage: python scripts/pmc_summary.py <prof root (e.g. gpurun_out/r01)> <tag> [dest dir]
 
-Reads <root>/prof_trace (--kernel-trace --stats) and every other <root>/prof_*
-PMC pass (counter_collection.csv), groups dispatches by (kernel, grid size),
+Reads <root>/prof_trace or <root>/trace (--kernel-trace --stats) and every
+other subdirectory's PMC pass (counter_collection.csv), groups dispatches by (kernel, grid size),
 keeps each kernel's most frequent shape (the bench's timed launches) and
 writes <dest>/<tag>_<kernel>_pmc.json with per-launch means:
 
@@ -12,8 +12,10 @@ writes <dest>/<tag>_<kernel>_pmc.json with per-launch means:
 * fetch_bytes     FETCH_SIZE x 1024 x 2: on gfx950 FETCH_SIZE reads 1/2 of a
                   wide coalesced read (MI355X_MICROARCH.md, HBM section)
 * hbm_bytes_per_launch = write_bytes + fetch_bytes
-* SQ_* / GRBM_* raw means, and VALU busy by the gfx94x formula
-  (SQ_ACTIVE_INST_VALU * 4 / (4 SIMD * 256 CU) / GRBM_GUI_ACTIVE)
+* SQ_* / GRBM_* raw means; VALU busy = SQ_ACTIVE_INST_VALU * 4 / (4 SIMD x 256 CU)
+  / (GRBM_GUI_ACTIVE / 8 XCDs); VALU issue share = SQ_INSTS_VALU x 4 cycles on
+  the same denominator; lane utilisation = SQ_THREAD_CYCLES_VALU /
+  (SQ_ACTIVE_INST_VALU x 64)
 """
 import collections
 import csv
@@ -46,7 +48,8 @@ def main():
     os.makedirs(dest, exist_ok=True)
     # kernel trace: per (kernel, grid) durations
     dur = collections.defaultdict(list)
-    for r in rows(os.path.join(root, 'prof_trace', '**', '*kernel_trace.csv')):
+    tdir = 'prof_trace' if os.path.isdir(os.path.join(root, 'prof_trace')) else 'trace'
+    for r in rows(os.path.join(root, tdir, '**', '*kernel_trace.csv')):
         k = which(r['Kernel_Name'])
         if k:
             grid = int(r['Grid_Size']) if r.get('Grid_Size') else \
@@ -58,8 +61,8 @@ def main():
             shape[k] = grid
     # counters: per (kernel, grid, dispatch, counter) sums
     ctr = collections.defaultdict(lambda: collections.defaultdict(float))
-    for d in sorted(glob.glob(os.path.join(root, 'prof_*'))):
-        if d.endswith('prof_trace'):
+    for d in sorted(glob.glob(os.path.join(root, '*'))):
+        if not os.path.isdir(d) or os.path.basename(d) == tdir:
             continue
         for r in rows(os.path.join(d, '**', '*counter_collection.csv')):
             k = which(r['Kernel_Name'])
@@ -81,13 +84,21 @@ def main():
             res['hbm_bytes_per_launch'] = res['write_bytes'] + res['fetch_bytes']
             res['hbm_GBps_at_traced_duration'] = res['hbm_bytes_per_launch'] / res['duration_ns']
         if 'SQ_ACTIVE_INST_VALU' in res and 'GRBM_GUI_ACTIVE' in res and res['GRBM_GUI_ACTIVE']:
-            res['valu_busy_pct'] = 100.0 * res['SQ_ACTIVE_INST_VALU'] * 4 / (4 * 256) / res['GRBM_GUI_ACTIVE']
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs; SQ_ACTIVE_INST_VALU counts quad-cycles
+            res['valu_busy_pct'] = 100.0 * res['SQ_ACTIVE_INST_VALU'] * 4 / (4 * 256) / (res['GRBM_GUI_ACTIVE'] / 8)
+        if 'SQ_INSTS_VALU' in res and 'GRBM_GUI_ACTIVE' in res and res['GRBM_GUI_ACTIVE']:
+            # a wave64 VALU instruction holds a 16-lane SIMD for 4 cycles: issue-limited share
+            res['valu_issue_pct'] = 100.0 * res['SQ_INSTS_VALU'] * 4 / (4 * 256) / (res['GRBM_GUI_ACTIVE'] / 8)
+        if 'SQ_THREAD_CYCLES_VALU' in res and 'SQ_ACTIVE_INST_VALU' in res and res['SQ_ACTIVE_INST_VALU']:
+            # active lanes per VALU instruction (divergence): thread-cycles / (quad-cycles * 64)
+            res['valu_lane_util_pct'] = 100.0 * res['SQ_THREAD_CYCLES_VALU'] / (res['SQ_ACTIVE_INST_VALU'] * 64)
         if 'SQ_INSTS_VALU' in res and 'SQ_WAVES' in res and res['SQ_WAVES']:
             res['valu_insts_per_wave'] = res['SQ_INSTS_VALU'] / res['SQ_WAVES']
         path = os.path.join(dest, '{}_{}_pmc.json'.format(tag, k))
         with open(path, 'w') as f:
             json.dump(res, f, indent=1, sort_keys=True)
-        print(path, json.dumps({x: res.get(x) for x in ('duration_ns', 'hbm_bytes_per_launch', 'valu_busy_pct')}))
+        print(path, json.dumps({x: res.get(x) for x in ('duration_ns', 'hbm_bytes_per_launch', 'valu_busy_pct',
+                                                        'valu_issue_pct', 'valu_lane_util_pct')}))
 
 
 if __name__ == '__main__':
