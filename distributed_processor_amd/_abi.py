@@ -19,6 +19,7 @@ X_GROUP_MAJOR = 0x2
 X_HIST_DIRECT = 0x4
 X_HIST_REPL = 0x8
 X_PROG_MAJOR = 0x10
+X_GENERAL = 0x20
 
 STATUS_NAMES = {0: 'running', ST_DONE: 'done', ST_MAX_CYCLES: 'max_cycles',
                 ST_HUNG_OPCODE: 'hung_opcode', ST_DEADLOCK: 'deadlock'}

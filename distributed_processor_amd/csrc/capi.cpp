@@ -30,6 +30,7 @@ struct dpemu_ctx {
     uint32_t n_programs = 0, n_groups = 0, C = 0;
     uint64_t n_quads = 0;
     bool has_fproc = false, has_sync = false, straight = false;
+    uint32_t max_len = 0;              // longest program (commands)
     std::vector<uint64_t> group_len;   // instructions of all C programs of each group
     // run constants
     uint32_t *d_thr = nullptr;
@@ -166,12 +167,14 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     for (uint64_t i = 0; i < quads; i++) decode_cmd(words + 4 * i, &uops[4 * i]);
     HIPCHK(ctx, hipMalloc(&ctx->d_uops, uops.size() * 4));
     HIPCHK(ctx, hipMemcpy(ctx->d_uops, uops.data(), uops.size() * 4, hipMemcpyHostToDevice));
-    // ... and command-major (zero = DONE past a program's end) when the padding
-    // stays small: at most 4x the programs, 1 GiB
+    // ... and command-major (zero = DONE past a program's end, and one zero row
+    // past the longest program for straight.hip) when the padding stays small:
+    // at most 4x the programs, 1 GiB
     uint32_t max_len = 0;
     for (uint32_t i = 0; i < n_programs; i++) max_len = std::max(max_len, n_instr[i]);
-    const uint64_t t_cmds = (uint64_t)max_len * n_programs;
-    if (max_len && t_cmds <= std::max<uint64_t>(4 * quads, 4096) && t_cmds * 16 <= (1ull << 30)) {
+    const uint64_t t_cmds = ((uint64_t)max_len + 1) * n_programs;
+    if (max_len && t_cmds <= std::max<uint64_t>(4 * quads + 4 * (uint64_t)n_programs, 4096) &&
+        t_cmds * 16 <= (1ull << 30)) {
         std::vector<uint32_t> ut(t_cmds * 4, 0u);
         for (uint32_t pr = 0; pr < n_programs; pr++)
             for (uint32_t k = 0; k < n_instr[pr]; k++)
@@ -189,6 +192,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     ctx->has_fproc = fp;
     ctx->has_sync = sy;
     ctx->straight = straight;
+    ctx->max_len = max_len;
     ctx->group_len.assign(n_groups, 0);
     for (uint32_t g = 0; g < n_groups; g++)
         for (uint32_t c = 0; c < C; c++) ctx->group_len[g] += n_instr[prog_table[(uint64_t)g * C + c]];
@@ -304,7 +308,26 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     }
     p.prog_lds_words = 0;
     int feat = 0;
-    if (footprint <= PROG_LDS_MAX && (cfg->exec_flags & DPEMU_X_PROG_LDS)) {
+    // pulse-only programs run on the wave-uniform-ip kernel (straight.hip)
+    // unless ip could wrap (a 2^16-command program) or the general interpreter
+    // is forced.  It stages the workgroup's programs in LDS when they fit the
+    // share of a CU's LDS that the grid's co-resident workgroups leave and the
+    // programs are long (a dependent global fetch per command is then the
+    // bottleneck) or staging is asked for; else it fetches the command-major
+    // image.  The general interpreter stages only on request, within 16 KiB.
+    const bool uniform = ctx->straight && ctx->max_len < 65536u && !(cfg->exec_flags & DPEMU_X_GENERAL);
+    int src = cmd_major ? STRAIGHT_ROWS : STRAIGHT_PROG;
+    if (uniform) {
+        const uint64_t blocks = ((uint64_t)p.n_lanes + BLOCK - 1) / BLOCK;
+        const uint64_t per_cu = std::min<uint64_t>(8, std::max<uint64_t>(1, (blocks + 255) / 256));
+        const uint64_t budget = std::min<uint64_t>(STRAIGHT_LDS_MAX, (150ull * 1024 / per_cu) / 16);
+        const bool want = (cfg->exec_flags & DPEMU_X_PROG_LDS) || ctx->max_len >= 64;
+        if (footprint <= budget && want) {
+            src = STRAIGHT_LDS;
+            p.prog_lds_words = (uint32_t)std::max<uint64_t>(16, (footprint + 15) & ~15ull);
+            feat |= FEAT_PROG_LDS;
+        }
+    } else if (footprint <= PROG_LDS_MAX && (cfg->exec_flags & DPEMU_X_PROG_LDS)) {
         feat |= FEAT_PROG_LDS;
         p.prog_lds_words = (uint32_t)std::max<uint64_t>(16, (footprint + 15) & ~15ull);
     }
@@ -349,11 +372,12 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             hist_stride = stride;
         }
     }
-    HIPCHK(ctx, launch_interp(p, feat, stream));
+    if (uniform) HIPCHK(ctx, launch_straight(p, src, stream));
+    else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (out->hist && p.hist_rep)
         HIPCHK(ctx, launch_hist_reduce(ctx->d_hist_rep, R, hist_stride, bins,
                                        reinterpret_cast<unsigned long long *>(out->hist), stream));
-    ctx->last_feat = feat;
+    ctx->last_feat = uniform ? (feat | FEAT_UNIFORM) : feat;
     return DPEMU_OK;
 }
 

@@ -29,11 +29,9 @@
 
 #include <algorithm>
 
-#include "kernels.h"
+#include "lane.h"
 
 namespace dpemu {
-
-#define INF32 0xFFFFFFFFu
 
 enum : uint32_t { M_RUN = 0, M_SYNC = 1, M_LUT = 2, M_FIN = 3 };
 
@@ -53,35 +51,6 @@ __device__ __forceinline__ uint32_t alu_op(uint32_t op, uint32_t a, uint32_t b)
     return r;
 }
 
-// pulse_reg.sv:59-97 for a pre-decoded pulse command (decode_cmd): each field
-// with its write enable takes its immediate (register-sourced fields are
-// zero here and ORed in by the caller)
-__device__ __forceinline__ void pulse_write(const uint4 u, uint32_t &pe, uint32_t &pp, uint32_t &pa)
-{
-    const uint32_t we = u.z >> 26;                  // env cfg phase freq amp
-    const uint32_t clr_e = (we & 1u ? 0x00FFFFFFu : 0u) | (we & 2u ? 0x0F000000u : 0u);
-    const uint32_t clr_p = (we & 4u ? 0x0001FFFFu : 0u) | (we & 8u ? 0x03FE0000u : 0u);
-    pe = (pe & ~clr_e) | (u.y & clr_e);
-    pp = (pp & ~clr_p) | (u.z & clr_p);
-    pa = (we & 16u) ? (u.w & 0xFFFFu) : pa;
-}
-
-// Philox4x32-10, output word 0 (counter = shot_lo, shot_hi, core, m; key = seed)
-__device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m)
-{
-    uint32_t c0 = (uint32_t)shot, c1 = (uint32_t)(shot >> 32), c2 = core, c3 = m;
-    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#pragma unroll
-    for (int r = 0; r < 10; r++) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-    return c0;
-}
-
 // group reductions over the C adjacent lanes of a shot (all lanes converged)
 template <int OP>   // 0 = min, 1 = max
 __device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t C)
@@ -93,35 +62,10 @@ __device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t C)
     return v;
 }
 
-__device__ __forceinline__ uint64_t group_bits(uint64_t ballot, uint32_t lane_in_wave, uint32_t C)
-{
-    const uint32_t base = lane_in_wave & ~(C - 1);
-    const uint64_t gm = (C >= 64) ? ~0ull : ((1ull << C) - 1);
-    return (ballot >> base) & gm;
-}
-
 __device__ __forceinline__ void wave_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-}
-
-// shot index within the run of the block-linear shot position sp: natural order, or
-// group-major (shot_order 1: shots_per_group 1, n_shots = rows * n_groups) so that a
-// workgroup's shots share their programs
-__device__ __forceinline__ uint32_t shot_of_pos(const KParams &p, uint32_t sp)
-{
-    return p.shot_order ? (sp % p.rows) * p.n_groups + sp / p.rows : sp;
-}
-
-// index of the program-group "step" of shot position sp relative to position sp0
-__device__ __forceinline__ uint32_t group_step(const KParams &p, uint32_t sp, uint32_t sp0)
-{
-    if (p.n_groups == 1) return 0;
-    if (p.shot_order) return sp / p.rows - sp0 / p.rows;
-    const uint64_t a = (p.shot_begin + shot_of_pos(p, sp)) / p.shots_per_group;
-    const uint64_t b = (p.shot_begin + shot_of_pos(p, sp0)) / p.shots_per_group;
-    return (uint32_t)(a - b);
 }
 
 template <int FEAT>
@@ -161,14 +105,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 
     uint32_t base = 0, nprog = 0, grp = 0, prog = 0;
     if (valid) {
-        // group of the shot, (shot / spg) % n_groups, from the run's first shot
-        // (g0, r0 from the host) in 32-bit arithmetic: a u64 division would cost
-        // ~150 VALU instructions per lane
-        const uint32_t sl = lane >> p.log2C;                 // shot within the run (< 2^31)
-        const uint64_t num = (uint64_t)p.grp_r0 + sl;
-        const uint32_t q = (num >> 32) ? (uint32_t)(num / p.shots_per_group) : (uint32_t)num / p.shots_per_group;
-        const uint32_t g = p.grp_g0 + q % p.n_groups;       // < 2 n_groups <= 2^32
-        grp = g >= p.n_groups ? g - p.n_groups : g;
+        grp = lane_group(p, lane);
         prog = p.prog_table[(uint64_t)grp * C + core];
         base = p.offsets[prog];
         nprog = p.n_instr[prog];
@@ -182,34 +119,8 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         __syncthreads();
     }
     if constexpr (PLDS) {
-        // slots k = step * C + c over the block's consecutive program groups
-        const uint32_t n_shots = p.n_lanes >> p.log2C;
-        const uint32_t sp0 = (blockIdx.x * BLOCK) >> p.log2C;
-        const uint32_t spl = min(sp0 + (BLOCK >> p.log2C), n_shots) - 1u;
-        const uint32_t g0 = (uint32_t)(((p.shot_begin + shot_of_pos(p, sp0)) / p.shots_per_group) % p.n_groups);
-        const uint32_t nslots = (group_step(p, spl, sp0) + 1u) * C;      // <= BLOCK (host-checked)
-        uint32_t len = 0;
-        if (tid < nslots) {
-            const uint32_t g = (g0 + tid / C) % p.n_groups;
-            len = p.n_instr[p.prog_table[(uint64_t)g * C + (tid & (C - 1))]];
-        }
-        uint32_t total;
-        const uint32_t pre = block_exclusive_scan(len, s_scan, &total);
-        if (tid < nslots) s_pref[tid] = pre;
-        if (tid == 0) s_pref[nslots] = total;
-        __syncthreads();
-        for (uint32_t idx = tid; idx < total; idx += BLOCK) {
-            uint32_t lo = 0, hi = nslots;                // largest k with s_pref[k] <= idx
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_pref[mid] <= idx) lo = mid; else hi = mid;
-            }
-            const uint32_t g = (g0 + lo / C) % p.n_groups;
-            const uint32_t prog = p.prog_table[(uint64_t)g * C + (lo & (C - 1))];
-            s_prog[idx] = p.uops[p.offsets[prog] + (idx - s_pref[lo])];
-        }
-        __syncthreads();
-        if (valid) base = s_pref[group_step(p, spos, sp0) * C + core];
+        const uint32_t b = stage_programs(p, s_prog, s_pref, s_scan, spos);
+        if (valid) base = b;
     }
     if constexpr (!STRAIGHT) {
 #pragma unroll
@@ -246,7 +157,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
             const uint64_t idx = (uint64_t)n_ev * n_lanes + lane;
             if (p.ev_main) {
                 const uint32_t q = (te < qa_t) ? 0u : qa_q + (te - qa_t);
-                p.ev_main[idx] = make_uint4(te, q, pe | (kind << 28), pp);
+                p.ev_main[idx] = make_uint4(te, q, event_word(pe, kind), pp);
             }
             if (p.ev_amp) p.ev_amp[idx] = (uint16_t)pa;
         } else flags |= F_EVENT_OVF;
@@ -429,7 +340,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                     if (go && op4 != 0xC) {
                         // pulse_reg.sv:59-97: immediates, then reg[rs0] into register-sourced fields
                         pulse_write(u, pe, pp, pa);
-                        if (u.z >> 31) {
+                        if (u.w & UOP_ANY_RS) {
                             if (u.w & UOP_RS_ENV) pe |= reg0 & 0xFFFFFFu;
                             if (u.w & UOP_RS_PH) pp |= reg0 & 0x1FFFFu;
                             if (u.w & UOP_RS_FR) pp |= (reg0 & 0x1FFu) << 17;
@@ -616,34 +527,13 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 
     if (valid && p.summary) {
         const uint32_t qclk_end = (t_end < qa_t) ? 0u : qa_q + (t_end - qa_t);
-        uint4 *s = reinterpret_cast<uint4 *>(p.summary + 8ull * lane);
-        s[0] = make_uint4(t_end, (ip & 0xFFFFu) | ((status & 0xFFu) << 16) | ((flags & 0xFFu) << 24),
-                          n_ev, n_exec);
-        s[1] = make_uint4(qclk_end, n_meas, meas_bits, n_tr);
+        write_summary(p, lane, t_end, ip, status, flags, n_ev, n_exec, qclk_end, n_meas, meas_bits, n_tr);
     }
     if (valid && p.regs_out) {
 #pragma unroll
         for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = STRAIGHT ? 0u : s_regs[r][tid];
     }
-    if (p.hist_rep) {
-        // outcome key: bit c = last measurement of core c; one count per shot
-        const uint64_t key = group_bits(__ballot(last_bit != 0u), wl, C);
-        const uint64_t bin = (uint64_t)grp * (1ull << C) + key;
-        uint32_t *rep = p.hist_rep + (uint64_t)(blockIdx.x % p.hist_reps) * p.hist_stride;
-        if (p.hist_lds) {
-            // small histogram: aggregate the workgroup's shots in LDS first
-            if (valid && core == 0u) atomicAdd(&s_hist[bin], 1u);
-            __syncthreads();
-            const uint32_t bins = p.n_groups << C;
-            for (uint32_t i = tid; i < bins; i += BLOCK)
-                if (s_hist[i]) atomicAdd(&rep[i], s_hist[i]);
-        } else if (valid && core == 0u) {
-            atomicAdd(&rep[bin], 1u);
-        }
-    } else if (p.hist) {
-        const uint64_t key = group_bits(__ballot(last_bit != 0u), wl, C);
-        if (valid && core == 0u) atomicAdd(&p.hist[(uint64_t)grp * (1ull << C) + key], 1ull);
-    }
+    count_outcome(p, s_hist, valid, core, grp, last_bit);
 }
 
 // out[i] += sum of the R replicas; thread = (bin, slice of 8 replicas), loads independent

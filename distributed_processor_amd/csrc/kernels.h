@@ -42,6 +42,7 @@ constexpr int FEAT_SYNC = 2;    // SYNC barriers
 constexpr int FEAT_LUT = 4;     // fproc_lut back end
 constexpr int FEAT_PROG_LDS = 8; // the workgroup's programs staged in LDS (fits PROG_LDS_MAX)
 constexpr int FEAT_STRAIGHT = 16; // only pulse / idle / done / hang opcodes: no register file
+constexpr int FEAT_UNIFORM = 32;  // (reporting) FEAT_STRAIGHT run by straight_kernel: wave-uniform ip
 constexpr uint32_t PROG_LDS_MAX = 1024;   // commands (16 KiB) of dynamic LDS per workgroup
 
 constexpr uint32_t ST_DONE = DPEMU_ST_DONE, ST_MAX_CYCLES = DPEMU_ST_MAX_CYCLES;
@@ -59,12 +60,14 @@ constexpr uint32_t TRACE_QCLK_LOAD = DPEMU_TRACE_QCLK_LOAD, TRACE_QCLK_RST = DPE
 //   y  op4[31:28]; pulse writes: env[23:0] cfg[27:24] immediates (zero when the
 //      field is not written or register-sourced); other ops: alu[2:0]
 //      in0_reg[3] rs1[7:4] rd[11:8]
-//   z  pulse writes: phase[16:0] freq[25:17] immediates, write enables
-//      env[26] cfg[27] phase[28] freq[29] amp[30], any register-sourced[31]
-//      (hdl/pulse_reg.sv:38-97); other ops: target[15:0] fproc_id[23:16]
+//   z  pulse writes: phase[16:0] freq[25:17] immediates (bits 31:26 zero);
+//      other ops: target[15:0] fproc_id[23:16]
 //   w  rs0[23:20] (cmd[119:116]); pulse writes: amp[15:0] immediate,
-//      register-sourced env[16] phase[17] freq[18] amp[19]
+//      register-sourced env[16] phase[17] freq[18] amp[19], write enables
+//      env[24] cfg[25] phase[26] freq[27] amp[28] (hdl/pulse_reg.sv:38-97),
+//      any register-sourced field[29]
 constexpr uint32_t UOP_RS_ENV = 1u << 16, UOP_RS_PH = 1u << 17, UOP_RS_FR = 1u << 18, UOP_RS_AMP = 1u << 19;
+constexpr uint32_t UOP_ANY_RS = 1u << 29;
 
 __host__ __device__ inline void decode_cmd(const uint32_t w[4], uint32_t u[4])
 {
@@ -86,9 +89,9 @@ __host__ __device__ inline void decode_cmd(const uint32_t w[4], uint32_t u[4])
         const uint32_t cfg_we = (w[1] >> 9) & 1u;
         const uint32_t rs = (env_we & env_rs) | ((ph_we & ph_rs) << 1) | ((fr_we & fr_rs) << 2) | ((amp_we & amp_rs) << 3);
         u[1] = (op4 << 28) | (env_we && !env_rs ? env_i : 0u) | (cfg_we ? cfg_i << 24 : 0u);
-        u[2] = (ph_we && !ph_rs ? ph_i : 0u) | (fr_we && !fr_rs ? fr_i << 17 : 0u) | (env_we << 26) |
-               (cfg_we << 27) | (ph_we << 28) | (fr_we << 29) | (amp_we << 30) | ((rs ? 1u : 0u) << 31);
-        u[3] = (rs0 << 20) | (amp_we && !amp_rs ? amp_i : 0u) | (rs << 16);
+        u[2] = (ph_we && !ph_rs ? ph_i : 0u) | (fr_we && !fr_rs ? fr_i << 17 : 0u);
+        u[3] = (rs0 << 20) | (amp_we && !amp_rs ? amp_i : 0u) | (rs << 16) | (env_we << 24) | (cfg_we << 25) |
+               (ph_we << 26) | (fr_we << 27) | (amp_we << 28) | ((rs ? 1u : 0u) << 29);
     }
 }
 
@@ -132,6 +135,10 @@ hipError_t launch_hist_reduce(const uint32_t *rep, uint32_t R, uint64_t stride, 
                               unsigned long long *hist, hipStream_t stream);
 
 hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
+// pulse-only programs (straight.hip); src: where commands are fetched from
+enum { STRAIGHT_ROWS = 0, STRAIGHT_PROG = 1, STRAIGHT_LDS = 2 };
+constexpr uint32_t STRAIGHT_LDS_MAX = 9216;   // commands (144 KiB) of dynamic LDS per workgroup
+hipError_t launch_straight(const KParams &p, int src, hipStream_t stream);
 
 // ---- DDS ------------------------------------------------------------------
 struct DDSParams {

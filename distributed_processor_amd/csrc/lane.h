@@ -1,0 +1,172 @@
+// lane.h -- per-lane helpers shared by the interpreter kernels (interp.hip:
+// the general lockstep interpreter; straight.hip: pulse-only programs).
+#pragma once
+
+#include "kernels.h"
+
+namespace dpemu {
+
+#define INF32 0xFFFFFFFFu
+
+// pulse_reg.sv:59-97 for a pre-decoded pulse command (decode_cmd): each field
+// with its write enable takes its immediate (register-sourced fields are zero
+// here and ORed in by the caller).  Enables are sign-extended to masks
+// (v_bfe_i32) and merged with 3-input bit selects (v_bitop3_b32 0xCA = a ? b : c
+// per bit): 10 VALU.  pe[31:28] picks up the opcode and pa[31:16] other
+// command bits: consumers mask them (pe & 0x0FFFFFFF, (uint16_t)pa).
+__device__ __forceinline__ uint32_t bit_select(uint32_t m, uint32_t a, uint32_t b)
+{
+    return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
+}
+
+__device__ __forceinline__ void pulse_write(const uint4 u, uint32_t &pe, uint32_t &pp, uint32_t &pa)
+{
+    const int32_t w = (int32_t)u.w;
+    const uint32_t m_env = (uint32_t)((w << 7) >> 31);      // enable bit 24
+    const uint32_t m_cfg = (uint32_t)((w << 6) >> 31);      // 25
+    const uint32_t m_ph = (uint32_t)((w << 5) >> 31);       // 26
+    const uint32_t m_fr = (uint32_t)((w << 4) >> 31);       // 27
+    const uint32_t m_amp = (uint32_t)((w << 3) >> 31);      // 28
+    pe = bit_select(bit_select(0x00FFFFFFu, m_env, m_cfg), u.y, pe);
+    pp = bit_select(bit_select(0x0001FFFFu, m_ph, m_fr), u.z, pp);
+    pa = bit_select(m_amp, u.w, pa);
+}
+
+// event word 2: env[23:0] cfg[27:24] kind[31:28]
+__device__ __forceinline__ uint32_t event_word(uint32_t pe, uint32_t kind)
+{
+    return (pe & 0x0FFFFFFFu) | (kind << 28);
+}
+
+// Philox4x32-10, output word 0 (counter = shot_lo, shot_hi, core, m; key = seed)
+__device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m)
+{
+    uint32_t c0 = (uint32_t)shot, c1 = (uint32_t)(shot >> 32), c2 = core, c3 = m;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return c0;
+}
+
+__device__ __forceinline__ uint64_t group_bits(uint64_t ballot, uint32_t lane_in_wave, uint32_t C)
+{
+    const uint32_t base = lane_in_wave & ~(C - 1);
+    const uint64_t gm = (C >= 64) ? ~0ull : ((1ull << C) - 1);
+    return (ballot >> base) & gm;
+}
+
+// shot index within the run of the block-linear shot position sp: natural order, or
+// group-major (shot_order 1: shots_per_group 1, n_shots = rows * n_groups) so that a
+// workgroup's shots share their programs
+__device__ __forceinline__ uint32_t shot_of_pos(const KParams &p, uint32_t sp)
+{
+    return p.shot_order ? (sp % p.rows) * p.n_groups + sp / p.rows : sp;
+}
+
+// program group of output lane `lane`: (shot / spg) % n_groups from the run's
+// first shot (g0, r0 from the host) in 32-bit arithmetic -- a u64 division
+// would cost ~150 VALU instructions per lane
+__device__ __forceinline__ uint32_t lane_group(const KParams &p, uint32_t lane)
+{
+    const uint32_t sl = lane >> p.log2C;                 // shot within the run (< 2^31)
+    const uint64_t num = (uint64_t)p.grp_r0 + sl;
+    const uint32_t q = (num >> 32) ? (uint32_t)(num / p.shots_per_group) : (uint32_t)num / p.shots_per_group;
+    const uint32_t g = p.grp_g0 + q % p.n_groups;       // < 2 n_groups <= 2^32
+    return g >= p.n_groups ? g - p.n_groups : g;
+}
+
+// index of the program-group "step" of shot position sp relative to position sp0
+__device__ __forceinline__ uint32_t group_step(const KParams &p, uint32_t sp, uint32_t sp0)
+{
+    if (p.n_groups == 1) return 0;
+    if (p.shot_order) return sp / p.rows - sp0 / p.rows;
+    const uint64_t a = (p.shot_begin + shot_of_pos(p, sp)) / p.shots_per_group;
+    const uint64_t b = (p.shot_begin + shot_of_pos(p, sp0)) / p.shots_per_group;
+    return (uint32_t)(a - b);
+}
+
+// Stage the programs of this workgroup's (group, core) slots in LDS -- the
+// analogue of each core's cmd_mem -- and return the LDS command index of
+// program slot (group of shot position spos, core).  Slots k = step * C + c
+// run over the block's consecutive program groups (at most BLOCK slots and
+// the footprint within the dynamic LDS: host-checked).  Every thread of the
+// workgroup calls it (barriers).  s_pref: BLOCK + 1 words, s_scan: BLOCK / 64.
+__device__ __forceinline__ uint32_t stage_programs(const KParams &p, uint4 *s_prog, uint32_t *s_pref,
+                                                   uint32_t *s_scan, uint32_t spos)
+{
+    const uint32_t tid = threadIdx.x, C = p.C;
+    const uint32_t n_shots = p.n_lanes >> p.log2C;
+    const uint32_t sp0 = (blockIdx.x * BLOCK) >> p.log2C;
+    const uint32_t spl = min(sp0 + (BLOCK >> p.log2C), n_shots) - 1u;
+    const uint32_t g0 = (uint32_t)(((p.shot_begin + shot_of_pos(p, sp0)) / p.shots_per_group) % p.n_groups);
+    const uint32_t nslots = (group_step(p, spl, sp0) + 1u) * C;
+    uint32_t len = 0;
+    if (tid < nslots) {
+        const uint32_t g = (g0 + tid / C) % p.n_groups;
+        len = p.n_instr[p.prog_table[(uint64_t)g * C + (tid & (C - 1))]];
+    }
+    uint32_t total;
+    const uint32_t pre = block_exclusive_scan(len, s_scan, &total);
+    if (tid < nslots) s_pref[tid] = pre;
+    if (tid == 0) s_pref[nslots] = total;
+    __syncthreads();
+    for (uint32_t idx = tid; idx < total; idx += BLOCK) {
+        uint32_t lo = 0, hi = nslots;                    // largest k with s_pref[k] <= idx
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_pref[mid] <= idx) lo = mid; else hi = mid;
+        }
+        const uint32_t g = (g0 + lo / C) % p.n_groups;
+        const uint32_t prog = p.prog_table[(uint64_t)g * C + (lo & (C - 1))];
+        s_prog[idx] = p.uops[p.offsets[prog] + (idx - s_pref[lo])];
+    }
+    __syncthreads();
+    const uint32_t sp = min(spos, spl);                  // threads past the run: any slot
+    return s_pref[group_step(p, sp, sp0) * C + (threadIdx.x & (C - 1))];
+}
+
+// dpemu_outputs::summary row of a lane (include/dpemu.h)
+__device__ __forceinline__ void write_summary(const KParams &p, uint32_t lane, uint32_t t_end, uint32_t ip,
+                                              uint32_t status, uint32_t flags, uint32_t n_ev, uint32_t n_exec,
+                                              uint32_t qclk_end, uint32_t n_meas, uint32_t meas_bits, uint32_t n_tr)
+{
+    uint4 *s = reinterpret_cast<uint4 *>(p.summary + 8ull * lane);
+    s[0] = make_uint4(t_end, (ip & 0xFFFFu) | ((status & 0xFFu) << 16) | ((flags & 0xFFu) << 24), n_ev, n_exec);
+    s[1] = make_uint4(qclk_end, n_meas, meas_bits, n_tr);
+}
+
+// outcome histogram: bit c of the key = last measurement of core c; one count per
+// shot into bin grp << C | key (direct u64 atomics, or a privatised u32 replica
+// with optional LDS pre-aggregation; capi.cpp chooses).  Called by every thread
+// of the workgroup (the LDS path has a barrier).
+__device__ __forceinline__ void count_outcome(const KParams &p, uint32_t *s_hist, bool valid, uint32_t core,
+                                              uint32_t grp, uint32_t last_bit)
+{
+    const uint32_t C = p.C, tid = threadIdx.x, wl = tid & 63;
+    if (p.hist_rep) {
+        const uint64_t key = group_bits(__ballot(last_bit != 0u), wl, C);
+        const uint64_t bin = (uint64_t)grp * (1ull << C) + key;
+        uint32_t *rep = p.hist_rep + (uint64_t)(blockIdx.x % p.hist_reps) * p.hist_stride;
+        if (p.hist_lds) {
+            // small histogram: aggregate the workgroup's shots in LDS first
+            if (valid && core == 0u) atomicAdd(&s_hist[bin], 1u);
+            __syncthreads();
+            const uint32_t bins = p.n_groups << C;
+            for (uint32_t i = tid; i < bins; i += BLOCK)
+                if (s_hist[i]) atomicAdd(&rep[i], s_hist[i]);
+        } else if (valid && core == 0u) {
+            atomicAdd(&rep[bin], 1u);
+        }
+    } else if (p.hist) {
+        const uint64_t key = group_bits(__ballot(last_bit != 0u), wl, C);
+        if (valid && core == 0u) atomicAdd(&p.hist[(uint64_t)grp * (1ull << C) + key], 1ull);
+    }
+}
+
+}  // namespace dpemu

@@ -36,6 +36,7 @@ class Gen:
     def __init__(self, rng, ncores, mode='meas', allow_late=False, allow_hang=False, meas_latency=20,
                  straight=False):
         self.straight = straight          # pulse / idle / pulse_reset / done only
+        self.shape = None                 # fixed opcode-kind sequence (shaped_case)
         self.rng = rng
         self.ncores = ncores
         self.mode = mode
@@ -64,8 +65,11 @@ class Gen:
         r = self.rng
         i = 0
         while i < n:
-            kind = r.choices(['trig', 'pw', 'idle', 'prst', 'alu', 'incq', 'jc', 'ji', 'loop', 'fproc'],
-                             [10, 3, 2, 1, 0, 0, 0, 0, 0, 0] if self.straight else [10, 3, 2, 1, 6, 2, 2, 1, 1, 2])[0]
+            if self.shape is not None:
+                kind = self.shape[i]
+            else:
+                kind = r.choices(['trig', 'pw', 'idle', 'prst', 'alu', 'incq', 'jc', 'ji', 'loop', 'fproc'],
+                                 [10, 3, 2, 1, 0, 0, 0, 0, 0, 0] if self.straight else [10, 3, 2, 1, 6, 2, 2, 1, 1, 2])[0]
             if kind == 'trig':
                 if self.allow_late and r.random() < 0.05:
                     t = (q - r.randint(1, 4)) & 0xFFFFFFFF
@@ -196,3 +200,16 @@ def random_case(seed, ncores=None, mode=None, allow_late=True, allow_hang=True, 
     progs = [g.program(n_sync, body) for _ in range(n_groups * ncores)]
     table = np.arange(n_groups * ncores, dtype=np.uint32)
     return dict(ncores=ncores, mode=mode, n_groups=n_groups, progs=progs, table=table, rng=rng)
+
+
+def shaped_case(seed, ncores, n_groups=4, allow_late=True, allow_hang=True):
+    """pulse-only programs that share one opcode sequence with random parameters
+    (cmd_times, pulse fields, late triggers) per (group, core), and a random
+    final command: the batched-experiment shape whose lanes agree on the opcode
+    at every step until their endings differ"""
+    rng = random.Random(seed)
+    g = Gen(rng, ncores, 'meas', allow_late, allow_hang, straight=True)
+    g.shape = rng.choices(['trig', 'pw', 'idle', 'prst'], [10, 3, 2, 1], k=rng.randint(3, 16))
+    progs = [g.program(0, len(g.shape)) for _ in range(n_groups * ncores)]
+    table = np.arange(n_groups * ncores, dtype=np.uint32)
+    return dict(ncores=ncores, mode='meas', n_groups=n_groups, progs=progs, table=table, rng=rng)

@@ -15,7 +15,7 @@ import pytest
 import oracle
 from distributed_processor_amd import _abi, workloads
 from distributed_processor_amd.emulator import Emulator, ProgramSet
-from tests.progfuzz import pack_programs, random_case
+from tests.progfuzz import pack_programs, random_case, shaped_case
 
 pytestmark = pytest.mark.gpu
 
@@ -42,12 +42,14 @@ def compare_all(gpu, ref, ctx=''):
 
 def run_pair(emu, ps, cfg, n_shots, shot0=0):
     """GPU run and oracle; the execution variants (LDS-staged programs,
-    group-major thread order, histogram strategy) must produce the same bytes"""
+    group-major thread order, histogram strategy, program-major fetch, the
+    general interpreter for pulse-only programs) must produce the same bytes"""
     emu.load(ps)
     g = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
     f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n_shots, want=ALL_OUT)
     base = cfg.exec_flags
-    for flags in (_abi.X_PROG_LDS | _abi.X_GROUP_MAJOR | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT | _abi.X_PROG_MAJOR):
+    for flags in (_abi.X_PROG_LDS | _abi.X_GROUP_MAJOR | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT | _abi.X_PROG_MAJOR,
+                  _abi.X_GENERAL):
         cfg.exec_flags = flags
         g2 = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
         compare_all(g2.arrays, g.arrays, 'execution variant {:#x}'.format(flags))
@@ -71,18 +73,39 @@ def test_fuzz_gpu_vs_fast(emu, seed):
     compare_all(g, f, 'seed {}'.format(seed))
 
 
-@pytest.mark.parametrize('seed', range(12))
+@pytest.mark.parametrize('seed', range(16))
 def test_fuzz_straight_programs(emu, seed):
-    """pulse / idle / pulse_reset / done / hang programs (the register-free
-    kernel specialisation): register-sourced pulse fields read 0, late
-    triggers, the reset-hold double strobe"""
+    """pulse / idle / pulse_reset / done / hang programs (straight.hip, and the
+    general interpreter's register-free specialisation): register-sourced
+    pulse fields read 0, late triggers, the reset-hold double strobe; seeds
+    >= 12 with tight cycle / event / measurement caps (max_cycles finishes
+    before and at a fetch, dropped events and measurements)"""
     C = [1, 2, 4, 8][seed % 4]
     case = random_case(9000 + seed, ncores=C, mode='meas', allow_late=True, allow_hang=True, straight=True)
     groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
     ps = ProgramSet(groups, cores_per_shot=C)
-    cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=6000, event_cap=64, trace_cap=16,
-                           meas_cap=16, meas_latency=1 + seed, seed=seed)
+    tight = seed >= 12
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=150 + 40 * seed if tight else 6000,
+                           event_cap=3 if tight else 64, trace_cap=16, meas_cap=1 if tight else 16,
+                           meas_latency=1 + seed, seed=seed)
     g, f = run_pair(emu, ps, cfg, 777, shot0=seed * 31)
+    compare_all(g, f, 'seed {}'.format(seed))
+
+
+@pytest.mark.parametrize('seed', range(16))
+def test_fuzz_shaped_straight_programs(emu, seed):
+    """pulse-only programs sharing one opcode sequence (straight.hip's
+    uniform-opcode path) with per-lane parameters, endings, late triggers;
+    odd seeds with tight cycle / event / measurement caps"""
+    C = [1, 2, 4, 8][seed % 4]
+    case = shaped_case(12000 + seed, C, n_groups=1 + seed % 5)
+    groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
+    ps = ProgramSet(groups, cores_per_shot=C)
+    tight = seed % 2 == 1
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=100 + 30 * seed if tight else 6000,
+                           event_cap=2 + seed % 3 if tight else 64, trace_cap=4, meas_cap=1 if tight else 16,
+                           meas_latency=1 + seed, seed=seed, meas_elem=seed % 4)
+    g, f = run_pair(emu, ps, cfg, 1000 + 37 * seed, shot0=seed * 77)
     compare_all(g, f, 'seed {}'.format(seed))
 
 
