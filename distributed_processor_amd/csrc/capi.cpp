@@ -29,7 +29,7 @@ struct dpemu_ctx {
     uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
     uint32_t n_programs = 0, n_groups = 0, C = 0;
     uint64_t n_quads = 0;
-    bool has_fproc = false, has_sync = false, straight = false;
+    bool has_fproc = false, has_sync = false, straight = false, linear = false;
     uint32_t max_len = 0;              // longest program (commands)
     std::vector<uint64_t> group_len;   // instructions of all C programs of each group
     // run constants
@@ -141,7 +141,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1)))
         return fail(ctx, DPEMU_E_INVALID, "cores_per_shot %u is not a power of two in [1, 64]", C);
     uint64_t quads = 0;
-    bool fp = false, sy = false, straight = true;
+    bool fp = false, sy = false, straight = true, linear = true;
     for (uint32_t i = 0; i < n_programs; i++) {
         if (n_instr[i] > 65536u)
             return fail(ctx, DPEMU_E_INVALID, "program %u: %u commands exceed the 2^16-deep cmd_mem", i, n_instr[i]);
@@ -153,6 +153,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
             fp |= (op4 == 4 || op4 == 5);
             sy |= (op4 == 7);
             straight &= !(op4 >= 1 && op4 <= 7);
+            linear &= !(op4 >= 2 && op4 <= 5) && op4 != 7;     // no jump / fproc / sync: ip advances by 1
         }
     for (uint64_t i = 0; i < (uint64_t)n_groups * C; i++)
         if (prog_table[i] >= n_programs)
@@ -162,9 +163,16 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     HIPCHK(ctx, hipMalloc(&ctx->d_offsets, n_programs * 4));
     HIPCHK(ctx, hipMalloc(&ctx->d_ninstr, n_programs * 4));
     HIPCHK(ctx, hipMalloc(&ctx->d_table, (uint64_t)n_groups * C * 4));
-    // every command pre-decoded once (kernels.h decode_cmd), program-major ...
-    std::vector<uint32_t> uops(std::max<uint64_t>(quads, 1) * 4, 0u);
-    for (uint64_t i = 0; i < quads; i++) decode_cmd(words + 4 * i, &uops[4 * i]);
+    // every command pre-decoded once (kernels.h decode_cmd), program-major with
+    // a zero (DONE) guard command after every program ...
+    std::vector<uint32_t> goff(n_programs);
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < n_programs; i++) { goff[i] = (uint32_t)tot; tot += (uint64_t)n_instr[i] + 1; }
+    if (tot >= (1ull << 32)) return fail(ctx, DPEMU_E_INVALID, "program set exceeds 2^32 commands");
+    std::vector<uint32_t> uops(tot * 4, 0u);
+    for (uint32_t i = 0; i < n_programs; i++)
+        for (uint32_t k = 0; k < n_instr[i]; k++)
+            decode_cmd(words + 4 * ((uint64_t)offsets[i] + k), &uops[4 * ((uint64_t)goff[i] + k)]);
     HIPCHK(ctx, hipMalloc(&ctx->d_uops, uops.size() * 4));
     HIPCHK(ctx, hipMemcpy(ctx->d_uops, uops.data(), uops.size() * 4, hipMemcpyHostToDevice));
     // ... and command-major (zero = DONE past a program's end, and one zero row
@@ -173,16 +181,16 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     uint32_t max_len = 0;
     for (uint32_t i = 0; i < n_programs; i++) max_len = std::max(max_len, n_instr[i]);
     const uint64_t t_cmds = ((uint64_t)max_len + 1) * n_programs;
-    if (max_len && t_cmds <= std::max<uint64_t>(4 * quads + 4 * (uint64_t)n_programs, 4096) &&
+    if (max_len && t_cmds <= std::max<uint64_t>(4 * tot, 4096) &&
         t_cmds * 16 <= (1ull << 30)) {
         std::vector<uint32_t> ut(t_cmds * 4, 0u);
         for (uint32_t pr = 0; pr < n_programs; pr++)
             for (uint32_t k = 0; k < n_instr[pr]; k++)
-                memcpy(&ut[4 * ((uint64_t)k * n_programs + pr)], &uops[4 * ((uint64_t)offsets[pr] + k)], 16);
+                memcpy(&ut[4 * ((uint64_t)k * n_programs + pr)], &uops[4 * ((uint64_t)goff[pr] + k)], 16);
         HIPCHK(ctx, hipMalloc(&ctx->d_uops_t, t_cmds * 16));
         HIPCHK(ctx, hipMemcpy(ctx->d_uops_t, ut.data(), t_cmds * 16, hipMemcpyHostToDevice));
     }
-    HIPCHK(ctx, hipMemcpy(ctx->d_offsets, offsets, n_programs * 4, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->d_offsets, goff.data(), n_programs * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->d_ninstr, n_instr, n_programs * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->d_table, prog_table, (uint64_t)n_groups * C * 4, hipMemcpyHostToDevice));
     ctx->n_programs = n_programs;
@@ -192,10 +200,11 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     ctx->has_fproc = fp;
     ctx->has_sync = sy;
     ctx->straight = straight;
+    ctx->linear = linear;
     ctx->max_len = max_len;
     ctx->group_len.assign(n_groups, 0);
     for (uint32_t g = 0; g < n_groups; g++)
-        for (uint32_t c = 0; c < C; c++) ctx->group_len[g] += n_instr[prog_table[(uint64_t)g * C + c]];
+        for (uint32_t c = 0; c < C; c++) ctx->group_len[g] += n_instr[prog_table[(uint64_t)g * C + c]] + 1;   // + guard
     return DPEMU_OK;
 }
 
@@ -247,6 +256,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.fetch = cmd_major ? ctx->d_uops_t : ctx->d_uops;
     p.fetch_stride = cmd_major ? ctx->n_programs : 1u;
     p.offsets = ctx->d_offsets; p.n_instr = ctx->d_ninstr; p.prog_table = ctx->d_table;
+    p.max_len = ctx->max_len;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
     p.summary = out->summary;
     p.ev_main = reinterpret_cast<uint4 *>(out->ev_main);
@@ -308,19 +318,32 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     }
     p.prog_lds_words = 0;
     int feat = 0;
-    // pulse-only programs run on the wave-uniform-ip kernel (straight.hip)
+    // Branch-free programs run on the wave-uniform-ip kernel (straight.hip)
     // unless ip could wrap (a 2^16-command program) or the general interpreter
-    // is forced.  It stages the workgroup's programs in LDS when they fit the
-    // share of a CU's LDS that the grid's co-resident workgroups leave and the
-    // programs are long (a dependent global fetch per command is then the
-    // bottleneck) or staging is asked for; else it fetches the command-major
-    // image.  The general interpreter stages only on request, within 16 KiB.
-    const bool uniform = ctx->straight && ctx->max_len < 65536u && !(cfg->exec_flags & DPEMU_X_GENERAL);
+    // is forced: pulse-only programs always, programs with reg_alu / inc_qclk
+    // on grids of <= 4 workgroups per CU, where latency (not VALU throughput)
+    // bounds the general interpreter -- at full occupancy its per-opcode
+    // switch retires a mixed wave's commands with fewer instructions.  Those
+    // small grids also fetch commands in batches of 4.  The kernel stages the
+    // workgroup's programs in LDS when they fit the share of a CU's LDS that
+    // the grid's co-resident workgroups leave and the programs are long (a
+    // dependent global fetch per command is then the bottleneck) or staging is
+    // asked for; else it fetches the command-major image.  The general
+    // interpreter stages only on request, within 16 KiB.
+    // A/B knobs: DPEMU_LINEAR = 0 / 1 never / always runs ALU programs on
+    // straight.hip; DPEMU_FETCH_BATCH = 1 / 4 forces the batch.
+    const uint64_t blocks = ((uint64_t)p.n_lanes + BLOCK - 1) / BLOCK;
+    const bool small = blocks <= 4 * 256;
+    const char *lin_env = getenv("DPEMU_LINEAR"), *fb_env = getenv("DPEMU_FETCH_BATCH");
+    const bool linear_ok = lin_env ? atoi(lin_env) != 0 : small;
+    const int fetch_batch = fb_env ? (atoi(fb_env) == 1 ? 1 : 4) : (small ? 4 : 1);
+    const bool uniform = (ctx->straight || (ctx->linear && linear_ok)) && ctx->max_len < 65536u &&
+                         !(cfg->exec_flags & DPEMU_X_GENERAL);
+    const bool regs = !ctx->straight;
     int src = cmd_major ? STRAIGHT_ROWS : STRAIGHT_PROG;
     if (uniform) {
-        const uint64_t blocks = ((uint64_t)p.n_lanes + BLOCK - 1) / BLOCK;
         const uint64_t per_cu = std::min<uint64_t>(8, std::max<uint64_t>(1, (blocks + 255) / 256));
-        const uint64_t budget = std::min<uint64_t>(STRAIGHT_LDS_MAX, (150ull * 1024 / per_cu) / 16);
+        const uint64_t budget = std::min<uint64_t>(STRAIGHT_LDS_MAX, ((regs ? 134ull : 150ull) * 1024 / per_cu) / 16);
         const bool want = (cfg->exec_flags & DPEMU_X_PROG_LDS) || ctx->max_len >= 64;
         if (footprint <= budget && want) {
             src = STRAIGHT_LDS;
@@ -372,7 +395,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             hist_stride = stride;
         }
     }
-    if (uniform) HIPCHK(ctx, launch_straight(p, src, stream));
+    if (uniform) HIPCHK(ctx, launch_straight(p, src, regs, fetch_batch, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (out->hist && p.hist_rep)
         HIPCHK(ctx, launch_hist_reduce(ctx->d_hist_rep, R, hist_stride, bins,

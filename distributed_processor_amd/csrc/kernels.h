@@ -103,7 +103,8 @@ struct KParams {
                                   //   program count selects the command-major copy (zero past a
                                   //   program's end), where adjacent lanes -- adjacent programs --
                                   //   fetch adjacent commands
-    const uint32_t *offsets, *n_instr, *prog_table;
+    const uint32_t *offsets, *n_instr, *prog_table;   // uops: a zero guard command follows every program
+    uint32_t max_len;             // longest program; the command-major image's guard row
     const uint32_t *p1_thr;
     const uint64_t *lut_table;
     // outputs (device, nullable)
@@ -135,10 +136,12 @@ hipError_t launch_hist_reduce(const uint32_t *rep, uint32_t R, uint64_t stride, 
                               unsigned long long *hist, hipStream_t stream);
 
 hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
-// pulse-only programs (straight.hip); src: where commands are fetched from
+// branch-free programs (straight.hip); src: where commands are fetched from;
+// regs: programs with reg_alu / inc_qclk (register file in LDS); fb: commands
+// fetched per batch (1 or 4)
 enum { STRAIGHT_ROWS = 0, STRAIGHT_PROG = 1, STRAIGHT_LDS = 2 };
 constexpr uint32_t STRAIGHT_LDS_MAX = 9216;   // commands (144 KiB) of dynamic LDS per workgroup
-hipError_t launch_straight(const KParams &p, int src, hipStream_t stream);
+hipError_t launch_straight(const KParams &p, int src, bool regs, int fb, hipStream_t stream);
 
 // ---- DDS ------------------------------------------------------------------
 struct DDSParams {

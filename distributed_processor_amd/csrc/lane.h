@@ -92,8 +92,9 @@ __device__ __forceinline__ uint32_t group_step(const KParams &p, uint32_t sp, ui
 }
 
 // Stage the programs of this workgroup's (group, core) slots in LDS -- the
-// analogue of each core's cmd_mem -- and return the LDS command index of
-// program slot (group of shot position spos, core).  Slots k = step * C + c
+// analogue of each core's cmd_mem -- each with its zero guard command, and
+// return the LDS command index of program slot (group of shot position spos,
+// core).  Slots k = step * C + c
 // run over the block's consecutive program groups (at most BLOCK slots and
 // the footprint within the dynamic LDS: host-checked).  Every thread of the
 // workgroup calls it (barriers).  s_pref: BLOCK + 1 words, s_scan: BLOCK / 64.
@@ -109,7 +110,7 @@ __device__ __forceinline__ uint32_t stage_programs(const KParams &p, uint4 *s_pr
     uint32_t len = 0;
     if (tid < nslots) {
         const uint32_t g = (g0 + tid / C) % p.n_groups;
-        len = p.n_instr[p.prog_table[(uint64_t)g * C + (tid & (C - 1))]];
+        len = p.n_instr[p.prog_table[(uint64_t)g * C + (tid & (C - 1))]] + 1u;   // + guard
     }
     uint32_t total;
     const uint32_t pre = block_exclusive_scan(len, s_scan, &total);

@@ -1,30 +1,41 @@
-// straight.hip -- the interpreter for pulse-only programs on CDNA4 (gfx950).
+// straight.hip -- the interpreter for branch-free programs on CDNA4 (gfx950).
 //
-// A program whose commands are all pulse writes / pulse triggers / idles /
-// done / hung opcodes (no ALU, jump, fproc or sync: op4 outside 1..7) never
-// writes the register file and never moves its instruction pointer except by
-// +1 (hdl/instr_ptr.v with no jump), and its qclk is never reloaded
-// (hdl/qclk.v: only ALU-class commands load it).  So every lane still running
-// in loop iteration k is executing command k of its program: the command
-// index is wave-uniform, the fetch address is k * stride (SALU) + program
-// (one VALU add), and the per-lane ip / qclk-anchor / mode state of the
-// general interpreter (interp.hip) disappears.  Timing is ctrl.v's closed
-// form for pulse-class commands with qclk = cycle - 1 (qclk.v after the
-// two-cycle reset hold); the first command is peeled to model the hold
-// (cmd_time 0 there strobes twice, oracle/fast_model.c).
+// A program with no jump, fproc or sync command (op4 not in {2, 3, 4, 5, 7})
+// never moves its instruction pointer except by +1 (hdl/instr_ptr.v without
+// a jump).  So every lane still running in loop iteration k is executing
+// command k of its program: the command index is wave-uniform, the per-lane
+// ip / mode state of the general interpreter (interp.hip) disappears, and the
+// next commands' addresses are known before the current one executes, so
+// they are fetched in batches of FB (one memory latency per FB commands).
 //
-// Outputs and their layout are identical to interp_kernel's; the launcher
-// (capi.cpp) picks this kernel for pulse-only program sets whose longest
-// program is shorter than the 2^16-deep cmd_mem (so ip never wraps).
+// Two specialisations:
+//   REGS = false  pulse-only programs (pulse write / trigger, idle, pulse
+//                 reset, done, hang): no register file, qclk never reloaded
+//                 (hdl/qclk.v), so qclk(D) = D - 1 after the two-cycle reset
+//                 hold;
+//   REGS = true   plus reg_alu (op4 1) and inc_qclk (op4 6): the 16 x 32-bit
+//                 reg_file in LDS as [reg][lane] (alu.v, reg_file.v),
+//                 register-sourced pulse fields, register / qclk traces and a
+//                 qclk anchor that inc_qclk reloads.
+// Timing is hdl/ctrl.v's closed form (oracle/fast_model.c); the first
+// command is peeled to model the reset hold (cmd_time 0 there strobes twice).
+// Outputs and their layout are identical to interp_kernel's.
 //
 // Commands come from the command-major image (STRAIGHT_ROWS: command k of
-// program p at fetch[k * n_programs + p], with a zero = DONE row past the
-// longest program, so every lane alive in iteration k <= its length reads in
-// bounds), the program-major one (STRAIGHT_PROG: offsets[p] + k, guarded by
-// k < length) or the workgroup's programs staged in LDS (STRAIGHT_LDS, for
-// long programs on grids too small to hide global-memory latency: an LDS
-// fetch does not wait for the lane's earlier event stores, which share
-// vmcnt with global loads).
+// program p at fetch[k * n_programs + p], zero = DONE past a program's end
+// and in the guard row max_len), the program-major image (STRAIGHT_PROG:
+// uops[offsets[p] + min(k, n_instr[p])], a zero guard command after every
+// program) or the workgroup's programs staged in LDS with their guards
+// (STRAIGHT_LDS, long programs on grids that leave LDS to spare: an LDS fetch
+// does not wait for the lane's earlier event stores, which share vmcnt with
+// global loads).  Every fetch is clamped in bounds, so loads are unconditional.
+//
+// Lanes that finish keep walking the loop with their state frozen by selects
+// (a divergent branch that writes loop-carried state makes the register
+// allocator copy that state around it every iteration); branches guard only
+// stores, LDS register writes and philox.  When the running lanes also share
+// the opcode (the batched-experiment shape: one program structure, different
+// parameters) a scalar switch runs that opcode's straight-line semantics.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -33,13 +44,31 @@
 
 namespace dpemu {
 
-template <int SRC>
+
+// alu.v:20-50; le = sub[31] ^ overflow == signed a < b
+__device__ __forceinline__ uint32_t alu_eval(uint32_t op, uint32_t a, uint32_t b)
+{
+    const uint32_t sub = a - b;
+    const uint32_t lt = (int32_t)a < (int32_t)b;
+    uint32_t r = a;                 // 0: id0
+    r = (op == 1) ? a + b : r;
+    r = (op == 2) ? sub : r;
+    r = (op == 3) ? (uint32_t)(sub == 0) : r;
+    r = (op == 4) ? lt : r;
+    r = (op == 5) ? (lt ^ 1u) : r;
+    r = (op == 6) ? b : r;
+    r = (op == 7) ? 0u : r;
+    return r;
+}
+
+template <int SRC, bool REGS, int FB>
 __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
 {
     constexpr bool ROWS = SRC == STRAIGHT_ROWS, LDS = SRC == STRAIGHT_LDS;
     __shared__ uint32_t s_hist[HIST_LDS_MAX];
     __shared__ uint32_t s_pref[LDS ? BLOCK + 1 : 1];
     __shared__ uint32_t s_scan[BLOCK / 64];
+    __shared__ uint32_t s_regs[REGS ? 16 : 1][REGS ? BLOCK : 1];
     extern __shared__ uint4 s_prog[];
     const uint32_t tid = threadIdx.x;
     const uint32_t C = p.C;
@@ -63,25 +92,25 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         __syncthreads();
     }
     if constexpr (LDS) base = stage_programs(p, s_prog, s_pref, s_scan, pos >> p.log2C);
+    if constexpr (REGS) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
+    }
 
     const uint32_t max_cycles = p.max_cycles;
     uint32_t t = 0, pe = 0, pp = 0, pa = 0;            // next DECODE cycle; pulse register image
-    uint32_t flags = 0, n_ev = 0, n_meas = 0, meas_bits = 0, last_bit = 0;
+    uint32_t qa_t = 1, qa_q = 0;                       // qclk(t) = qa_q + t - qa_t for t >= qa_t
+    uint32_t flags = 0, n_ev = 0, n_meas = 0, meas_bits = 0, last_bit = 0, n_tr = 0;
     // st: 0 while running, else the finish status (| ST_TOP: stopped by the
     // max_cycles check before a fetch, so that command did not retire); k_end:
     // the command index at the finish.  A finish leaves t alone: t_end = t
     constexpr uint32_t ST_TOP = 0x100u;
     uint32_t st = valid ? 0u : ST_DONE, k_end = 0;
 
-    // State updates below are selects, not branches: a divergent branch that
-    // writes loop-carried state makes the register allocator copy that state
-    // around it on every iteration.  Branches guard only stores and philox.
-    //
     // pulse_iface strobe at cycle te, qclk q (kind 0: trigger, 1: phase reset)
     // with the current pulse registers, for lanes with `ok`; readout-element
     // triggers draw the measurement.  Overflow flags are derived from the
-    // final counts (an event / measurement is dropped iff its count exceeds
-    // the cap)
+    // final counts (a record is dropped iff its count exceeds the cap)
     auto emit = [&](bool ok, uint32_t te, uint32_t q, uint32_t kind) {
         if (ok && n_ev < p.event_cap) {
             const uint64_t slot = (uint64_t)n_ev * n_lanes + lane;
@@ -102,29 +131,48 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         n_meas += is_meas ? 1u : 0u;
     };
 
-    // command k of a running lane (k <= its program length, so the command-major
-    // fetch is in bounds)
+    // register write / qclk load record (trace_cap 0: trace output off)
+    auto trace = [&](bool ok, uint32_t tt, uint32_t addr, uint32_t val) {
+        if (ok && n_tr < p.trace_cap && p.trace)
+            p.trace[(uint64_t)n_tr * n_lanes + lane] = make_uint4(tt, addr, val, 0u);
+        n_tr += ok ? 1u : 0u;
+    };
+
+    // command k of this lane's program, zero (DONE) past its end; in bounds for any k
     auto fetch = [&](uint32_t k) -> uint4 {
         if constexpr (ROWS) {
-            return p.fetch[(uint64_t)(k * p.fetch_stride) + prog];
+            return p.fetch[(uint64_t)(min(k, p.max_len) * p.fetch_stride) + prog];
         } else {
-            uint4 u = make_uint4(0u, 0u, 0u, 0u);           // past the program: op4 0 = DONE
-            if (k < nprog) u = LDS ? s_prog[base + k] : p.fetch[(uint64_t)base + k];
-            return u;
+            const uint32_t i = base + min(k, nprog);
+            return LDS ? s_prog[i] : p.fetch[i];
         }
     };
 
-    // retire command u = k for the lanes still running: any opcode, any state
-    auto retire = [&](const uint4 u, uint32_t k, bool first) {
-        const bool live = st == 0u;
+    // register-sourced pulse fields: reg[rs0] ORed into the cleared fields
+    auto pulse_regs = [&](const uint4 u, uint32_t reg0) {
+        pe |= (u.w & UOP_RS_ENV) ? (reg0 & 0xFFFFFFu) : 0u;
+        pp |= (u.w & UOP_RS_PH) ? (reg0 & 0x1FFFFu) : 0u;
+        pp |= (u.w & UOP_RS_FR) ? ((reg0 & 0x1FFu) << 17) : 0u;
+        pa = (u.w & UOP_RS_AMP) ? (reg0 & 0xFFFFu) : pa;
+    };
+
+    // retire command u = k for the lanes in `live` (running): any opcode, any state
+    auto retire = [&](const uint4 u, uint32_t k, bool first, bool live) {
         const uint32_t D = t;
         const uint32_t op4 = u.y >> 28;
         // opcode classes as bit tables: cmd_time wait 9/C, pulse class 8/9/B/C,
-        // strobe 9/B.  Pulse writes need no class: decode_cmd leaves the write
-        // enables of every other opcode zero, so pulse_write is a no-op there
+        // strobe 9/B, ALU class 1/6.  Pulse writes need no class: decode_cmd
+        // leaves the write enables and register-source bits of every other
+        // opcode zero, so pulse_write / pulse_regs are no-ops there
         const bool waits = (0x1200u >> op4) & 1u;
         const bool pulse_cls = (0x1B00u >> op4) & 1u;
         const bool strobe = (0x0A00u >> op4) & 1u;
+        const bool alu_cls = REGS && ((0x0042u >> op4) & 1u);
+        uint32_t reg0 = 0, reg1 = 0;
+        if constexpr (REGS) {
+            reg0 = s_regs[(u.w >> 20) & 15u][tid];
+            reg1 = s_regs[(u.y >> 4) & 15u][tid];
+        }
         const uint32_t T = u.x;
         uint32_t wait;
         bool big = false, dbl = false;
@@ -134,26 +182,42 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
             wait = dbl ? 0u : T + 1u;
             big = T == INF32;
         } else {
-            wait = T - (D - 1u);                            // qclk(D) = D - 1 for D >= 3
+            wait = T - (qa_q + (D - qa_t));                 // D > qa_t after the first command
         }
         const bool top = D > max_cycles;
         const bool over = waits && (big || wait > max_cycles - D);
         flags |= (live && !top && waits && (big || wait >= 0x80000000u)) ? F_LATE : 0u;
         const uint32_t fin = top ? (ST_MAX_CYCLES | ST_TOP) : over ? ST_MAX_CYCLES
-                           : pulse_cls ? 0u : (op4 >= 0xDu ? ST_HUNG_OPCODE : ST_DONE);
+                           : (pulse_cls || alu_cls) ? 0u : (op4 >= 0xDu ? ST_HUNG_OPCODE : ST_DONE);
         st = live ? fin : st;
         k_end = live ? k : k_end;
         const bool ok = live && fin == 0u;
         const uint32_t tT = D + (waits ? wait : 0u);
-        pulse_write(u, pe, pp, pa);                     // pulse_reg.sv:59-97, reg_in = 0
+        pulse_write(u, pe, pp, pa);                     // pulse_reg.sv:59-97
+        if constexpr (REGS) pulse_regs(u, reg0);
         const bool rst = op4 == 0xBu;
-        emit(ok && strobe, rst ? D : tT + 2u, rst ? (first ? 0u : D - 1u) : tT + 1u, rst ? 1u : 0u);
+        // qclk of the strobe: first command (qa = (1, 0)) 0 at cycle 0
+        const uint32_t te = rst ? D : tT + 2u;
+        emit(ok && strobe, te, first ? (te ? te - 1u : 0u) : qa_q + (te - qa_t), rst ? 1u : 0u);
         if (first) {
             const bool two = ok && dbl && op4 == 0x9u;
             emit(two, tT + 3u, tT + 2u, 0u);
             flags |= two ? F_DOUBLE_STROBE : 0u;
         }
-        t = ok ? tT + 3u : t;
+        if constexpr (REGS) {
+            // reg_alu: reg[rd] = alu(in0, reg[rs1]); inc_qclk: qclk = alu(in0, qclk(D)) + 3 at D + 3
+            const uint32_t in0 = (u.y & 8u) ? reg0 : u.x;
+            const uint32_t qD = first ? 0u : qa_q + (D - qa_t);
+            const bool is_q = op4 == 0x6u;
+            const uint32_t out = alu_eval(u.y & 7u, in0, is_q ? qD : reg1);
+            const uint32_t rd = (u.y >> 8) & 15u;
+            if (ok && op4 == 0x1u) s_regs[rd][tid] = out;
+            trace(ok && alu_cls, D + 3u, is_q ? TRACE_QCLK_LOAD : rd, is_q ? out + 3u : out);
+            const bool load = ok && is_q;
+            qa_t = load ? D + 3u : qa_t;
+            qa_q = load ? out + 3u : qa_q;
+        }
+        t = ok ? (alu_cls ? D + 4u : tT + 3u) : t;
     };
 
     // the cmd_time wait of a pulse / idle command after the first: past the
@@ -163,7 +227,7 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
     auto timed = [&](const uint4 u, uint32_t k, uint32_t &tT) -> bool {
         const bool live = st == 0u;
         const uint32_t D = t;
-        const uint32_t wait = u.x - (D - 1u);
+        const uint32_t wait = u.x - (qa_q + (D - qa_t));
         const bool stop = live && wait > max_cycles - D;
         flags |= (stop && wait >= 0x80000000u) ? F_LATE : 0u;
         st = stop ? ST_MAX_CYCLES : st;
@@ -172,17 +236,13 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         return live && !stop;
     };
 
-    // Every lane walks the loop (finished lanes only select their old state),
-    // so the loop and the per-opcode switch below branch on scalars.  The
-    // running lanes share k; when they also share the opcode and none is past
-    // max_cycles (the common case: the same program shape with different
-    // parameters) the switch runs that opcode's straight-line semantics
-    retire(fetch(0u), 0u, true);
-    for (uint32_t k = 1;; k++) {
-        const uint64_t running = __ballot(st == 0u);
-        if (running == 0ull) break;
-        const uint4 u = fetch(k);
+    // one command for all lanes (finished ones keep their state): a scalar
+    // switch on the opcode when the running lanes agree on it and none is past
+    // max_cycles, else the any-opcode path.  (A waterfall over the distinct
+    // opcodes of a mixed wave measured slower than the any-opcode path.)
+    auto step = [&](const uint4 u, uint32_t k) {
         const uint32_t op4 = u.y >> 28;
+        const uint64_t running = __ballot(st == 0u);
         const uint32_t op_u = __builtin_amdgcn_readlane(op4, (int)__builtin_ctzll(running));
         const bool live = st == 0u;
         uint32_t tT;
@@ -190,7 +250,8 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         case 0x9: {                                         // pulse write + trigger at cmd_time
             const bool ok = timed(u, k, tT);
             pulse_write(u, pe, pp, pa);
-            emit(ok, tT + 2u, tT + 1u, 0u);
+            if constexpr (REGS) pulse_regs(u, s_regs[(u.w >> 20) & 15u][tid]);
+            emit(ok, tT + 2u, qa_q + (tT + 2u - qa_t), 0u);
             t = ok ? tT + 3u : t;
             break;
         }
@@ -201,54 +262,79 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         }
         case 0x8:                                           // pulse write, no trigger
             pulse_write(u, pe, pp, pa);
+            if constexpr (REGS) pulse_regs(u, s_regs[(u.w >> 20) & 15u][tid]);
             t = live ? t + 3u : t;
             break;
         case 0xB:                                           // phase reset strobe at decode
-            emit(live, t, t - 1u, 1u);
+            emit(live, t, qa_q + (t - qa_t), 1u);
             t = live ? t + 3u : t;
             break;
         case 0x0: case 0xA:                                 // done
             st = live ? ST_DONE : st;
             k_end = live ? k : k_end;
             break;
-        default:                                            // mixed opcodes, hung, past max_cycles
-            retire(u, k, false);
+        default:                                            // ALU / qclk, mixed opcodes, hung, past max_cycles
+            retire(u, k, false, live);
+        }
+    };
+
+    retire(fetch(0u), 0u, true, st == 0u);
+    for (uint32_t k = 1; __ballot(st == 0u); k += FB) {
+        uint4 u[FB];
+#pragma unroll
+        for (int j = 0; j < FB; j++) u[j] = fetch(k + j);  // independent loads: one latency per batch
+#pragma unroll
+        for (int j = 0; j < FB; j++) {
+            if (j && !__ballot(st == 0u)) break;
+            step(u[j], k + j);
         }
     }
     flags |= (n_ev > p.event_cap ? F_EVENT_OVF : 0u) |
-             (n_meas > min(p.meas_cap, MEAS_LOOKUP) ? F_MEAS_OVF : 0u);
+             (n_meas > min(p.meas_cap, MEAS_LOOKUP) ? F_MEAS_OVF : 0u) |
+             (p.trace_cap && n_tr > p.trace_cap ? F_TRACE_OVF : 0u);
 
     if (valid && p.summary)
         write_summary(p, lane, t, k_end, st & 0xFFu, flags, n_ev, k_end + ((st & ST_TOP) ? 0u : 1u),
-                      t ? t - 1u : 0u, n_meas, meas_bits, 0u);
+                      t < qa_t ? 0u : qa_q + (t - qa_t), n_meas, meas_bits, n_tr);
     if (valid && p.regs_out) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = 0u;
+        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = REGS ? s_regs[r][tid] : 0u;
     }
     count_outcome(p, s_hist, valid, core, grp, last_bit);
 }
 
-hipError_t launch_straight(const KParams &p, int src, hipStream_t stream)
+template <int SRC, bool REGS, int FB>
+static hipError_t launch_src(const KParams &p, uint32_t blocks, size_t shmem, hipStream_t stream)
 {
-    const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
-    if (blocks == 0) return hipSuccess;
-    if (src == STRAIGHT_ROWS) {
-        hipLaunchKernelGGL(straight_kernel<STRAIGHT_ROWS>, dim3(blocks), dim3(BLOCK), 0, stream, p);
-    } else if (src == STRAIGHT_PROG) {
-        hipLaunchKernelGGL(straight_kernel<STRAIGHT_PROG>, dim3(blocks), dim3(BLOCK), 0, stream, p);
-    } else {
+    if (shmem > 64 * 1024) {
         // programs staged in dynamic LDS beyond the default 64 KiB need the opt-in
-        const size_t shmem = (size_t)p.prog_lds_words * sizeof(uint4);
         static size_t granted = 0;
         if (shmem > granted) {
-            hipError_t e = hipFuncSetAttribute((const void *)straight_kernel<STRAIGHT_LDS>,
+            hipError_t e = hipFuncSetAttribute((const void *)straight_kernel<SRC, REGS, FB>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
             if (e != hipSuccess) return e;
             granted = shmem;
         }
-        hipLaunchKernelGGL(straight_kernel<STRAIGHT_LDS>, dim3(blocks), dim3(BLOCK), shmem, stream, p);
     }
+    hipLaunchKernelGGL((straight_kernel<SRC, REGS, FB>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
     return hipGetLastError();
+}
+
+hipError_t launch_straight(const KParams &p, int src, bool regs, int fb, hipStream_t stream)
+{
+    const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
+    if (blocks == 0) return hipSuccess;
+    const size_t shmem = src == STRAIGHT_LDS ? (size_t)p.prog_lds_words * sizeof(uint4) : 0;
+#define SRC_CASE(S)                                                                                    \
+    case S: return regs ? (fb == 1 ? launch_src<S, true, 1>(p, blocks, shmem, stream)                 \
+                                   : launch_src<S, true, 4>(p, blocks, shmem, stream))                \
+                        : (fb == 1 ? launch_src<S, false, 1>(p, blocks, shmem, stream)                \
+                                   : launch_src<S, false, 4>(p, blocks, shmem, stream));
+    switch (src) {
+    SRC_CASE(STRAIGHT_ROWS) SRC_CASE(STRAIGHT_PROG) SRC_CASE(STRAIGHT_LDS)
+    }
+#undef SRC_CASE
+    return hipErrorInvalidValue;
 }
 
 }  // namespace dpemu

@@ -27,6 +27,10 @@ cases = {
     'config3_reset': (rst, 10 ** 6, dict(meas_latency=workloads.CONFIG3_MEAS_LATENCY, max_cycles=1 << 16,
                                          event_cap=16, meas_cap=4), OUT),
     'config4_rb_2core': (rb, 10 ** 5, dict(n_groups=1000, shots_per_group=100, event_cap=512, meas_cap=4), OUT),
+    'config4_rb_summary': (rb, 10 ** 5, dict(n_groups=1000, shots_per_group=100, event_cap=512, meas_cap=4),
+                           ('summary',)),
+    'config4_rb_1e6': (rb, 10 ** 6, dict(n_groups=1000, shots_per_group=1000, event_cap=512, meas_cap=4),
+                       ('summary', 'meas', 'hist')),
 }
 libs = {'new': Emulator(0), 'old': Emulator(0, lib_path=os.path.join(REPO, 'distributed_processor_amd',
                                                                      'libdpemu_ab.so'))}

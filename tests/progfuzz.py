@@ -34,8 +34,9 @@ def raw(op4, in0_reg=0, alu_op=0, imm=0, rs0=0, rs1=0, rd=0, target=0, fproc_id=
 
 class Gen:
     def __init__(self, rng, ncores, mode='meas', allow_late=False, allow_hang=False, meas_latency=20,
-                 straight=False):
+                 straight=False, linear=False):
         self.straight = straight          # pulse / idle / pulse_reset / done only
+        self.linear = linear              # plus reg_alu / inc_qclk: no jump, fproc or sync
         self.shape = None                 # fixed opcode-kind sequence (shaped_case)
         self.rng = rng
         self.ncores = ncores
@@ -69,7 +70,9 @@ class Gen:
                 kind = self.shape[i]
             else:
                 kind = r.choices(['trig', 'pw', 'idle', 'prst', 'alu', 'incq', 'jc', 'ji', 'loop', 'fproc'],
-                                 [10, 3, 2, 1, 0, 0, 0, 0, 0, 0] if self.straight else [10, 3, 2, 1, 6, 2, 2, 1, 1, 2])[0]
+                                 [10, 3, 2, 1, 0, 0, 0, 0, 0, 0] if self.straight else
+                                 [10, 3, 2, 1, 6, 2, 0, 0, 0, 0] if self.linear else
+                                 [10, 3, 2, 1, 6, 2, 2, 1, 1, 2])[0]
             if kind == 'trig':
                 if self.allow_late and r.random() < 0.05:
                     t = (q - r.randint(1, 4)) & 0xFFFFFFFF
@@ -189,27 +192,31 @@ def pack_programs(progs):
     return words, np.array(offsets, np.uint32), np.array(n_instr, np.uint32)
 
 
-def random_case(seed, ncores=None, mode=None, allow_late=True, allow_hang=True, n_groups=None, straight=False):
+def random_case(seed, ncores=None, mode=None, allow_late=True, allow_hang=True, n_groups=None, straight=False,
+                linear=False):
     rng = random.Random(seed)
     ncores = ncores or rng.choice([1, 2, 4])
     mode = mode or rng.choice(['meas', 'meas', 'lut'])
     n_groups = n_groups or rng.choice([1, 2])
-    n_sync = 0 if straight else (rng.choice([0, 0, 1, 2]) if ncores > 1 else rng.choice([0, 1]))
-    g = Gen(rng, ncores, mode, allow_late, allow_hang, straight=straight)
+    n_sync = 0 if (straight or linear) else (rng.choice([0, 0, 1, 2]) if ncores > 1 else rng.choice([0, 1]))
+    g = Gen(rng, ncores, mode, allow_late, allow_hang, straight=straight, linear=linear)
     body = rng.randint(3, 14)
     progs = [g.program(n_sync, body) for _ in range(n_groups * ncores)]
     table = np.arange(n_groups * ncores, dtype=np.uint32)
     return dict(ncores=ncores, mode=mode, n_groups=n_groups, progs=progs, table=table, rng=rng)
 
 
-def shaped_case(seed, ncores, n_groups=4, allow_late=True, allow_hang=True):
-    """pulse-only programs that share one opcode sequence with random parameters
-    (cmd_times, pulse fields, late triggers) per (group, core), and a random
-    final command: the batched-experiment shape whose lanes agree on the opcode
-    at every step until their endings differ"""
+def shaped_case(seed, ncores, n_groups=4, allow_late=True, allow_hang=True, linear=False):
+    """branch-free programs that share one opcode sequence with random
+    parameters (cmd_times, pulse fields, ALU operands, late triggers) per
+    (group, core), and a random final command: the batched-experiment shape
+    whose lanes agree on the opcode at every step until their endings differ.
+    linear: reg_alu / inc_qclk commands in the sequence too"""
     rng = random.Random(seed)
-    g = Gen(rng, ncores, 'meas', allow_late, allow_hang, straight=True)
-    g.shape = rng.choices(['trig', 'pw', 'idle', 'prst'], [10, 3, 2, 1], k=rng.randint(3, 16))
+    g = Gen(rng, ncores, 'meas', allow_late, allow_hang, straight=not linear, linear=linear)
+    kinds, weights = (['trig', 'pw', 'idle', 'prst', 'alu', 'incq'], [10, 3, 2, 1, 6, 2]) if linear else \
+        (['trig', 'pw', 'idle', 'prst'], [10, 3, 2, 1])
+    g.shape = rng.choices(kinds, weights, k=rng.randint(3, 16))
     progs = [g.program(0, len(g.shape)) for _ in range(n_groups * ncores)]
     table = np.arange(n_groups * ncores, dtype=np.uint32)
     return dict(ncores=ncores, mode='meas', n_groups=n_groups, progs=progs, table=table, rng=rng)

@@ -109,6 +109,27 @@ def test_fuzz_shaped_straight_programs(emu, seed):
     compare_all(g, f, 'seed {}'.format(seed))
 
 
+@pytest.mark.parametrize('seed', range(16))
+def test_fuzz_linear_programs(emu, seed):
+    """branch-free programs with reg_alu / inc_qclk (straight.hip with the
+    register file; all 8 ALU ops, register-sourced pulse fields, qclk
+    reloads), random per lane (odd seeds) or sharing one opcode sequence (even
+    seeds); seeds >= 8 with tight cycle / event / trace / measurement caps"""
+    C = [1, 2, 4, 8][seed % 4]
+    if seed % 2:
+        case = random_case(15000 + seed, ncores=C, mode='meas', allow_late=True, allow_hang=True, linear=True)
+    else:
+        case = shaped_case(16000 + seed, C, n_groups=1 + seed % 3, linear=True)
+    groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
+    ps = ProgramSet(groups, cores_per_shot=C)
+    tight = seed >= 8
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=120 + 25 * seed if tight else 6000,
+                           event_cap=3 if tight else 64, trace_cap=2 if tight else 64,
+                           meas_cap=1 if tight else 16, meas_latency=1 + seed, seed=seed, meas_elem=seed % 4)
+    g, f = run_pair(emu, ps, cfg, 900 + 41 * seed, shot0=seed * 13)
+    compare_all(g, f, 'seed {}'.format(seed))
+
+
 @pytest.mark.parametrize('C', [1, 2, 4, 8, 16, 32, 64])
 def test_fuzz_all_group_sizes(emu, C):
     case = random_case(500 + C, ncores=C, mode='meas', allow_late=True, allow_hang=True)
