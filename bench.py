@@ -34,6 +34,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+PROFILE_TAG = 'r01'            # profiles/<tag>_{interp,dds}_pmc.json: PMC passes of this workload
 
 
 def build_workload(n_points=100, n_cores=8):
@@ -130,24 +131,26 @@ def dds_leg(emu, args, world, rank, stream):
     for _ in range(args.warmup):
         emu.synthesize(plan, ev, n_samples, iq, stream)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    emu.kernel_times()                                # drop earlier records
+    emu.kernel_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for a, b in evs:
-        a.record(stream)
+    for _ in range(args.steps):
         emu.synthesize(plan, ev, n_samples, iq, stream)
-        b.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    emu.kernel_timing(False)
+    kt = emu.kernel_times()
+    assert len(kt) == args.steps, kt
+    kernel_ms = float(np.mean(kt))                    # HIP events around the DDS kernel, same stream
     samples = plan.n_channels * n_samples
     gbs = samples * 4 / (kernel_ms * 1e-3) / 1e9
     traffic = None
-    pmc = os.path.join(REPO, 'profiles', 'r01_dds_pmc.json')
+    pmc = os.path.join(REPO, 'profiles', PROFILE_TAG + '_dds_pmc.json')
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get('hbm_bytes_per_launch')
@@ -158,7 +161,7 @@ def dds_leg(emu, args, world, rank, stream):
                       'samples_per_channel': n_samples, 'rb_depth': 200},
            'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                         'frac': gbs / HBM_PEAK_GBS, 'traffic': traffic, 'bytes_per_launch': samples * 4,
-                        'kernel': 'dpemu::dds_kernel'}}
+                        'kernel': 'dpemu::dds_chunk_kernel'}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host_ev = {k: v.cpu().numpy() for k, v in ev.items()}
         res['cpu_baseline'] = dds_cpu_baseline(plan, host_ev, n_samples, args.cpu_seconds * 2 / 3)
@@ -206,32 +209,31 @@ def main():
     stream = torch.cuda.current_stream()
     shot0, n = sharding.weak_shard(n, rank)
 
-    def step(ev_pair=None):
+    def step():
         out['hist'].zero_()
-        if ev_pair:
-            ev_pair[0].record(stream)
         emu.run_device(cfg, n, shot0, out, stream)
-        if ev_pair:
-            ev_pair[1].record(stream)
         sharding.allreduce_histogram(out['hist'])     # the path's only exchange (RCCL)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    emu.kernel_timing(True)                           # HIP events around the interpreter kernel
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(events[k])
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    emu.kernel_timing(False)
+    kt = emu.kernel_times()
+    assert len(kt) == args.steps, kt
+    kernel_ms = float(np.mean(kt))
+    kernel_name = emu.last_kernel()
 
     # accounting from the last step's outputs (identical every step)
     summ = out['summary'].cpu().numpy().view(np.uint32)
@@ -248,11 +250,18 @@ def main():
     value = total_core_shots / dt
     achieved_gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
-    traffic = None
-    pmc = os.path.join(REPO, 'profiles', 'r01_interp_pmc.json')
+    # rocprofv3 PMC passes of this workload (scripts/gpu_r01.sh -> profiles/): HBM
+    # bytes per launch, and the VALU view (instructions per wave, issue share,
+    # active lanes per VALU instruction = divergence)
+    traffic, valu = None, None
+    pmc = os.path.join(REPO, 'profiles', PROFILE_TAG + '_interp_pmc.json')
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get('hbm_bytes_per_launch')
+            prof = json.load(f)
+        traffic = prof.get('hbm_bytes_per_launch')
+        valu = {k: prof.get(k) for k in ('valu_insts_per_wave', 'valu_issue_pct', 'valu_lane_util_pct',
+                                         'duration_ns', 'kernel')}
+        valu['source'] = os.path.relpath(pmc, REPO)
 
     result = {
         'metric': 'emulated core-shots/s (config 2: 8-core Ramsey, 100 delays, 1e6 shots/GPU)',
@@ -276,8 +285,8 @@ def main():
         'kernel_ms': kernel_ms,
         'roofline': {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved_gbs / HBM_PEAK_GBS, 'traffic': traffic,
-                     'bytes_per_launch': alg_bytes,
-                     'kernel': 'dpemu::interp_kernel<0>'},
+                     'bytes_per_launch': alg_bytes, 'kernel_ms': kernel_ms,
+                     'kernel': 'dpemu::' + kernel_name, 'valu': valu},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline(ps, cfg, args.cpu_seconds)

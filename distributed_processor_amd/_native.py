@@ -9,7 +9,8 @@ LIB_PATH = os.path.join(HERE, 'libdpemu.so')
 
 # every entry point declared in include/dpemu.h
 EXPORTS = ('dpemu_abi_version', 'dpemu_create', 'dpemu_destroy', 'dpemu_last_error',
-           'dpemu_load_programs', 'dpemu_run', 'dpemu_run_host', 'dpemu_dds', 'dpemu_dds_sin_lut')
+           'dpemu_load_programs', 'dpemu_run', 'dpemu_run_host', 'dpemu_dds', 'dpemu_dds_sin_lut',
+           'dpemu_set_kernel_timing', 'dpemu_kernel_times', 'dpemu_last_kernel')
 
 _libs = {}
 
@@ -46,6 +47,10 @@ def load_library(path=LIB_PATH):
     L.dpemu_run_host.argtypes = [vp, vp, u64, u64, vp]
     L.dpemu_dds.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.dpemu_dds_sin_lut.argtypes = [vp]
+    L.dpemu_set_kernel_timing.argtypes = [vp, C.c_int]
+    L.dpemu_kernel_times.argtypes = [vp, vp, C.c_int, vp]
+    L.dpemu_last_kernel.argtypes = [vp]
+    L.dpemu_last_kernel.restype = C.c_char_p
     from . import _abi
     if L.dpemu_abi_version() != _abi.ABI_VERSION:
         raise DpemuError('ABI version mismatch: library {} vs host {}'.format(

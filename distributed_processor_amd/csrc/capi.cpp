@@ -47,6 +47,10 @@ struct dpemu_ctx {
     uint32_t dds_probe = 0;                 // DPEMU_DDS_PROBE: store-pattern probes (A/B only)
     uint32_t dds_lds_pad = 0;               // DPEMU_DDS_LDSPAD: occupancy A/B
     int last_feat = -1;
+    std::string last_kernel;                // variant the last dpemu_run launched (dpemu_last_kernel)
+    // kernel timing (dpemu_set_kernel_timing): event pairs recorded around main kernels
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
     // privatised outcome histograms (R replicas, reduced after the interpreter)
     uint32_t *d_hist_rep = nullptr;
     uint64_t hist_rep_bytes = 0;
@@ -70,6 +74,27 @@ static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...)
         if (e_ != hipSuccess)                                                              \
             return fail(ctx, DPEMU_E_DEVICE, "%s: %s", #call, hipGetErrorString(e_));      \
     } while (0)
+
+// kernel timing: record the start event of a main-kernel launch on `stream`;
+// *stop gets the pair's stop event (null while timing is off)
+static hipError_t timing_start(dpemu_ctx *ctx, hipStream_t stream, hipEvent_t *stop)
+{
+    *stop = nullptr;
+    if (!ctx->timing) return hipSuccess;
+    std::pair<hipEvent_t, hipEvent_t> e;
+    if (!ctx->ev_free.empty()) {
+        e = ctx->ev_free.back();
+        ctx->ev_free.pop_back();
+    } else {
+        hipError_t r = hipEventCreate(&e.first);
+        if (r != hipSuccess) return r;
+        r = hipEventCreate(&e.second);
+        if (r != hipSuccess) { (void)hipEventDestroy(e.first); return r; }
+    }
+    ctx->ev_used.push_back(e);
+    *stop = e.second;
+    return hipEventRecord(e.first, stream);
+}
 
 static void free_programs(dpemu_ctx *ctx)
 {
@@ -124,11 +149,38 @@ int dpemu_destroy(dpemu_ctx *ctx)
     free_programs(ctx);
     (void)hipFree(ctx->d_thr); (void)hipFree(ctx->d_lut); (void)hipFree(ctx->d_sin); (void)hipFree(ctx->d_ch);
     (void)hipFree(ctx->d_hist_rep);
+    for (auto *v : {&ctx->ev_used, &ctx->ev_free})
+        for (auto &e : *v) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     delete ctx;
     return DPEMU_OK;
 }
 
 const char *dpemu_last_error(dpemu_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+const char *dpemu_last_kernel(dpemu_ctx *ctx) { return ctx ? ctx->last_kernel.c_str() : ""; }
+
+int dpemu_set_kernel_timing(dpemu_ctx *ctx, int enable)
+{
+    if (!ctx) return DPEMU_E_INVALID;
+    ctx->timing = enable != 0;
+    return DPEMU_OK;
+}
+
+int dpemu_kernel_times(dpemu_ctx *ctx, float *ms, int max_n, int *n_out)
+{
+    if (!ctx || (max_n > 0 && !ms)) return DPEMU_E_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int n = 0;
+    for (auto &e : ctx->ev_used) {
+        HIPCHK(ctx, hipEventSynchronize(e.second));
+        if (n < max_n) HIPCHK(ctx, hipEventElapsedTime(&ms[n], e.first, e.second));
+        n++;
+    }
+    ctx->ev_free.insert(ctx->ev_free.end(), ctx->ev_used.begin(), ctx->ev_used.end());
+    ctx->ev_used.clear();
+    if (n_out) *n_out = n < max_n ? n : max_n;
+    return DPEMU_OK;
+}
 
 int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *offsets,
                         const uint32_t *n_instr, uint32_t n_programs, const uint32_t *prog_table,
@@ -395,8 +447,21 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             hist_stride = stride;
         }
     }
+    hipEvent_t ev_stop = nullptr;
+    HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, regs, fetch_batch, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
+    if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, stream));
+    {
+        char name[96];
+        if (uniform)
+            snprintf(name, sizeof name, "straight_kernel<%s,%s,fb%d>",
+                     src == STRAIGHT_ROWS ? "rows" : src == STRAIGHT_PROG ? "prog" : "lds",
+                     regs ? "regs" : "pulse", fetch_batch);
+        else
+            snprintf(name, sizeof name, "interp_kernel<feat=0x%x>", feat);
+        ctx->last_kernel = name;
+    }
     if (out->hist && p.hist_rep)
         HIPCHK(ctx, launch_hist_reduce(ctx->d_hist_rep, R, hist_stride, bins,
                                        reinterpret_cast<unsigned long long *>(out->hist), stream));
@@ -533,6 +598,9 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.rows = ctx->dds_rows;
     p.probe = ctx->dds_probe;
     p.lds_pad = ctx->dds_lds_pad;
+    hipEvent_t ev_stop = nullptr;
+    HIPCHK(ctx, timing_start(ctx, s, &ev_stop));
     HIPCHK(ctx, launch_dds(p, s));
+    if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, s));
     return DPEMU_OK;
 }

@@ -172,6 +172,24 @@ class Emulator:
     def __exit__(self, *a):
         self.close()
 
+    # ---- measurement (dpemu_set_kernel_timing / dpemu_kernel_times) ----
+    def kernel_timing(self, enable: bool = True):
+        """record a HIP event pair around every main-kernel launch (interpreter, DDS)"""
+        check(self._h, self._L.dpemu_set_kernel_timing(self._h, int(bool(enable))), 'dpemu_set_kernel_timing',
+              self._L)
+
+    def kernel_times(self, max_n: int = 4096):
+        """elapsed ms of the launches recorded since the last call (waits for them)"""
+        buf = np.zeros(max_n, np.float32)
+        n = C.c_int(0)
+        check(self._h, self._L.dpemu_kernel_times(self._h, buf.ctypes.data, int(max_n), C.byref(n)),
+              'dpemu_kernel_times', self._L)
+        return [float(x) for x in buf[:n.value]]
+
+    def last_kernel(self) -> str:
+        """the interpreter variant the last run launched"""
+        return self._L.dpemu_last_kernel(self._h).decode()
+
     # -------------------------------------------------------------- programs
     def load(self, programs, cores_per_shot: Optional[int] = None) -> ProgramSet:
         ps = programs if isinstance(programs, ProgramSet) else ProgramSet(programs, cores_per_shot)

@@ -204,6 +204,19 @@ int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uint32_t *summ
 /* The Q15 sine table both the DDS kernel and its CPU restatement use. */
 int dpemu_dds_sin_lut(int16_t *out4096);
 
+/*
+ * Measurement.  While kernel timing is on, dpemu_run and dpemu_dds record a
+ * HIP event pair on the call's stream around their main kernel (the
+ * interpreter / the DDS kernel; not the histogram memset and reduction).
+ * dpemu_kernel_times waits for the recorded pairs, writes up to max_n
+ * elapsed times in ms (oldest first) to ms, *n_out = how many, and clears the
+ * record.  dpemu_last_kernel names the interpreter variant the last dpemu_run
+ * launched (e.g. "straight_kernel<rows,pulse,fb1>", "interp_kernel<feat=0x3>").
+ */
+int         dpemu_set_kernel_timing(dpemu_ctx *ctx, int enable);
+int         dpemu_kernel_times(dpemu_ctx *ctx, float *ms, int max_n, int *n_out);
+const char *dpemu_last_kernel(dpemu_ctx *ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,7 +28,8 @@ prof trace --kernel-trace --stats || exit $?
 find $out/prof_trace -name "*kernel_stats.csv" -exec cat {} \;
 prof fetch --pmc FETCH_SIZE || exit $?
 prof write --pmc WRITE_SIZE || exit $?
-prof sq1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES || exit $?
-prof sq2 --pmc SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE || exit $?
+prof sq1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU || exit $?
+prof sq2 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE || exit $?
 timeout -k 10 60 rocprofv3 -L > $out/counters_avail.txt 2>&1; echo "list rc=$?"
+[ -x scripts/micro/valu_peak ] && { step valu_peak 120 scripts/micro/valu_peak || exit $?; }
 python3 scripts/pmc_summary.py $out r01 || exit $?

@@ -24,7 +24,16 @@ import json
 import os
 import sys
 
-KERNELS = {'interp': 'interp_kernel', 'dds': 'dds_kernel', 'hist_reduce': 'hist_reduce_kernel'}
+# summary key -> kernel-name substrings (the interpreter is interp_kernel or, for
+# branch-free programs, straight_kernel)
+KERNELS = {'interp': ('interp_kernel', 'straight_kernel'), 'dds': ('dds_kernel', 'dds_chunk_kernel'),
+           'hist_reduce': ('hist_reduce_kernel',)}
+
+
+# wave64 integer-VALU instructions per second, whole chip: the best rate of
+# scripts/micro/valu_peak.hip (independent add/shift/xor chains, 2-8 waves per
+# SIMD) measured on MI355X (profiles/r01_valu_peak.jsonl)
+VALU_PEAK_WAVE_INSTS = 7.7e11
 
 
 def rows(pattern):
@@ -36,8 +45,8 @@ def rows(pattern):
 
 
 def which(name):
-    for k, sub in KERNELS.items():
-        if sub in name:
+    for k, subs in KERNELS.items():
+        if any(sub in name for sub in subs):
             return k
     return None
 
@@ -48,6 +57,7 @@ def main():
     os.makedirs(dest, exist_ok=True)
     # kernel trace: per (kernel, grid) durations
     dur = collections.defaultdict(list)
+    names = {}
     tdir = 'prof_trace' if os.path.isdir(os.path.join(root, 'prof_trace')) else 'trace'
     for r in rows(os.path.join(root, tdir, '**', '*kernel_trace.csv')):
         k = which(r['Kernel_Name'])
@@ -55,6 +65,7 @@ def main():
             grid = int(r['Grid_Size']) if r.get('Grid_Size') else \
                 int(r['Grid_Size_X']) * int(r.get('Grid_Size_Y') or 1) * int(r.get('Grid_Size_Z') or 1)
             dur[(k, grid)].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+            names[(k, grid)] = r['Kernel_Name']
     shape = {}
     for (k, grid), v in dur.items():
         if k not in shape or len(v) > len(dur[(k, shape[k])]):
@@ -71,7 +82,7 @@ def main():
             grid = int(r.get('Grid_Size') or 0)
             ctr[(k, grid, r['Counter_Name'])][(d, r['Dispatch_Id'])] += float(r['Counter_Value'])
     for k, grid in shape.items():
-        res = {'kernel': KERNELS[k], 'grid_size': grid, 'dispatches_traced': len(dur[(k, grid)]),
+        res = {'kernel': names[(k, grid)], 'grid_size': grid, 'dispatches_traced': len(dur[(k, grid)]),
                'duration_ns': sum(dur[(k, grid)]) / len(dur[(k, grid)])}
         for (kk, g, name), per in ctr.items():
             if kk == k and g == grid:
@@ -92,6 +103,10 @@ def main():
         if 'SQ_THREAD_CYCLES_VALU' in res and 'SQ_ACTIVE_INST_VALU' in res and res['SQ_ACTIVE_INST_VALU']:
             # active lanes per VALU instruction (divergence): thread-cycles / (quad-cycles * 64)
             res['valu_lane_util_pct'] = 100.0 * res['SQ_THREAD_CYCLES_VALU'] / (res['SQ_ACTIVE_INST_VALU'] * 64)
+        if 'SQ_INSTS_VALU' in res and res.get('duration_ns'):
+            # against the measured integer-VALU issue peak (scripts/micro/valu_peak.hip)
+            res['valu_insts_per_s'] = res['SQ_INSTS_VALU'] / (res['duration_ns'] * 1e-9)
+            res['valu_frac_of_measured_peak'] = res['valu_insts_per_s'] / VALU_PEAK_WAVE_INSTS
         if 'SQ_INSTS_VALU' in res and 'SQ_WAVES' in res and res['SQ_WAVES']:
             res['valu_insts_per_wave'] = res['SQ_INSTS_VALU'] / res['SQ_WAVES']
         path = os.path.join(dest, '{}_{}_pmc.json'.format(tag, k))
