@@ -17,18 +17,17 @@ rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 OUT = ('summary', 'ev_main', 'ev_amp', 'meas', 'hist')
 KNOBS = {'auto': {}, 'fb4': {'DPEMU_FETCH_BATCH': '4'}, 'fb1': {'DPEMU_FETCH_BATCH': '1'},
-         'general': {'DPEMU_LINEAR': '0'}, 'linear': {'DPEMU_LINEAR': '1'}}
+         'general': {'DPEMU_LINEAR': '0'}, 'linear': {'DPEMU_LINEAR': '1'},
+         'sum_lane': {'DPEMU_SUMMARY_WAVE': '0'}, 'general_sum_lane': {'DPEMU_LINEAR': '0', 'DPEMU_SUMMARY_WAVE': '0'}}
 ramsey = ProgramSet(workloads.config2_ramsey(8, 100))
 rb = ProgramSet(workloads.config4_rb(n_seq=1000, depth=200, n_cores=2))
 cases = {
-    'ramsey': (ramsey, 10 ** 6, dict(n_groups=100), OUT, ('auto', 'fb4')),
-    'ramsey_summary_only': (ramsey, 10 ** 6, dict(n_groups=100), ('summary',), ('auto', 'fb4')),
-    'rb_2e5': (rb, 10 ** 5, dict(n_groups=1000, shots_per_group=100, event_cap=512, meas_cap=4), OUT,
-               ('auto', 'fb1', 'general')),
-    'rb_2e5_summary': (rb, 10 ** 5, dict(n_groups=1000, shots_per_group=100, event_cap=512, meas_cap=4),
-                       ('summary',), ('auto', 'general')),
-    'rb_2e6_summary': (rb, 10 ** 6, dict(n_groups=1000, shots_per_group=1000, event_cap=512, meas_cap=4),
-                       ('summary', 'meas', 'hist'), ('auto', 'linear')),
+    'ramsey': (ramsey, 10 ** 6, dict(n_groups=100), OUT, ('auto', 'sum_lane')),
+    'ramsey_summary_only': (ramsey, 10 ** 6, dict(n_groups=100), ('summary',), ('auto', 'sum_lane')),
+    'config3_reset': (ProgramSet(workloads.config3_active_reset(8)), 10 ** 6,
+                      dict(meas_latency=workloads.CONFIG3_MEAS_LATENCY, max_cycles=1 << 16, event_cap=16,
+                           meas_cap=4), OUT, ('auto', 'sum_lane')),
+
 }
 emu = Emulator(0)
 stream = torch.cuda.current_stream()
@@ -43,7 +42,7 @@ for r in range(rounds):
         k.setdefault('meas_cap', 2)
         cfg = _abi.make_config(ps.cores_per_shot, **k)
         for kn in knobs:
-            for var in ('DPEMU_FETCH_BATCH', 'DPEMU_LINEAR'):
+            for var in ('DPEMU_FETCH_BATCH', 'DPEMU_LINEAR', 'DPEMU_SUMMARY_WAVE'):
                 os.environ.pop(var, None)
             os.environ.update(KNOBS[kn])
             out = alloc_device_outputs(cfg, n, want)

@@ -161,6 +161,23 @@ def test_config1_golden_program(emu, golden_dir):
     assert [int(e[1]) for e in ev[1:4]] == [7, 23, 323]       # qclk at cstrobe = cmd_time + 2
 
 
+@pytest.mark.parametrize('name', ['test_fproc_hold', 'test_hw_virtualz_out', 'test_linear_compile_out',
+                                  'test_multirst_cfg', 'test_multirst_fproc_res_cfg', 'test_pulse_compile_out',
+                                  'test_simple_loop'])
+def test_clean_room_assembled_goldens(emu, name):
+    """the reference's compiler golden programs, assembled by this framework's
+    clean-room GlobalAssembler (byte-identical to the reference's, see
+    tests/test_assembler.py), run on the GPU against oracle_fast"""
+    from distributed_processor_amd import hwconfig
+    from tests.test_assembler import assemble
+    ps = ProgramSet([assemble(name, hwconfig.DDSElementConfig)])
+    cfg = _abi.make_config(ps.cores_per_shot, max_cycles=20000, event_cap=32, trace_cap=32, meas_cap=8,
+                           p1=0.5, seed=len(name))
+    g, f = run_pair(emu, ps, cfg, 3000, shot0=11)
+    compare_all(g, f, name)
+    assert (_abi.unpack_summary(g['summary'])['status'] == _abi.ST_DONE).all()
+
+
 def test_config1_dds_element(emu):
     ps = ProgramSet(workloads.config1_linear())
     cfg = _abi.make_config(1, max_cycles=10000, event_cap=8, trace_cap=8, meas_cap=4)
