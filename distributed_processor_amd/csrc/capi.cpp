@@ -46,6 +46,9 @@ struct dpemu_ctx {
     uint32_t dds_chunk = DDS_CHUNK;         // DPEMU_DDS_CHUNK: samples per workgroup
     uint32_t dds_probe = 0;                 // DPEMU_DDS_PROBE: store-pattern probes (A/B only)
     uint32_t dds_lds_pad = 0;               // DPEMU_DDS_LDSPAD: occupancy A/B
+    uint32_t dds_seg = 0;                   // DPEMU_DDS_SEG=1: eligible channels on the segment kernel (A/B)
+    uint32_t dds_seg_chunk = DDS_SEG_CHUNK; // DPEMU_DDS_SEG_CHUNK: samples per segment-kernel sub-chunk
+    uint32_t dds_seg_per_cu = 0;            // DPEMU_DDS_SEG_PER_CU: segment-kernel workgroups per CU (0 = occupancy)
     int last_feat = -1;
     std::string last_kernel;                // variant the last dpemu_run launched (dpemu_last_kernel)
     // kernel timing (dpemu_set_kernel_timing): event pairs recorded around main kernels
@@ -126,6 +129,12 @@ int dpemu_create(int device, dpemu_ctx **out)
     }
     if (const char *e = getenv("DPEMU_DDS_PROBE")) ctx->dds_probe = (uint32_t)atoi(e);
     if (const char *e = getenv("DPEMU_DDS_LDSPAD")) ctx->dds_lds_pad = (uint32_t)atoi(e) & ~15u;
+    if (const char *e = getenv("DPEMU_DDS_SEG")) ctx->dds_seg = (uint32_t)atoi(e) != 0;
+    if (const char *e = getenv("DPEMU_DDS_SEG_PER_CU")) ctx->dds_seg_per_cu = (uint32_t)atoi(e);
+    if (const char *e = getenv("DPEMU_DDS_SEG_CHUNK")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v >= 8 * BLOCK && (v % (8 * BLOCK)) == 0 && v <= (1u << 17)) ctx->dds_seg_chunk = v;
+    }
     if (hipMalloc(&ctx->d_thr, DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&ctx->d_lut, 256 * sizeof(uint64_t)) != hipSuccess) {
         delete ctx;
@@ -558,6 +567,10 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     if (ch->n_channels > 65535) return fail(ctx, DPEMU_E_INVALID, "n_channels > 65535");
     std::vector<uint32_t> desc((size_t)ch->n_channels * DDS_CH_WORDS);
     uint32_t env_max = 0, freq_max = 0;         // LDS staging sizes: largest tables that fit
+    uint32_t seg_env = 0, seg_freq = 0;         // the same for the segment kernel (pairs counted)
+    bool any_seg = false, any_chunk = false;
+    std::vector<uint32_t> seg_list;             // appended to the descriptors on the device
+    const bool seg_ok = ctx->dds_seg && (ctx->dds_probe == 0 || ctx->dds_probe >= 5);
     for (uint32_t i = 0; i < ch->n_channels; i++) {
         uint32_t *d = &desc[(size_t)i * DDS_CH_WORDS];
         d[0] = ch->ch_lane[i]; d[1] = ch->ch_elem[i] & 3u; d[2] = ch->spc[i]; d[3] = ch->interp[i];
@@ -565,17 +578,31 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
         if (d[0] >= ch->n_lanes) return fail(ctx, DPEMU_E_INVALID, "channel %u: lane %u >= n_lanes", i, d[0]);
         if (d[2] < 1 || d[2] > 16) return fail(ctx, DPEMU_E_INVALID, "channel %u: spc %u not in [1, 16]", i, d[2]);
         if (d[3] < 1) return fail(ctx, DPEMU_E_INVALID, "channel %u: interp must be >= 1", i);
-        if (d[5] <= DDS_ENV_LDS_MAX) env_max = std::max(env_max, d[5]);
-        if (d[7] <= DDS_FREQ_LDS_MAX) freq_max = std::max(freq_max, d[7]);
+        const uint32_t interp = d[3], env_w = interp == 1 ? 2 * d[5] : d[5];
+        const bool seg = seg_ok && (d[2] == 8 || d[2] == 16) && (interp & (interp - 1)) == 0 &&
+                         env_w <= DDS_SEG_ENV_MAX && d[7] <= DDS_FREQ_LDS_MAX;
+        if (seg) {
+            d[1] |= DDS_SEG_FLAG;
+            seg_list.push_back(i);
+            any_seg = true;
+            seg_env = std::max(seg_env, env_w);
+            seg_freq = std::max(seg_freq, 2 * d[7]);
+        } else {
+            any_chunk = true;
+            if (d[5] <= DDS_ENV_LDS_MAX) env_max = std::max(env_max, d[5]);
+            if (d[7] <= DDS_FREQ_LDS_MAX) freq_max = std::max(freq_max, d[7]);
+        }
     }
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
+    const size_t n_desc = desc.size();
+    desc.insert(desc.end(), seg_list.begin(), seg_list.end());
     if (desc != ctx->ch_cache) {            // descriptors change rarely: upload only then
-        if (ch->n_channels > ctx->ch_cap) {
+        if (desc.size() > ctx->ch_cap) {
             (void)hipFree(ctx->d_ch);
             ctx->d_ch = nullptr; ctx->ch_cap = 0;
             HIPCHK(ctx, hipMalloc(&ctx->d_ch, desc.size() * 4));
-            ctx->ch_cap = ch->n_channels;
+            ctx->ch_cap = desc.size();
         }
         HIPCHK(ctx, hipStreamSynchronize(s));   // the previous launch may still read d_ch
         HIPCHK(ctx, hipMemcpy(ctx->d_ch, desc.data(), desc.size() * 4, hipMemcpyHostToDevice));
@@ -598,9 +625,16 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.rows = ctx->dds_rows;
     p.probe = ctx->dds_probe;
     p.lds_pad = ctx->dds_lds_pad;
+    DDSParams ps = p;
+    ps.env_lds = (seg_env + 3) & ~3u;
+    ps.freq_lds = (seg_freq + 3) & ~3u;
+    ps.chunk = ctx->dds_seg_chunk;
+    ps.seg_list = ctx->d_ch + n_desc;
+    ps.n_seg = (uint32_t)seg_list.size();
+    ps.grid_per_cu = ctx->dds_seg_per_cu;
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, s, &ev_stop));
-    HIPCHK(ctx, launch_dds(p, s));
+    HIPCHK(ctx, launch_dds(p, ps, any_seg, any_chunk, s));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, s));
     return DPEMU_OK;
 }

@@ -125,13 +125,10 @@ __device__ __forceinline__ void store4(uint32_t *out, uint32_t j0, uint32_t c_en
 // elem) and the lane's pulse_resets, in event (= time) order, into LDS.
 // Every global load of the events is issued before the first barrier.
 // ---------------------------------------------------------------------------
-struct Compacted {
-    uint32_t *st_t, *st_env, *st_pf, *rs_t;
-    uint16_t *st_amp;
-};
-
-__device__ __forceinline__ void compact_events(const DDSParams &p, uint32_t lane, uint32_t elem, const Compacted &c,
-                                               uint32_t *s_tmp, uint32_t *s_cnt, int *n_st, int *n_rs)
+// sink(i, ev, amp) stores strobe i (ev = {t, -, env | cfg | kind, phase | freq index}).
+template <class StrobeSink>
+__device__ __forceinline__ void compact_events(const DDSParams &p, uint32_t lane, uint32_t elem, StrobeSink sink,
+                                               uint32_t *rs_t, uint32_t *s_tmp, uint32_t *s_cnt, int *n_st, int *n_rs)
 {
     const uint32_t tid = threadIdx.x, wl = tid & 63, wv = tid >> 6;
     uint32_t n_ev = min(p.summary[8ull * lane + 2], p.event_cap);
@@ -169,11 +166,8 @@ __device__ __forceinline__ void compact_events(const DDSParams &p, uint32_t lane
             ts += s_tmp[k];
             tr += s_tmp[BLOCK / 64 + k];
         }
-        if (is_st) {
-            const uint32_t i = os + (uint32_t)__popcll(bs & below);
-            c.st_t[i] = ev.x; c.st_env[i] = ev.z & 0xFFFFFFu; c.st_pf[i] = ev.w; c.st_amp[i] = (uint16_t)ampr[ps];
-        }
-        if (is_rs) c.rs_t[orr + (uint32_t)__popcll(br & below)] = ev.x;
+        if (is_st) sink(os + (uint32_t)__popcll(bs & below), ev, ampr[ps]);
+        if (is_rs) rs_t[orr + (uint32_t)__popcll(br & below)] = ev.x;
         __syncthreads();
         if (tid == 0) { s_cnt[0] += ts; s_cnt[1] += tr; }
         __syncthreads();
@@ -416,7 +410,8 @@ __global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
     const uint32_t tid = threadIdx.x;
     const uint32_t ch = blockIdx.y;
     const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
-    const uint32_t lane = d[0], elem = d[1], spc = d[2], interp = d[3] ? d[3] : 1u;
+    if (d[1] & DDS_SEG_FLAG) return;        // synthesised by dds_seg_kernel
+    const uint32_t lane = d[0], elem = d[1] & 3u, spc = d[2], interp = d[3] ? d[3] : 1u;
     const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
     const uint32_t spc_sh = __ffs(spc) - 1, int_sh = __ffs(interp) - 1;
@@ -431,13 +426,17 @@ __global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
         for (uint32_t i = tid; i < freq_len; i += BLOCK) s_freq[i] = p.freq[freq_off + i];
     }
     int n_st, n_rs;
-    compact_events(p, lane, elem, Compacted{s_st_t, s_st_env, s_st_pf, s_rs_t, s_st_amp}, s_tmp, s_cnt,
-                   &n_st, &n_rs);
+    compact_events(
+        p, lane, elem,
+        [&](uint32_t i, const uint4 &ev, uint32_t amp) {
+            s_st_t[i] = ev.x; s_st_env[i] = ev.z & 0xFFFFFFu; s_st_pf[i] = ev.w; s_st_amp[i] = (uint16_t)amp;
+        },
+        s_rs_t, s_tmp, s_cnt, &n_st, &n_rs);
 
     uint32_t *out = p.iq + (uint64_t)ch * p.n_samples;
     const uint32_t c_begin = blockIdx.x * p.chunk;
     const uint32_t c_end = min(c_begin + p.chunk, p.n_samples);
-    if (p.probe >= 3) {          // probes: zero stores of the sweep, 8 samples per thread per tile
+    if (p.probe == 3 || p.probe == 4) {   // probes: zero stores of the sweep, 8 samples per thread per tile
         const uint32_t z[4] = {0, 0, 0, (uint32_t)(n_st + n_rs) & 0u};
         if (p.probe == 3) {      // thread-contiguous 32 B (two half-dense store instructions)
             for (uint32_t j0 = c_begin + 8 * tid; j0 < c_end; j0 += 8 * BLOCK) {
@@ -503,6 +502,306 @@ __global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
     }
 }
 
+// ===========================================================================
+// Segment path: dds_seg_kernel (channels with spc in {8, 16}, power-of-two
+// interp, env / freq tables staged in LDS; DDS_SEG_FLAG in the descriptor).
+//
+// The chunk kernel's sweep re-finds and re-decodes the current pulse on every
+// tile, and on pulse-dense channels (RB qdrv: a 16-cycle X90 every 16 cycles,
+// while a thread's tiles are 128 cycles apart) that is every tile.  Here the
+// prologue does it once per workgroup:
+//   * per strobe, a 32-B record {b, e, env base | cw | amp, phase<<15, F0,
+//     rotation-table base}: b = strobe sample, e = end of the samples it
+//     plays (b + lim; b when its freq entry is invalid);
+//   * per 8-sample group of the chunk, the latest strobe and pulse_reset
+//     (u16 + u16), found by one binary search per thread and a forward walk.
+// Strobes and resets sit on cycle boundaries (8 | spc), so a group never
+// straddles one; it can straddle only a pulse end that is not a multiple of
+// 8 samples, handled by the per-sample path.
+//
+// The sweep then costs per group: the table word, the record, t_ref, one
+// carrier, and per sample 6 VALU for the rotation and 5 for the mix:
+//   with Y = {lo: ai, hi: aq}, R = {lo: rq, hi: ri}, R' = {lo: ri, hi: -rq}:
+//     (a (x) R).re = dot2(R', Y),  .im = dot2(R, Y)
+//   and with E = {lo: eq, hi: ei}, E' = {lo: ei, hi: -eq}:
+//     (E (x) a).re = dot2(E', a),  .im = dot2(E, a)
+// so only Y-form words are ever packed (one v_cvt_pk_i16_i32 + one
+// v_pk_max_i16 for symsat).  R' / E' need rq, eq != -32768; a workgroup whose
+// tables hold one falls back to the per-sample X/Y path for every group.
+// ===========================================================================
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+// {lo: hi, hi: -lo} of an I16|Q16 word
+__device__ __forceinline__ uint32_t neg_swap(uint32_t w) { return (w >> 16) | (((0u - w) & 0xFFFFu) << 16); }
+
+// dot2 results (+2^14) >> 15 of two components -> {lo, hi} saturated to int16
+__device__ __forceinline__ uint32_t pk_sat(int32_t lo, int32_t hi)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(lo >> 15, hi >> 15));
+}
+
+// a0 (x) R_k, symsat, Y form
+__device__ __forceinline__ uint32_t rot_y(uint32_t y0, uint32_t r, uint32_t rp)
+{
+    const short2v v = __builtin_bit_cast(short2v, pk_sat(dot2(rp, y0, 1 << 14), dot2(r, y0, 1 << 14)));
+    const short2v lo = {-32767, -32767};
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, lo));
+}
+
+// sat16(E (x) a), packed {I low, Q high}
+__device__ __forceinline__ uint32_t mix_y(uint32_t e, uint32_t ep, uint32_t y)
+{
+    return pk_sat(dot2(ep, y, 1 << 14), dot2(e, y, 1 << 14));
+}
+
+struct SegArgs {
+    const int16_t *lut;
+    const uint4 *rec;               // 2 x uint4 per strobe
+    const uint32_t *rs_t;
+    const uint32_t *gseg;           // per group: (strobe + 1) | (reset + 1) << 16
+    const uint32_t *env;            // ISH == 0: (E, E') pairs; else E
+    const uint32_t *fr2;            // per freq entry 16 (R, R') pairs; pair 0 = (F0, 0)
+    uint32_t spc_sh, int_sh, c_begin, c_end, ng;
+    uint32_t *out;
+    bool bad;                       // some eq or rq == -32768: per-sample X/Y path
+};
+
+// the definition, sample by sample (X/Y form): straddling groups and bad tables
+template <int ISH>
+__device__ __forceinline__ void seg_group_slow(const SegArgs &q, uint32_t j0, const uint4 ra, const uint4 rb,
+                                            uint32_t t_ref, uint32_t v[8])
+{
+    const uint32_t n = j0 >> q.spc_sh, k0 = j0 & ((1u << q.spc_sh) - 1u);
+    const Carrier a0 = carrier(q.lut, rb.x * (n - t_ref) + ra.w, (int32_t)(ra.z >> 16));
+    const uint32_t eb = ra.z & 0x3FFFu;
+    const bool cw = (ra.z >> 15) & 1u;
+    for (int s = 0; s < 8; s++) {
+        const uint32_t j = j0 + s;
+        v[s] = 0;
+        if (j < ra.y) {
+            const uint32_t widx = eb + (cw ? 0u : ((j - ra.x) >> q.int_sh));
+            const uint32_t e = ISH == 0 ? q.env[2 * widx] : q.env[widx];
+            const uint32_t k = k0 + s;
+            v[s] = mix(e, k ? rotate(a0, q.fr2[rb.y + 2 * k]) : a0);
+        }
+    }
+}
+
+template <int ISH>
+__device__ __forceinline__ void sweep_seg(const SegArgs &q)
+{
+    const uint32_t spc_m = (1u << q.spc_sh) - 1u;
+    for (uint32_t g = threadIdx.x; g < q.ng; g += BLOCK) {
+        const uint32_t j0 = q.c_begin + 8 * g;
+        const uint32_t gs = q.gseg[g];
+        const int si = (int)(gs & 0xFFFFu) - 1, ri = (int)(gs >> 16) - 1;
+        uint32_t v[8];
+#pragma unroll
+        for (int s = 0; s < 8; s++) v[s] = 0;
+        if (si >= 0) {
+            const uint4 ra = q.rec[2 * si];
+            if (j0 < ra.y) {
+                const uint4 rb = q.rec[2 * si + 1];
+                const uint32_t t_ref = ri >= 0 ? q.rs_t[ri] : 0u;
+                if (j0 + 8 <= ra.y && !q.bad) {
+                    const uint32_t n = j0 >> q.spc_sh, k0 = j0 & spc_m;
+                    const uint32_t idx = (rb.x * (n - t_ref) + ra.w) >> 20;
+                    const int32_t c = q.lut[(idx + 1024) & 4095], sn = q.lut[idx];
+                    const int32_t a16 = (int32_t)(ra.z >> 16);
+                    const uint32_t y0 = pack16((c * a16 + (1 << 15)) >> 16, (sn * a16 + (1 << 15)) >> 16);
+                    // rotation pairs (R_k, R'_k), k = k0 .. k0 + 7
+                    const uint4 *rp = reinterpret_cast<const uint4 *>(q.fr2 + rb.y + 2 * k0);
+                    uint32_t R[8], Rp[8], E[8], Ep[8];
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {
+                        const uint4 w = rp[h];
+                        R[2 * h] = w.x; Rp[2 * h] = w.y; R[2 * h + 1] = w.z; Rp[2 * h + 1] = w.w;
+                    }
+                    const uint32_t eb = ra.z & 0x3FFFu, d0 = j0 - ra.x;
+                    if ((ra.z >> 15) & 1u) {                       // CW: env word 4A throughout
+                        const uint32_t e = ISH == 0 ? q.env[2 * eb] : q.env[eb];
+                        const uint32_t ep = ISH == 0 ? q.env[2 * eb + 1] : neg_swap(e);
+#pragma unroll
+                        for (int s = 0; s < 8; s++) { E[s] = e; Ep[s] = ep; }
+                    } else if (ISH == 0) {                         // 8 (E, E') pairs
+                        const uint4 *ep4 = reinterpret_cast<const uint4 *>(q.env + 2 * (eb + d0));
+#pragma unroll
+                        for (int h = 0; h < 4; h++) {
+                            const uint4 w = ep4[h];
+                            E[2 * h] = w.x; Ep[2 * h] = w.y; E[2 * h + 1] = w.z; Ep[2 * h + 1] = w.w;
+                        }
+                    } else if (ISH == 1) {                         // 4 words, 2 samples each
+                        const uint4 w = *reinterpret_cast<const uint4 *>(q.env + eb + (d0 >> 1));
+                        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                        for (int s = 0; s < 8; s++) { E[s] = ww[s >> 1]; Ep[s] = neg_swap(ww[s >> 1]); }
+                    } else if (ISH == 2) {                         // 2 words, 4 samples each
+                        const uint2 w = *reinterpret_cast<const uint2 *>(q.env + eb + (d0 >> 2));
+                        const uint32_t e0 = w.x, e1 = w.y, p0 = neg_swap(e0), p1 = neg_swap(e1);
+#pragma unroll
+                        for (int s = 0; s < 8; s++) { E[s] = s < 4 ? e0 : e1; Ep[s] = s < 4 ? p0 : p1; }
+                    } else {                                       // one word for all 8
+                        const uint32_t e = q.env[eb + (d0 >> q.int_sh)], ep = neg_swap(e);
+#pragma unroll
+                        for (int s = 0; s < 8; s++) { E[s] = e; Ep[s] = ep; }
+                    }
+#pragma unroll
+                    for (int s = 0; s < 8; s++) {
+                        uint32_t y = rot_y(y0, R[s], Rp[s]);
+                        if (s == 0) y = k0 == 0 ? y0 : y;         // sub-sample 0 is the unrotated carrier
+                        v[s] = mix_y(E[s], Ep[s], y);
+                    }
+                } else {
+                    seg_group_slow<ISH>(q, j0, ra, rb, t_ref, v);
+                }
+            }
+        }
+        store4(q.out, j0, q.c_end, v);
+        store4(q.out, j0 + 4, q.c_end, v + 4);
+    }
+}
+
+// Persistent: gridDim.x workgroups (all resident) each take a contiguous
+// range of the (segment channel, sub-chunk) items, channel-major, so a
+// workgroup stages the sine table once and compacts a channel's events once
+// per channel it visits (2-3 per workgroup at config 5) instead of once per
+// chunk; per sub-chunk it only rebuilds the group table.
+__global__ void __launch_bounds__(BLOCK) dds_seg_kernel(const DDSParams p)
+{
+    // dynamic LDS (dds_seg_lds_bytes): sine table | strobe records | strobe
+    // times | reset times | group table | env | (R, R') freq pairs
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    int16_t *s_lut = reinterpret_cast<int16_t *>(s_dyn);
+    uint4 *s_rec = reinterpret_cast<uint4 *>(s_dyn + 8192);
+    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_rec + 2 * p.ev_lds);
+    uint32_t *s_rs_t = s_st_t + p.ev_lds;
+    uint32_t *s_gseg = s_rs_t + p.ev_lds;
+    uint32_t *s_env = s_gseg + p.chunk / 8;
+    uint32_t *s_fr2 = s_env + p.env_lds;
+    __shared__ uint32_t s_tmp[2 * (BLOCK / 64)];
+    __shared__ uint32_t s_cnt[2];
+
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < 4096 / 8; i += BLOCK)
+        reinterpret_cast<uint4 *>(s_lut)[i] = reinterpret_cast<const uint4 *>(p.sin_lut)[i];
+
+    const uint32_t n_sub = (p.n_samples + p.chunk - 1) / p.chunk;
+    const uint64_t total = (uint64_t)p.n_seg * n_sub;
+    const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
+    const uint64_t it_end = min((uint64_t)(blockIdx.x + 1) * per, total);
+    uint32_t cur = 0xFFFFFFFFu, ch = 0, spc_sh = 0, int_sh = 0;
+    int n_st = 0, n_rs = 0;
+    bool bad = false;
+    if (p.probe == 5) {                     // probe: the sweep's stores alone (zeros)
+        for (uint64_t it = (uint64_t)blockIdx.x * per; it < it_end; it++) {
+            const uint32_t ci = (uint32_t)(it / n_sub), sub = (uint32_t)(it - (uint64_t)ci * n_sub);
+            const uint32_t c_begin = sub * p.chunk, c_end = min(c_begin + p.chunk, p.n_samples);
+            uint32_t *out = p.iq + (uint64_t)p.seg_list[ci] * p.n_samples;
+            const uint32_t z[4] = {0, 0, 0, 0};
+            for (uint32_t j0 = c_begin + 8 * tid; j0 < c_end; j0 += 8 * BLOCK) {
+                store4(out, j0, c_end, z);
+                store4(out, j0 + 4, c_end, z);
+            }
+        }
+        return;
+    }
+    for (uint64_t it = (uint64_t)blockIdx.x * per; it < it_end; it++) {
+        const uint32_t ci = (uint32_t)(it / n_sub), sub = (uint32_t)(it - (uint64_t)ci * n_sub);
+        __syncthreads();                    // the previous sweep is done with the tables
+        if (ci != cur) {                    // new channel: stage its tables, compact its events
+            cur = ci;
+            ch = p.seg_list[ci];
+            const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
+            const uint32_t lane = d[0], elem = d[1] & 3u, spc = d[2], interp = d[3] ? d[3] : 1u;
+            const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
+            spc_sh = __ffs(spc) - 1;
+            int_sh = __ffs(interp) - 1;
+            bad = false;
+            if (int_sh == 0) {              // E' beside E
+                for (uint32_t i = tid; i < env_len; i += BLOCK) {
+                    const uint32_t e = p.env[env_off + i];
+                    bad |= (e & 0xFFFFu) == 0x8000u;
+                    reinterpret_cast<uint2 *>(s_env)[i] = make_uint2(e, neg_swap(e));
+                }
+            } else {
+                for (uint32_t i = tid; i < env_len; i += BLOCK) {
+                    const uint32_t e = p.env[env_off + i];
+                    bad |= (e & 0xFFFFu) == 0x8000u;
+                    s_env[i] = e;
+                }
+            }
+            for (uint32_t i = tid; i < freq_len; i += BLOCK) {   // R' beside R
+                const uint32_t w = p.freq[freq_off + i];
+                const bool rot = (i & 15u) != 0;
+                bad |= rot && (w & 0xFFFFu) == 0x8000u;
+                reinterpret_cast<uint2 *>(s_fr2)[i] = make_uint2(w, rot ? neg_swap(w) : 0u);
+            }
+            const uint32_t ish = int_sh;
+            compact_events(
+                p, lane, elem,
+                [&](uint32_t i, const uint4 &ev, uint32_t amp) {
+                    const uint32_t env_w = ev.z & 0xFFFFFFu, pf = ev.w;
+                    const uint32_t A = env_w & 0xFFFu, L = (env_w >> 12) & 0xFFFu, fi = pf >> 17;
+                    const uint32_t b = ev.x * spc;
+                    const uint32_t room = env_len > 4 * A ? env_len - 4 * A : 0u;
+                    uint32_t lim;
+                    if (L) {
+                        const uint32_t n_env = min(4 * L, room);
+                        lim = n_env << ish;
+                        if ((lim >> ish) != n_env) lim = 0xFFFFFFFFu;
+                    } else {
+                        lim = room ? 0xFFFFFFFFu : 0u;
+                    }
+                    const bool act = 16 * fi + 15 < freq_len;
+                    const uint32_t e = !act ? b : (lim > 0xFFFFFFFFu - b ? 0xFFFFFFFFu : b + lim);
+                    s_st_t[i] = ev.x;
+                    s_rec[2 * i] = make_uint4(b, e, (4 * A) | ((L ? 0u : 1u) << 15) | ((amp & 0xFFFFu) << 16),
+                                              (pf & 0x1FFFFu) << 15);
+                    s_rec[2 * i + 1] = make_uint4(act ? s_fr2[32 * fi] : 0u, 32 * fi, 0u, 0u);
+                },
+                s_rs_t, s_tmp, s_cnt, &n_st, &n_rs);
+            bad = __syncthreads_or(bad);
+        }
+
+        // group table of the sub-chunk: thread tid owns groups [g0, g1)
+        const uint32_t c_begin = sub * p.chunk;
+        const uint32_t c_end = min(c_begin + p.chunk, p.n_samples);
+        const uint32_t ng = (c_end - c_begin + 7) / 8;
+        const uint32_t gper = (ng + BLOCK - 1) / BLOCK;
+        const uint32_t g0 = min(tid * gper, ng), g1 = min(g0 + gper, ng);
+        if (g0 < g1) {
+            uint32_t n = (c_begin + 8 * g0) >> spc_sh;
+            int si = last_le(s_st_t, n_st, n), ri = last_le(s_rs_t, n_rs, n);
+            for (uint32_t g = g0; g < g1; g++) {
+                n = (c_begin + 8 * g) >> spc_sh;
+                while (si + 1 < n_st && s_st_t[si + 1] <= n) si++;
+                while (ri + 1 < n_rs && s_rs_t[ri + 1] <= n) ri++;
+                s_gseg[g] = (uint32_t)(si + 1) | ((uint32_t)(ri + 1) << 16);
+            }
+        }
+        __syncthreads();
+
+        const SegArgs q{s_lut, s_rec, s_rs_t, s_gseg, s_env, s_fr2, spc_sh, int_sh, c_begin, c_end, ng,
+                        p.iq + (uint64_t)ch * p.n_samples, bad};
+        if (p.probe == 6 || p.probe == 7) {  // probes: tables built; stores of zeros / of the group words
+            for (uint32_t g = tid; g < ng; g += BLOCK) {
+                const uint32_t j0 = c_begin + 8 * g;
+                const uint32_t w = p.probe == 7 ? s_gseg[g] : 0u;
+                const uint32_t z[4] = {w, w, w, w};
+                store4(q.out, j0, c_end, z);
+                store4(q.out, j0 + 4, c_end, z);
+            }
+            continue;
+        }
+        switch (int_sh) {
+        case 0: sweep_seg<0>(q); break;
+        case 1: sweep_seg<1>(q); break;
+        case 2: sweep_seg<2>(q); break;
+        default: sweep_seg<3>(q); break;
+        }
+    }
+}
+
 // dynamic LDS above 64 KiB needs an opt-in per kernel, raised as requests grow
 static hipError_t opt_in_lds(const void *fn, uint32_t bytes, uint32_t *granted)
 {
@@ -512,15 +811,34 @@ static hipError_t opt_in_lds(const void *fn, uint32_t bytes, uint32_t *granted)
     return e;
 }
 
-hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
+hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, bool any_chunk, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
-    const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) + p.lds_pad;
-    static uint32_t granted = 0;
-    const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_chunk_kernel), lds, &granted);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(dds_chunk_kernel, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
+    if (any_seg && ps.n_seg) {
+        const uint32_t lds = dds_seg_lds_bytes(ps.ev_lds, ps.env_lds, ps.freq_lds, ps.chunk) + ps.lds_pad;
+        static uint32_t granted = 0;
+        hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_seg_kernel), lds, &granted);
+        if (e != hipSuccess) return e;
+        // one resident wave of workgroups: CUs x workgroups per CU (occupancy,
+        // or ps.grid_per_cu when set), never more than there are items
+        int dev = 0, cus = 0, per_cu = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dds_seg_kernel, BLOCK, lds)) != hipSuccess)
+            return e;
+        if (ps.grid_per_cu) per_cu = std::min<int>(per_cu, (int)ps.grid_per_cu);
+        const uint64_t items = (uint64_t)ps.n_seg * ((ps.n_samples + ps.chunk - 1) / ps.chunk);
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(items, (uint64_t)std::max(1, cus * std::max(1, per_cu)));
+        hipLaunchKernelGGL(dds_seg_kernel, dim3(grid), dim3(BLOCK), lds, stream, ps);
+    }
+    if (any_chunk) {
+        const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
+        const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) + p.lds_pad;
+        static uint32_t granted = 0;
+        const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_chunk_kernel), lds, &granted);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(dds_chunk_kernel, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
+    }
     return hipGetLastError();
 }
 

@@ -160,6 +160,9 @@ struct DDSParams {
     uint32_t probe;                // measurement probes (DPEMU_DDS_PROBE): 3 / 4 = bare stores,
                                    // thread-contiguous / rows layout; 0 = normal
     uint32_t lds_pad;              // extra dynamic LDS per workgroup (DPEMU_DDS_LDSPAD, occupancy A/B)
+    const uint32_t *seg_list;      // segment kernel: its channels (indices into ch)
+    uint32_t n_seg;
+    uint32_t grid_per_cu;          // segment kernel: workgroups per CU (0 = occupancy)
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
 constexpr uint32_t DDS_MAX_EVENTS = 1024;
@@ -173,6 +176,17 @@ inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_l
     return 4096 * 2 + ev_lds * 18 + (env_lds + freq_lds) * 4;
 }
 
-hipError_t launch_dds(const DDSParams &p, hipStream_t stream);
+// dynamic LDS bytes of dds_seg_kernel; env_lds counts words as staged
+// (pairs for interp 1), freq_lds the (R, R') pair words
+inline uint32_t dds_seg_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_lds, uint32_t chunk)
+{
+    return 4096 * 2 + ev_lds * 40 + chunk / 2 + (env_lds + freq_lds) * 4;
+}
+constexpr uint32_t DDS_SEG_FLAG = 0x100;        // descriptor word 1: channel runs on dds_seg_kernel
+constexpr uint32_t DDS_SEG_CHUNK = 1u << 15;    // samples per sub-chunk (group table) on the segment path
+constexpr uint32_t DDS_SEG_ENV_MAX = 4096;      // staged env words (pairs counted) on the segment path
+
+// p: chunk-kernel parameters; ps: segment-kernel parameters (same buffers)
+hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, bool any_chunk, hipStream_t stream);
 
 }  // namespace dpemu

@@ -1,7 +1,7 @@
 """Interleaved A/B of the DDS paths on the config-5 workload, in ONE process,
 next to a pure streaming-store reference (torch fill of the same output
 buffer) that measures the achievable HBM write bandwidth.
-usage: python scripts/ab_dds.py [rounds] [steps] [n_seq]"""
+usage: python scripts/ab_dds.py [rounds] [steps] [n_seq] [elements: 01 = qdrv + rdrv, 0, 1]"""
 import json
 import os
 import sys
@@ -17,20 +17,31 @@ from distributed_processor_amd.emulator import Emulator, ProgramSet, alloc_devic
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 n_seq = int(sys.argv[3]) if len(sys.argv) > 3 else 128
+elems = tuple(int(c) for c in (sys.argv[4] if len(sys.argv) > 4 else '01'))
 
 ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
 ctx = {}
-VARIANTS = [  # name, rows, chunk, probe, lds pad
-    ('contig8_c32k_default', 0, 32768, 0, 0), ('rows1_c32k', 1, 32768, 0, 0),
-    ('contig8_c16k', 0, 16384, 0, 0), ('contig8_c64k', 0, 65536, 0, 0),
-    ('probe_rows_stores', 2, 32768, 4, 0), ('probe_contig_stores', 2, 32768, 3, 0)]
-for name, rows, chunk, probe, pad in VARIANTS:
-    os.environ['DPEMU_DDS_LDSPAD'] = str(pad)
-    os.environ['DPEMU_DDS_PROBE'] = str(probe)
-    os.environ['DPEMU_DDS_ROWS'] = str(rows)
-    os.environ['DPEMU_DDS_CHUNK'] = str(chunk)
+VARIANTS = [  # name, env knobs (read once, at dpemu_create)
+    ('seg_c32k', {}),
+    ('seg_c16k', {'DPEMU_DDS_SEG_CHUNK': '16384'}),
+    ('seg_c32k_2cu', {'DPEMU_DDS_SEG_PER_CU': '2'}),
+    ('chunk_contig8_c32k', {'DPEMU_DDS_SEG': '0'}),
+    ('probe_contig_stores', {'DPEMU_DDS_PROBE': '3'}),
+    ('probe_seg_stores', {'DPEMU_DDS_PROBE': '5'}),
+    ('probe_seg_tables_zero', {'DPEMU_DDS_PROBE': '6'}),
+    ('probe_seg_tables_gword', {'DPEMU_DDS_PROBE': '7'}),
+    ('probe_seg_stores_c16k', {'DPEMU_DDS_PROBE': '5', 'DPEMU_DDS_SEG_CHUNK': '16384'}),
+    ('probe_seg_stores_2cu', {'DPEMU_DDS_PROBE': '5', 'DPEMU_DDS_SEG_PER_CU': '2'}),
+]
+KNOBS = ('DPEMU_DDS_SEG', 'DPEMU_DDS_SEG_CHUNK', 'DPEMU_DDS_SEG_PER_CU', 'DPEMU_DDS_PROBE', 'DPEMU_DDS_ROWS', 'DPEMU_DDS_CHUNK')
+for name, knobs in VARIANTS:
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    os.environ.update(knobs)
     ctx[name] = Emulator(0)
-emu = ctx['contig8_c32k_default']
+for k in KNOBS:
+    os.environ.pop(k, None)
+emu = ctx['seg_c32k']
 emu.load(ps)
 cfg = _abi.make_config(8, n_groups=ps.n_groups, event_cap=512, meas_cap=4)
 ev = alloc_device_outputs(cfg, n_seq, want=('summary', 'ev_main', 'ev_amp'))
@@ -39,7 +50,7 @@ torch.cuda.synchronize()
 t_end = int(ev['summary'][:, 0].max().item())
 n_samples = ((t_end + 8) * 16 + 3) // 4 * 4
 params = {i: (e['samples_per_clk'], e['interp_ratio']) for i, e in enumerate(workloads.ELEMS)}
-plan = ChannelPlan(ps, cfg, 0, n_seq, [(q, c, e) for q in range(n_seq) for c in range(8) for e in (0, 1)], params)
+plan = ChannelPlan(ps, cfg, 0, n_seq, [(q, c, e) for q in range(n_seq) for c in range(8) for e in elems], params)
 iq = torch.empty((plan.n_channels, n_samples), dtype=torch.int32, device='cuda')
 ref = None
 stream = torch.cuda.current_stream()

@@ -27,24 +27,29 @@ def emu():
     e.close()
 
 
-def make_emu(rows):
-    """an Emulator whose DDS sweep uses `rows` quad rows per thread (0 = eight
-    contiguous samples); DPEMU_DDS_ROWS is read once, at dpemu_create"""
+def make_emu(rows, seg=1):
+    """an Emulator whose DDS uses the segment kernel for eligible channels
+    (seg=1, the default) or the chunk kernel for all (seg=0), with `rows`
+    quad rows per thread in the chunk kernel (0 = eight contiguous samples);
+    DPEMU_DDS_SEG / DPEMU_DDS_ROWS are read once, at dpemu_create"""
     import os
-    old = os.environ.get('DPEMU_DDS_ROWS')
-    os.environ['DPEMU_DDS_ROWS'] = str(rows)
+    knobs = {'DPEMU_DDS_ROWS': str(rows), 'DPEMU_DDS_SEG': str(seg)}
+    old = {k: os.environ.get(k) for k in knobs}
+    os.environ.update(knobs)
     try:
         return Emulator(0)
     finally:
-        if old is None:
-            os.environ.pop('DPEMU_DDS_ROWS', None)
-        else:
-            os.environ['DPEMU_DDS_ROWS'] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
-@pytest.fixture(scope='module', params=[0, 1, 2, 4], ids=lambda r: 'rows{}'.format(r))
+@pytest.fixture(scope='module', params=[(0, 1), (0, 0), (1, 0), (2, 0), (4, 0)],
+                ids=lambda r: 'seg' if r[1] else 'chunk_rows{}'.format(r[0]))
 def emu_path(request):
-    e = make_emu(request.param)
+    e = make_emu(*request.param)
     yield e
     e.close()
 
@@ -207,24 +212,36 @@ def plan_from(desc, env_tab, freq_tab, n_lanes, cap):
     return plan
 
 
-@pytest.mark.parametrize('spcs', [(16, 16, 16, 16), (16, 8, 4, 16)], ids=['spc16', 'spc_mixed'])
-def test_sweep_edges(emu_path, spcs):
+SWEEP_CASES = {   # (samples per clock, interp) of the four elements
+    'spc16': ((16, 1), (16, 3), (16, 16), (16, 2)),
+    'spc_mixed': ((16, 1), (8, 3), (4, 16), (16, 2)),
+    'spc8': ((8, 1), (16, 3), (8, 16), (8, 2)),
+    'interp_4_8_32': ((16, 4), (8, 8), (16, 32), (8, 1)),
+    'bad_words': ((16, 1), (16, 4), (8, 16), (16, 2)),
+}
+
+
+@pytest.mark.parametrize('case', list(SWEEP_CASES))
+def test_sweep_edges(emu_path, case):
     """every pulse rule against oracle_dds on every sweep variant: CW, pulse
     end inside a thread's samples (odd env lengths), non-power-of-two interp
     (generic sweep), resets inside pulses, odd env / freq offsets, missing
     freq entries, env words past the table, ragged tail, overflowed and empty
-    lanes"""
+    lanes; 'bad_words' puts Q = -32768 into env and rotation words (the
+    segment kernel's per-sample fallback)"""
     import torch
     rng = np.random.default_rng(11)
     cap, n_lanes, n_cycles = 48, 6, 9000
     env_tab = pack_iq16(np.exp(1j * rng.uniform(0, 2 * np.pi, 301)) * rng.uniform(0, 1, 301))
     freq_tab = np.concatenate([np.zeros(3, np.uint32)] + [DDSElementConfig(samples_per_clk=16).get_freq_buffer([f])
                               for f in (91.7e6, -13.1e6, 250e6)])
+    if case == 'bad_words':
+        env_tab[::37] = (env_tab[::37] & 0xFFFF0000) | 0x8000
+        freq_tab[3 + 16 + 5] = (freq_tab[3 + 16 + 5] & 0xFFFF0000) | 0x8000
     summary, ev, amp = synthetic_timelines(rng, n_lanes, cap, n_cycles, 280, 3)
     desc = []
     for L in range(n_lanes):
-        for e, spc in enumerate(spcs):
-            interp = (1, 3, 16, 2)[e]
+        for e, (spc, interp) in enumerate(SWEEP_CASES[case]):
             env_off = (0, 1, 5, 2)[e]                       # odd offsets: unaligned env reads
             env_len = (280, 279, 290, 301 - 2)[e]           # not multiples of 4
             desc.append((L, e, spc, interp, env_off, env_len, 3 if e % 2 else 1, len(freq_tab) - 3))
@@ -236,7 +253,7 @@ def test_sweep_edges(emu_path, spcs):
            'ev_amp': torch.from_numpy(amp.view(np.int16)).cuda()}
     iq = emu_path.synthesize(plan_from(desc, env_tab, freq_tab, n_lanes, cap), dev, n_samples)
     torch.cuda.synchronize()
-    check_equal(host(iq), ref, 'sweep edges')
+    check_equal(host(iq), ref, 'sweep edges ' + case)
     assert (ref != 0).sum() > 10000
 
 
