@@ -161,7 +161,7 @@ def dds_leg(emu, args, world, rank, stream):
                       'samples_per_channel': n_samples, 'rb_depth': 200},
            'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                         'frac': gbs / HBM_PEAK_GBS, 'traffic': traffic, 'bytes_per_launch': samples * 4,
-                        'kernel': 'dpemu::dds_chunk_kernel'}}
+                        'kernel': 'dpemu::dds_index_kernel + dpemu::dds_chunk_kernel<8> (one HIP-event bracket)'}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host_ev = {k: v.cpu().numpy() for k, v in ev.items()}
         res['cpu_baseline'] = dds_cpu_baseline(plan, host_ev, n_samples, args.cpu_seconds * 2 / 3)

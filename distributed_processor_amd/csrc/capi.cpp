@@ -46,6 +46,11 @@ struct dpemu_ctx {
     uint32_t dds_chunk = DDS_CHUNK;         // DPEMU_DDS_CHUNK: samples per workgroup
     uint32_t dds_probe = 0;                 // DPEMU_DDS_PROBE: store-pattern probes (A/B only)
     uint32_t dds_lds_pad = 0;               // DPEMU_DDS_LDSPAD: occupancy A/B
+    uint32_t dds_spt = 8;                   // DPEMU_DDS_SPT=4: lean chunk kernel with 4 samples per thread per tile
+    uint32_t dds_yform = 1;                 // DPEMU_DDS_YFORM=0: chunk kernel's X/Y-form quad sweep (A/B)
+    uint32_t dds_index = 1;                 // DPEMU_DDS_INDEX=0: chunk workgroups compact events themselves (A/B)
+    void *d_dds_index = nullptr;            // chunk-path event index (dds_index_kernel)
+    uint64_t dds_index_cap = 0;
     uint32_t dds_seg = 0;                   // DPEMU_DDS_SEG=1: eligible channels on the segment kernel (A/B)
     uint32_t dds_seg_chunk = DDS_SEG_CHUNK; // DPEMU_DDS_SEG_CHUNK: samples per segment-kernel sub-chunk
     uint32_t dds_seg_per_cu = 0;            // DPEMU_DDS_SEG_PER_CU: segment-kernel workgroups per CU (0 = occupancy)
@@ -129,6 +134,9 @@ int dpemu_create(int device, dpemu_ctx **out)
     }
     if (const char *e = getenv("DPEMU_DDS_PROBE")) ctx->dds_probe = (uint32_t)atoi(e);
     if (const char *e = getenv("DPEMU_DDS_LDSPAD")) ctx->dds_lds_pad = (uint32_t)atoi(e) & ~15u;
+    if (const char *e = getenv("DPEMU_DDS_SPT")) ctx->dds_spt = atoi(e) == 4 ? 4u : 8u;
+    if (const char *e = getenv("DPEMU_DDS_YFORM")) ctx->dds_yform = (uint32_t)atoi(e) != 0;
+    if (const char *e = getenv("DPEMU_DDS_INDEX")) ctx->dds_index = (uint32_t)atoi(e) != 0;
     if (const char *e = getenv("DPEMU_DDS_SEG")) ctx->dds_seg = (uint32_t)atoi(e) != 0;
     if (const char *e = getenv("DPEMU_DDS_SEG_PER_CU")) ctx->dds_seg_per_cu = (uint32_t)atoi(e);
     if (const char *e = getenv("DPEMU_DDS_SEG_CHUNK")) {
@@ -157,6 +165,7 @@ int dpemu_destroy(dpemu_ctx *ctx)
     (void)hipSetDevice(ctx->device);
     free_programs(ctx);
     (void)hipFree(ctx->d_thr); (void)hipFree(ctx->d_lut); (void)hipFree(ctx->d_sin); (void)hipFree(ctx->d_ch);
+    (void)hipFree(ctx->d_dds_index);
     (void)hipFree(ctx->d_hist_rep);
     for (auto *v : {&ctx->ev_used, &ctx->ev_free})
         for (auto &e : *v) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -589,8 +598,10 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
             seg_freq = std::max(seg_freq, 2 * d[7]);
         } else {
             any_chunk = true;
-            if (d[5] <= DDS_ENV_LDS_MAX) env_max = std::max(env_max, d[5]);
-            if (d[7] <= DDS_FREQ_LDS_MAX) freq_max = std::max(freq_max, d[7]);
+            // staged words: (E, E') pairs for interp 1 and (R, R') pairs in Y form
+            const uint32_t ew = ctx->dds_yform ? env_w : d[5], fw = ctx->dds_yform ? 2 * d[7] : d[7];
+            if (ew <= DDS_ENV_LDS_MAX) env_max = std::max(env_max, ew);
+            if (fw <= DDS_FREQ_LDS_MAX) freq_max = std::max(freq_max, fw);
         }
     }
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -625,10 +636,27 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.rows = ctx->dds_rows;
     p.probe = ctx->dds_probe;
     p.lds_pad = ctx->dds_lds_pad;
+    p.yform = ctx->dds_yform;
+    p.spt = ctx->dds_spt;
+    if (ctx->dds_index && (any_chunk || any_seg) && ctx->dds_probe != 5 && ctx->dds_probe != 12) {      // event index of the chunk path (grown, never shrunk)
+        const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
+        const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds, chunks);
+        if (need > ctx->dds_index_cap) {
+            HIPCHK(ctx, hipStreamSynchronize(s));   // the previous launch may still use it
+            (void)hipFree(ctx->d_dds_index);
+            ctx->d_dds_index = nullptr; ctx->dds_index_cap = 0;
+            HIPCHK(ctx, hipMalloc(&ctx->d_dds_index, need));
+            ctx->dds_index_cap = need;
+        }
+        uint8_t *b = static_cast<uint8_t *>(ctx->d_dds_index);
+        p.xs = reinterpret_cast<uint4 *>(b);
+        p.win = reinterpret_cast<uint4 *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
+        p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16 + (uint64_t)p.n_channels * chunks * 16);
+    }
     DDSParams ps = p;
     ps.env_lds = (seg_env + 3) & ~3u;
     ps.freq_lds = (seg_freq + 3) & ~3u;
-    ps.chunk = ctx->dds_seg_chunk;
+    ps.chunk = p.xs ? p.chunk : ctx->dds_seg_chunk;   // one window per chunk of the index
     ps.seg_list = ctx->d_ch + n_desc;
     ps.n_seg = (uint32_t)seg_list.size();
     ps.grid_per_cu = ctx->dds_seg_per_cu;

@@ -5,28 +5,38 @@
 // event records) and the assembler's env / freq buffers (asmparse.py:46-86
 // formats).  HBM-write-bound by design: 4 B per output sample.
 //
-// Grid: (sample chunks, channels).  A workgroup compacts its channel's
-// events into LDS -- strobes of the channel's element and pulse_resets, both
-// time-sorted because a core emits them in time order -- stages the sine
-// table and the channel's env / freq tables there, then sweeps its chunk
-// with no global loads in the loop: on gfx950 stores count in vmcnt, and a
-// load in the loop would make every tile wait for the previous tile's
-// stores.  Everything a pulse needs (env pointer, phase, amp, rotation words)
-// is decoded once per pulse; the carrier once per quad of samples.
+// Two launches per synthesis:
+//   * dds_index_kernel (one workgroup per channel) compacts the lane's strobes
+//     of the channel's element and its pulse_resets (time-sorted: a core emits
+//     them in time order) once, channel-contiguous, plus each chunk's window;
+//   * dds_chunk_kernel, grid (sample chunks, channels).  A workgroup loads its
+//     window of records, stages the sine table and the channel's env / freq
+//     tables in LDS -- as (E, E') / (R, R') pairs for the Y-form products --
+//     and sweeps its chunk with no global loads in the loop: on gfx950 stores
+//     count in vmcnt, and a load in the loop would make every tile wait for
+//     the previous tile's stores.  A pulse's fields are decoded once per
+//     thread, the carrier once per 8 samples.  The production instance
+//     (LSPT = 8, the "lean" kernel) holds only that path plus the generic
+//     per-sample sweep, so it fits 64 VGPRs (8 waves per SIMD).
 //
-// Store layout: thread-contiguous 8 samples (sweep_quad<8>, the default:
-// one carrier per 8 samples) or rows (sweep_rows<R>, DPEMU_DDS_ROWS=R): a
-// thread's quads sit 1024 samples apart, so each store instruction of a
-// wave is 1 KiB dense.  A/B history (scripts/ab_dds.py, config 5, 1.72 GB
-// per launch):
-//   * rows vs contiguous: +5-7 % on bare stores (5.7-5.8 vs 5.45 TB/s), but
-//     -10..-25 % on the real kernel, which is VALU-heavy (~24 VALU lane-ops
-//     per sample before v_cvt_pk_i16_i32) and pays a carrier per quad;
-//   * a two-kernel design -- per-channel pulse-segment tables, then one short
-//     fill-like workgroup per 1-8 KiB tile -- lost (3.2-3.5 TB/s): every tile
-//     paid a chain of dependent table lookups that 8 resident workgroups per
-//     CU cannot hide, while a torch fill of the same buffer reaches 6.9 TB/s;
-//   * 2..7 resident workgroups per CU: within 2 % on bare stores.
+// Store layout: thread-contiguous 8 samples.  A/B history (scripts/ab_dds.py,
+// config 5, 1.72 GB per launch, medians; a torch fill of the same buffer
+// takes 0.25 ms):
+//   * every workgroup compacting its own events (slot-major loads, one line
+//     per event) vs the index kernel: 0.36 vs 0.35 ms at 32 Ki-sample chunks;
+//     the index is what makes shorter chunks affordable;
+//   * lean kernel, 16 Ki-sample chunks: 0.344 ms; 8 / 24 / 32 / 64 Ki: 0.41 /
+//     0.36 / 0.37 / 0.47; 4 samples per thread per tile: 0.367;
+//   * the general kernel (89 VGPRs, 5 waves per SIMD), X/Y form: 0.352-0.358
+//     at 32 Ki chunks, 0.397 at 16 Ki;
+//   * the probes with the same grid and prologue but zero stores take 0.33-
+//     0.35 ms and bare chunk-shaped stores 0.29-0.30 (scripts/micro/
+//     store_probe.hip): short 1-D fill-shaped workgroups (4-16 KiB) reach
+//     6.5-7.0 TB/s, 128-KiB chunks 5.6-6.0, persistent grids 4.8-5.4.  The
+//     kernel sits on its store pattern, not on its arithmetic;
+//   * a two-kernel design with a per-tile segment table and one short
+//     fill-like workgroup per 1-8 KiB tile lost (3.2-3.5 TB/s): every tile
+//     paid a chain of dependent table lookups.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,6 +46,10 @@
 #include "kernels.h"
 
 namespace dpemu {
+
+#ifndef LWAVES
+#define LWAVES 8            // waves per SIMD the lean chunk kernel is register-budgeted for
+#endif
 
 // a.lo * b.lo + a.hi * b.hi + c on packed int16 pairs: one VOP3P
 // v_dot2_i32_i16 with the rounding constant in an SGPR
@@ -176,6 +190,35 @@ __device__ __forceinline__ void compact_events(const DDSParams &p, uint32_t lane
     *n_rs = (int)s_cnt[1];
 }
 
+// ---------------------------------------------------------------------------
+// Y-form complex products (the segment kernel and the chunk kernel's quad
+// sweep; see the comment above dds_seg_kernel)
+// ---------------------------------------------------------------------------
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+// {lo: hi, hi: -lo} of an I16|Q16 word
+__device__ __forceinline__ uint32_t neg_swap(uint32_t w) { return (w >> 16) | (((0u - w) & 0xFFFFu) << 16); }
+
+// dot2 results (+2^14) >> 15 of two components -> {lo, hi} saturated to int16
+__device__ __forceinline__ uint32_t pk_sat(int32_t lo, int32_t hi)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(lo >> 15, hi >> 15));
+}
+
+// a0 (x) R_k, symsat, Y form
+__device__ __forceinline__ uint32_t rot_y(uint32_t y0, uint32_t r, uint32_t rp)
+{
+    const short2v v = __builtin_bit_cast(short2v, pk_sat(dot2(rp, y0, 1 << 14), dot2(r, y0, 1 << 14)));
+    const short2v lo = {-32767, -32767};
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, lo));
+}
+
+// sat16(E (x) a), packed {I low, Q high}
+__device__ __forceinline__ uint32_t mix_y(uint32_t e, uint32_t ep, uint32_t y)
+{
+    return pk_sat(dot2(ep, y, 1 << 14), dot2(e, y, 1 << 14));
+}
+
 // ===========================================================================
 // Chunk path
 // ===========================================================================
@@ -285,6 +328,111 @@ __device__ __forceinline__ void sweep_quad(const QuadArgs &q, uint32_t j_first)
     }
 }
 
+// Quad sweep in Y form: the same walk as sweep_quad, with the rotation pairs
+// (R, R') staged in LDS and the env words as (E, E') pairs (PAIRS, interp 1)
+// or single words (E' formed per word), so a sample costs 2 dot2 + pack +
+// max for the rotation and 2 dot2 + pack for the mix.  Needs every staged
+// eq, rq != -32768 (the workgroup's tables; else the generic sweep runs).
+template <int SPT, bool PAIRS>
+__device__ __forceinline__ void sweep_quad_y(const QuadArgs &q, uint32_t j_first)
+{
+    const uint32_t k0 = j_first & (q.spc - 1);
+    int si = last_le(q.st_t, q.n_st, j_first >> q.spc_sh), ri = last_le(q.rs_t, q.n_rs, j_first >> q.spc_sh);
+    int cur = -2;
+    bool act = false;
+    uint32_t base = 0, lim = 0, emask = 0, F0 = 0, ph15 = 0;
+    int32_t a16 = 0;
+    uint32_t R[SPT], Rp[SPT];
+#pragma unroll
+    for (int s = 0; s < SPT; s++) R[s] = Rp[s] = 0;
+    const uint32_t *envp = q.env;
+    for (uint32_t j0 = j_first; j0 < q.c_end; j0 += SPT * BLOCK) {
+        const uint32_t n = j0 >> q.spc_sh;
+        while (si + 1 < q.n_st && q.st_t[si + 1] <= n) si++;
+        while (ri + 1 < q.n_rs && q.rs_t[ri + 1] <= n) ri++;
+        uint32_t v[SPT];
+#pragma unroll
+        for (int s = 0; s < SPT; s++) v[s] = 0;
+        if (si != cur) {                            // new pulse: decode its fields once
+            cur = si;
+            act = false;
+            if (si >= 0) {
+                const uint32_t env_w = q.st_env[si], pf = q.st_pf[si];
+                const uint32_t A = env_w & 0xFFFu, L = (env_w >> 12) & 0xFFFu, fi = pf >> 17;
+                base = q.st_t[si] * q.spc;
+                const uint32_t room = q.env_len > 4 * A ? q.env_len - 4 * A : 0u;
+                if (L) {
+                    emask = 0xFFFFFFFFu;
+                    const uint32_t n_env = min(4 * L, room);
+                    lim = n_env << q.int_sh;
+                    if ((lim >> q.int_sh) != n_env) lim = 0xFFFFFFFFu;
+                } else {
+                    emask = 0u;
+                    lim = room ? 0xFFFFFFFFu : 0u;
+                }
+                envp = q.env + (PAIRS ? 8 * A : 4 * A);
+                act = 16 * fi + 15 < q.freq_len;
+                if (act) {
+                    const uint32_t *frp = q.freq + 32 * fi;     // (R, R') pairs; pair 0 = (F0, 0)
+                    F0 = frp[0];
+#pragma unroll
+                    for (int h = 0; h < SPT / 2; h++) {
+                        const uint4 w = *reinterpret_cast<const uint4 *>(frp + 2 * k0 + 4 * h);
+                        R[2 * h] = w.x; Rp[2 * h] = w.y; R[2 * h + 1] = w.z; Rp[2 * h + 1] = w.w;
+                    }
+                }
+                ph15 = (pf & 0x1FFFFu) << 15;
+                a16 = q.st_amp[si];
+            }
+        }
+        if (act) {
+            const uint32_t t_ref = ri >= 0 ? q.rs_t[ri] : 0u;
+            const uint32_t idx = (F0 * (n - t_ref) + ph15) >> 20;
+            const int32_t c = q.lut[(idx + 1024) & 4095], sn = q.lut[idx];
+            const uint32_t y0 = pack16((c * a16 + (1 << 15)) >> 16, (sn * a16 + (1 << 15)) >> 16);
+            uint32_t E[SPT], Ep[SPT];
+            const uint32_t d0 = j0 - base;
+            const bool inside = d0 + (SPT - 1) < lim;
+            if (PAIRS && inside && emask) {
+#pragma unroll
+                for (int h = 0; h < SPT / 2; h++) {
+                    const uint4 w = *reinterpret_cast<const uint4 *>(envp + 2 * d0 + 4 * h);
+                    E[2 * h] = w.x; Ep[2 * h] = w.y; E[2 * h + 1] = w.z; Ep[2 * h + 1] = w.w;
+                }
+            } else if (PAIRS) {
+#pragma unroll
+                for (int s = 0; s < SPT; s++) {
+                    const uint32_t wi = (d0 + s) & emask;
+                    E[s] = d0 + s < lim ? envp[2 * wi] : 0u;
+                    Ep[s] = d0 + s < lim ? envp[2 * wi + 1] : 0u;
+                }
+            } else if (inside && (((d0 >> q.int_sh) == ((d0 + SPT - 1) >> q.int_sh)) || !emask)) {
+                const uint32_t e = envp[(d0 >> q.int_sh) & emask], ep = neg_swap(e);   // one word for all
+#pragma unroll
+                for (int s = 0; s < SPT; s++) { E[s] = e; Ep[s] = ep; }
+            } else {
+#pragma unroll
+                for (int s = 0; s < SPT; s++) {
+                    E[s] = d0 + s < lim ? envp[((d0 + s) >> q.int_sh) & emask] : 0u;
+                    Ep[s] = neg_swap(E[s]);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < SPT; s++) {
+                uint32_t y = rot_y(y0, R[s], Rp[s]);
+                if (s == 0 && k0 == 0) y = y0;              // sub-sample 0 is the unrotated carrier
+                v[s] = mix_y(E[s], Ep[s], y);
+            }
+            if (!inside) {                                  // the pulse ends inside these samples
+#pragma unroll
+                for (int s = 0; s < SPT; s++) v[s] = d0 + s < lim ? v[s] : 0u;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < SPT / 4; h++) store4(q.out, j0 + 4 * h, q.c_end, v + 4 * h);
+    }
+}
+
 // Row sweep: per tile iteration a thread produces R quads, quad h at
 // j0 + h * ROW (ROW = 4 * BLOCK samples, a multiple of spc), so every store
 // instruction of a wave writes 1 KiB contiguous -- measured 5-7 % faster
@@ -391,8 +539,16 @@ __device__ __forceinline__ void sweep_rows(const QuadArgs &q, uint32_t c_begin)
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
+// LSPT = 0: the general kernel (every path, probe and A/B knob).  LSPT = 4 / 8:
+// the lean production instance -- event index + Y-form quad sweep with LSPT
+// samples per thread per tile (4 where spc is not a multiple of LSPT), the
+// generic sweep for everything else -- whose register budget allows
+// amdgpu_waves_per_eu(LWAVES) (more resident store streams per SIMD).
+template <int LSPT>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LSPT ? LWAVES : 1)))
+dds_chunk_kernel(const DDSParams p)
 {
+    constexpr bool LEAN = LSPT != 0;
     // dynamic LDS (dds_lds_bytes): sine table | compacted strobes / resets |
     // staged env table | staged freq table
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
@@ -415,30 +571,76 @@ __global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
     const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
     const uint32_t spc_sh = __ffs(spc) - 1, int_sh = __ffs(interp) - 1;
-    const bool staged = env_len <= p.env_lds && freq_len <= p.freq_lds;
+    const bool yf = p.yform != 0;           // Y-form quad sweep: (R, R') and interp-1 (E, E') pairs staged
+    const bool staged = yf ? (interp == 1 ? 2 * env_len : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds
+                           : env_len <= p.env_lds && freq_len <= p.freq_lds;
 
     // prologue: every global load of the workgroup up front (compact_events
     // issues the event loads before its first barrier)
-    for (uint32_t i = tid; i < 4096 / 8; i += BLOCK)
-        reinterpret_cast<uint4 *>(s_lut)[i] = reinterpret_cast<const uint4 *>(p.sin_lut)[i];
-    if (staged) {
+    // probes 8..11 (A/B only): the contiguous-store probe minus parts of the
+    // prologue -- 8: no sine table, 9: no env / freq tables, 10: no event
+    // window, 11: none of them, 12: none and no index kernel
+    const uint32_t pr = p.probe;
+    if (pr != 8 && pr < 11)
+        for (uint32_t i = tid; i < 4096 / 8; i += BLOCK)
+            reinterpret_cast<uint4 *>(s_lut)[i] = reinterpret_cast<const uint4 *>(p.sin_lut)[i];
+    bool bad = false;                       // a staged eq or rq is -32768: no Y form
+    if (pr == 9 || pr >= 11) {
+    } else if (staged && yf) {
+        if (interp == 1) {
+            for (uint32_t i = tid; i < env_len; i += BLOCK) {
+                const uint32_t e = p.env[env_off + i];
+                bad |= (e & 0xFFFFu) == 0x8000u;
+                reinterpret_cast<uint2 *>(s_env)[i] = make_uint2(e, neg_swap(e));
+            }
+        } else {
+            for (uint32_t i = tid; i < env_len; i += BLOCK) {
+                const uint32_t e = p.env[env_off + i];
+                bad |= (e & 0xFFFFu) == 0x8000u;
+                s_env[i] = e;
+            }
+        }
+        for (uint32_t i = tid; i < freq_len; i += BLOCK) {
+            const uint32_t w = p.freq[freq_off + i];
+            const bool rot = (i & 15u) != 0;
+            bad |= rot && (w & 0xFFFFu) == 0x8000u;
+            reinterpret_cast<uint2 *>(s_freq)[i] = make_uint2(w, rot ? neg_swap(w) : 0u);
+        }
+    } else if (staged) {
         for (uint32_t i = tid; i < env_len; i += BLOCK) s_env[i] = p.env[env_off + i];
         for (uint32_t i = tid; i < freq_len; i += BLOCK) s_freq[i] = p.freq[freq_off + i];
     }
-    int n_st, n_rs;
-    compact_events(
-        p, lane, elem,
-        [&](uint32_t i, const uint4 &ev, uint32_t amp) {
-            s_st_t[i] = ev.x; s_st_env[i] = ev.z & 0xFFFFFFu; s_st_pf[i] = ev.w; s_st_amp[i] = (uint16_t)amp;
-        },
-        s_rs_t, s_tmp, s_cnt, &n_st, &n_rs);
+    int n_st = 0, n_rs = 0;
+    if (!LEAN && pr >= 10) {
+        __syncthreads();
+    } else if (LEAN || p.xs) {     // indexed: this chunk's window of the channel's compacted events
+        const uint4 w = p.win[(uint64_t)ch * gridDim.x + blockIdx.x];
+        n_st = (int)w.y;
+        n_rs = (int)w.w;
+        const uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds + w.x;
+        const uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds + w.z;
+        for (uint32_t i = tid; i < w.y; i += BLOCK) {
+            const uint4 r = xs[i];
+            s_st_t[i] = r.x; s_st_env[i] = r.y; s_st_pf[i] = r.z; s_st_amp[i] = (uint16_t)r.w;
+        }
+        for (uint32_t i = tid; i < w.w; i += BLOCK) s_rs_t[i] = xr[i];
+        bad = __syncthreads_or(bad);
+    } else if constexpr (!LEAN) {
+        compact_events(
+            p, lane, elem,
+            [&](uint32_t i, const uint4 &ev, uint32_t amp) {
+                s_st_t[i] = ev.x; s_st_env[i] = ev.z & 0xFFFFFFu; s_st_pf[i] = ev.w; s_st_amp[i] = (uint16_t)amp;
+            },
+            s_rs_t, s_tmp, s_cnt, &n_st, &n_rs);
+        if (yf) bad = __syncthreads_or(bad);
+    }
 
     uint32_t *out = p.iq + (uint64_t)ch * p.n_samples;
     const uint32_t c_begin = blockIdx.x * p.chunk;
     const uint32_t c_end = min(c_begin + p.chunk, p.n_samples);
-    if (p.probe == 3 || p.probe == 4) {   // probes: zero stores of the sweep, 8 samples per thread per tile
+    if (!LEAN && (p.probe == 3 || p.probe == 4 || p.probe >= 8)) {   // probes: zero stores of the sweep, 8 samples per thread per tile
         const uint32_t z[4] = {0, 0, 0, (uint32_t)(n_st + n_rs) & 0u};
-        if (p.probe == 3) {      // thread-contiguous 32 B (two half-dense store instructions)
+        if (p.probe != 4 && p.rows == 0) {   // thread-contiguous 32 B (two half-dense store instructions)
             for (uint32_t j0 = c_begin + 8 * tid; j0 < c_end; j0 += 8 * BLOCK) {
                 store4(out, j0, c_end, z);
                 store4(out, j0 + 4, c_end, z);
@@ -452,7 +654,19 @@ __global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
         return;
     }
     const bool quad = staged && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
-    if (quad) {
+    if (quad && (LEAN || yf) && !bad) {
+        const QuadArgs q{s_lut, s_st_t, s_st_env, s_st_pf, s_st_amp, s_rs_t, n_st, n_rs, spc, spc_sh, interp, int_sh,
+                         s_env, env_len, s_freq, freq_len, out, c_end};
+        if (LSPT != 4 && (spc & 7u) == 0) {
+            if (interp == 1) sweep_quad_y<8, true>(q, c_begin + 8 * tid);
+            else sweep_quad_y<8, false>(q, c_begin + 8 * tid);
+        } else {
+            if (interp == 1) sweep_quad_y<4, true>(q, c_begin + 4 * tid);
+            else sweep_quad_y<4, false>(q, c_begin + 4 * tid);
+        }
+        return;
+    }
+    if (!LEAN && quad && !yf) {
         const QuadArgs q{s_lut, s_st_t, s_st_env, s_st_pf, s_st_amp, s_rs_t, n_st, n_rs, spc, spc_sh, interp, int_sh,
                          s_env, env_len, s_freq, freq_len, out, c_end};
         switch (p.rows) {
@@ -502,6 +716,50 @@ __global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
     }
 }
 
+// Event index of the chunk path: one workgroup per channel compacts the
+// lane's strobes of the channel's element and its pulse_resets once (instead
+// of once per chunk: the slot-major event loads are one 16-B line access per
+// event), writes them channel-contiguous, and for every chunk the window of
+// strobes / resets its sweep can see: from the latest one at or before the
+// chunk's first cycle to the latest one at or before its last cycle.  The
+// chunk kernel then loads only its window, coalesced.
+__global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn);
+    uint32_t *s_st_env = s_st_t + p.ev_lds;
+    uint32_t *s_st_pf = s_st_env + p.ev_lds;
+    uint32_t *s_rs_t = s_st_pf + p.ev_lds;
+    uint16_t *s_st_amp = reinterpret_cast<uint16_t *>(s_rs_t + p.ev_lds);
+    __shared__ uint32_t s_tmp[2 * (BLOCK / 64)];
+    __shared__ uint32_t s_cnt[2];
+
+    const uint32_t tid = threadIdx.x, ch = blockIdx.x;
+    const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
+    const uint32_t lane = d[0], elem = d[1] & 3u, spc = d[2];
+    int n_st, n_rs;
+    compact_events(
+        p, lane, elem,
+        [&](uint32_t i, const uint4 &ev, uint32_t amp) {
+            s_st_t[i] = ev.x; s_st_env[i] = ev.z & 0xFFFFFFu; s_st_pf[i] = ev.w; s_st_amp[i] = (uint16_t)amp;
+        },
+        s_rs_t, s_tmp, s_cnt, &n_st, &n_rs);
+    uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
+    uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
+    for (int i = (int)tid; i < n_st; i += BLOCK) xs[i] = make_uint4(s_st_t[i], s_st_env[i], s_st_pf[i], s_st_amp[i]);
+    for (int i = (int)tid; i < n_rs; i += BLOCK) xr[i] = s_rs_t[i];
+    const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
+    for (uint32_t c = tid; c < chunks; c += BLOCK) {
+        const uint64_t c0 = (uint64_t)c * p.chunk, c1 = min(c0 + p.chunk, (uint64_t)p.n_samples) - 1;
+        const uint32_t n0 = (uint32_t)(c0 / spc), n1 = (uint32_t)(c1 / spc);
+        const int s0 = last_le(s_st_t, n_st, n0), s1 = last_le(s_st_t, n_st, n1);
+        const int r0 = last_le(s_rs_t, n_rs, n0), r1 = last_le(s_rs_t, n_rs, n1);
+        const int sl = max(s0, 0), rl = max(r0, 0);
+        p.win[(uint64_t)ch * chunks + c] = make_uint4((uint32_t)sl, (uint32_t)(s1 + 1 - sl), (uint32_t)rl,
+                                                     (uint32_t)(r1 + 1 - rl));
+    }
+}
+
 // ===========================================================================
 // Segment path: dds_seg_kernel (channels with spc in {8, 16}, power-of-two
 // interp, env / freq tables staged in LDS; DDS_SEG_FLAG in the descriptor).
@@ -529,31 +787,6 @@ __global__ void __launch_bounds__(BLOCK) dds_chunk_kernel(const DDSParams p)
 // v_pk_max_i16 for symsat).  R' / E' need rq, eq != -32768; a workgroup whose
 // tables hold one falls back to the per-sample X/Y path for every group.
 // ===========================================================================
-typedef short short2v __attribute__((ext_vector_type(2)));
-
-// {lo: hi, hi: -lo} of an I16|Q16 word
-__device__ __forceinline__ uint32_t neg_swap(uint32_t w) { return (w >> 16) | (((0u - w) & 0xFFFFu) << 16); }
-
-// dot2 results (+2^14) >> 15 of two components -> {lo, hi} saturated to int16
-__device__ __forceinline__ uint32_t pk_sat(int32_t lo, int32_t hi)
-{
-    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(lo >> 15, hi >> 15));
-}
-
-// a0 (x) R_k, symsat, Y form
-__device__ __forceinline__ uint32_t rot_y(uint32_t y0, uint32_t r, uint32_t rp)
-{
-    const short2v v = __builtin_bit_cast(short2v, pk_sat(dot2(rp, y0, 1 << 14), dot2(r, y0, 1 << 14)));
-    const short2v lo = {-32767, -32767};
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, lo));
-}
-
-// sat16(E (x) a), packed {I low, Q high}
-__device__ __forceinline__ uint32_t mix_y(uint32_t e, uint32_t ep, uint32_t y)
-{
-    return pk_sat(dot2(ep, y, 1 << 14), dot2(e, y, 1 << 14));
-}
-
 struct SegArgs {
     const int16_t *lut;
     const uint4 *rec;               // 2 x uint4 per strobe
@@ -661,6 +894,29 @@ __device__ __forceinline__ void sweep_seg(const SegArgs &q)
     }
 }
 
+// strobe i's 32-B segment record (t = strobe cycle, env_w = env word, pf =
+// phase | freq index, amp); F0 comes from the staged (R, R') pairs
+__device__ __forceinline__ void seg_record(uint4 *rec, const uint32_t *fr2, uint32_t i, uint32_t t, uint32_t env_w,
+                                           uint32_t pf, uint32_t amp, uint32_t spc, uint32_t ish, uint32_t env_len,
+                                           uint32_t freq_len)
+{
+    const uint32_t A = env_w & 0xFFFu, L = (env_w >> 12) & 0xFFFu, fi = pf >> 17;
+    const uint32_t b = t * spc;
+    const uint32_t room = env_len > 4 * A ? env_len - 4 * A : 0u;
+    uint32_t lim;
+    if (L) {
+        const uint32_t n_env = min(4 * L, room);
+        lim = n_env << ish;
+        if ((lim >> ish) != n_env) lim = 0xFFFFFFFFu;
+    } else {
+        lim = room ? 0xFFFFFFFFu : 0u;
+    }
+    const bool act = 16 * fi + 15 < freq_len;
+    const uint32_t e = !act ? b : (lim > 0xFFFFFFFFu - b ? 0xFFFFFFFFu : b + lim);
+    rec[2 * i] = make_uint4(b, e, (4 * A) | ((L ? 0u : 1u) << 15) | ((amp & 0xFFFFu) << 16), (pf & 0x1FFFFu) << 15);
+    rec[2 * i + 1] = make_uint4(act ? fr2[32 * fi] : 0u, 32 * fi, 0u, 0u);
+}
+
 // Persistent: gridDim.x workgroups (all resident) each take a contiguous
 // range of the (segment channel, sub-chunk) items, channel-major, so a
 // workgroup stages the sine table once and compacts a channel's events once
@@ -689,7 +945,7 @@ __global__ void __launch_bounds__(BLOCK) dds_seg_kernel(const DDSParams p)
     const uint64_t total = (uint64_t)p.n_seg * n_sub;
     const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
     const uint64_t it_end = min((uint64_t)(blockIdx.x + 1) * per, total);
-    uint32_t cur = 0xFFFFFFFFu, ch = 0, spc_sh = 0, int_sh = 0;
+    uint32_t cur = 0xFFFFFFFFu, ch = 0, spc_sh = 0, int_sh = 0, spc_c = 1, env_len_c = 0, freq_len_c = 0;
     int n_st = 0, n_rs = 0;
     bool bad = false;
     if (p.probe == 5) {                     // probe: the sweep's stores alone (zeros)
@@ -736,31 +992,30 @@ __global__ void __launch_bounds__(BLOCK) dds_seg_kernel(const DDSParams p)
                 bad |= rot && (w & 0xFFFFu) == 0x8000u;
                 reinterpret_cast<uint2 *>(s_fr2)[i] = make_uint2(w, rot ? neg_swap(w) : 0u);
             }
-            const uint32_t ish = int_sh;
-            compact_events(
-                p, lane, elem,
-                [&](uint32_t i, const uint4 &ev, uint32_t amp) {
-                    const uint32_t env_w = ev.z & 0xFFFFFFu, pf = ev.w;
-                    const uint32_t A = env_w & 0xFFFu, L = (env_w >> 12) & 0xFFFu, fi = pf >> 17;
-                    const uint32_t b = ev.x * spc;
-                    const uint32_t room = env_len > 4 * A ? env_len - 4 * A : 0u;
-                    uint32_t lim;
-                    if (L) {
-                        const uint32_t n_env = min(4 * L, room);
-                        lim = n_env << ish;
-                        if ((lim >> ish) != n_env) lim = 0xFFFFFFFFu;
-                    } else {
-                        lim = room ? 0xFFFFFFFFu : 0u;
-                    }
-                    const bool act = 16 * fi + 15 < freq_len;
-                    const uint32_t e = !act ? b : (lim > 0xFFFFFFFFu - b ? 0xFFFFFFFFu : b + lim);
-                    s_st_t[i] = ev.x;
-                    s_rec[2 * i] = make_uint4(b, e, (4 * A) | ((L ? 0u : 1u) << 15) | ((amp & 0xFFFFu) << 16),
-                                              (pf & 0x1FFFFu) << 15);
-                    s_rec[2 * i + 1] = make_uint4(act ? s_fr2[32 * fi] : 0u, 32 * fi, 0u, 0u);
-                },
-                s_rs_t, s_tmp, s_cnt, &n_st, &n_rs);
-            bad = __syncthreads_or(bad);
+            env_len_c = env_len; freq_len_c = freq_len; spc_c = spc;
+            if (!p.xs)
+                compact_events(
+                    p, lane, elem,
+                    [&](uint32_t i, const uint4 &ev, uint32_t amp) {
+                        s_st_t[i] = ev.x;
+                        seg_record(s_rec, s_fr2, i, ev.x, ev.z & 0xFFFFFFu, ev.w, amp, spc, int_sh, env_len, freq_len);
+                    },
+                    s_rs_t, s_tmp, s_cnt, &n_st, &n_rs);
+            bad = __syncthreads_or(bad);    // (index path: also publishes s_fr2 for the records)
+        }
+        if (p.xs) {                         // indexed: this sub-chunk's window of the channel's events
+            const uint4 w = p.win[(uint64_t)ch * n_sub + sub];
+            n_st = (int)w.y;
+            n_rs = (int)w.w;
+            const uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds + w.x;
+            const uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds + w.z;
+            for (uint32_t i = tid; i < w.y; i += BLOCK) {
+                const uint4 r = xs[i];
+                s_st_t[i] = r.x;
+                seg_record(s_rec, s_fr2, i, r.x, r.y, r.z, r.w, spc_c, int_sh, env_len_c, freq_len_c);
+            }
+            for (uint32_t i = tid; i < w.w; i += BLOCK) s_rs_t[i] = xr[i];
+            __syncthreads();
         }
 
         // group table of the sub-chunk: thread tid owns groups [g0, g1)
@@ -814,6 +1069,13 @@ static hipError_t opt_in_lds(const void *fn, uint32_t bytes, uint32_t *granted)
 hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, bool any_chunk, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
+    if (p.xs) {                             // the event index of every channel (both paths)
+        const uint32_t ilds = p.ev_lds * 18;
+        static uint32_t igranted = 0;
+        const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_index_kernel), ilds, &igranted);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), ilds, stream, p);
+    }
     if (any_seg && ps.n_seg) {
         const uint32_t lds = dds_seg_lds_bytes(ps.ev_lds, ps.env_lds, ps.freq_lds, ps.chunk) + ps.lds_pad;
         static uint32_t granted = 0;
@@ -828,16 +1090,24 @@ hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, boo
             return e;
         if (ps.grid_per_cu) per_cu = std::min<int>(per_cu, (int)ps.grid_per_cu);
         const uint64_t items = (uint64_t)ps.n_seg * ((ps.n_samples + ps.chunk - 1) / ps.chunk);
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(items, (uint64_t)std::max(1, cus * std::max(1, per_cu)));
+        // indexed: one item per workgroup (no per-channel compaction to amortise)
+        const uint32_t grid = ps.xs ? (uint32_t)items
+                                    : (uint32_t)std::min<uint64_t>(items, (uint64_t)std::max(1, cus * std::max(1, per_cu)));
         hipLaunchKernelGGL(dds_seg_kernel, dim3(grid), dim3(BLOCK), lds, stream, ps);
     }
     if (any_chunk) {
         const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
         const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) + p.lds_pad;
-        static uint32_t granted = 0;
-        const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_chunk_kernel), lds, &granted);
+        const bool lean = p.xs && p.yform && !p.rows && !p.probe;
+        const void *fn = !lean ? reinterpret_cast<const void *>(dds_chunk_kernel<0>)
+                         : p.spt == 4 ? reinterpret_cast<const void *>(dds_chunk_kernel<4>)
+                                      : reinterpret_cast<const void *>(dds_chunk_kernel<8>);
+        static uint32_t granted[3] = {0, 0, 0};
+        const hipError_t e = opt_in_lds(fn, lds, &granted[!lean ? 0 : p.spt == 4 ? 1 : 2]);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(dds_chunk_kernel, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
+        if (!lean) hipLaunchKernelGGL(dds_chunk_kernel<0>, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
+        else if (p.spt == 4) hipLaunchKernelGGL(dds_chunk_kernel<4>, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
+        else hipLaunchKernelGGL(dds_chunk_kernel<8>, dim3(chunks, p.n_channels), dim3(BLOCK), lds, stream, p);
     }
     return hipGetLastError();
 }

@@ -159,14 +159,21 @@ struct DDSParams {
     uint32_t rows;                 // quad rows per thread per tile (1, 2, 4); 0 = 8 contiguous samples
     uint32_t probe;                // measurement probes (DPEMU_DDS_PROBE): 3 / 4 = bare stores,
                                    // thread-contiguous / rows layout; 0 = normal
+    uint32_t spt;                  // lean chunk kernel: samples per thread per tile (4 or 8)
+    uint32_t yform;                // chunk kernel: Y-form quad sweep (pair-staged tables; 0 = X/Y form)
     uint32_t lds_pad;              // extra dynamic LDS per workgroup (DPEMU_DDS_LDSPAD, occupancy A/B)
     const uint32_t *seg_list;      // segment kernel: its channels (indices into ch)
     uint32_t n_seg;
     uint32_t grid_per_cu;          // segment kernel: workgroups per CU (0 = occupancy)
+    // chunk path event index (dds_index_kernel -> dds_chunk_kernel; null = each
+    // workgroup compacts its lane's events itself)
+    uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env, phase | freq, amp}
+    uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
+    uint4 *win;                    // [n_channels][chunks] {strobe lo, count, reset lo, count}
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
 constexpr uint32_t DDS_MAX_EVENTS = 1024;
-constexpr uint32_t DDS_CHUNK = 1u << 15;   // samples per workgroup
+constexpr uint32_t DDS_CHUNK = 1u << 14;   // samples per workgroup (lean kernel A/B: 16 Ki beats 8 / 24 / 32 Ki)
 constexpr uint32_t DDS_ENV_LDS_MAX = 8192;   // words: tables up to 32 KiB are staged in LDS
 constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;  // words: 128 freq entries
 
@@ -174,6 +181,12 @@ constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;  // words: 128 freq entries
 inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_lds)
 {
     return 4096 * 2 + ev_lds * 18 + (env_lds + freq_lds) * 4;
+}
+
+// bytes of the chunk path's event index (xs, xr, win)
+inline uint64_t dds_index_bytes(uint32_t n_channels, uint32_t ev_lds, uint32_t chunks)
+{
+    return (uint64_t)n_channels * ev_lds * 20 + (uint64_t)n_channels * chunks * 16;
 }
 
 // dynamic LDS bytes of dds_seg_kernel; env_lds counts words as staged

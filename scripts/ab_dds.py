@@ -22,18 +22,16 @@ elems = tuple(int(c) for c in (sys.argv[4] if len(sys.argv) > 4 else '01'))
 ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
 ctx = {}
 VARIANTS = [  # name, env knobs (read once, at dpemu_create)
-    ('seg_c32k', {}),
-    ('seg_c16k', {'DPEMU_DDS_SEG_CHUNK': '16384'}),
-    ('seg_c32k_2cu', {'DPEMU_DDS_SEG_PER_CU': '2'}),
-    ('chunk_contig8_c32k', {'DPEMU_DDS_SEG': '0'}),
-    ('probe_contig_stores', {'DPEMU_DDS_PROBE': '3'}),
-    ('probe_seg_stores', {'DPEMU_DDS_PROBE': '5'}),
-    ('probe_seg_tables_zero', {'DPEMU_DDS_PROBE': '6'}),
-    ('probe_seg_tables_gword', {'DPEMU_DDS_PROBE': '7'}),
-    ('probe_seg_stores_c16k', {'DPEMU_DDS_PROBE': '5', 'DPEMU_DDS_SEG_CHUNK': '16384'}),
-    ('probe_seg_stores_2cu', {'DPEMU_DDS_PROBE': '5', 'DPEMU_DDS_SEG_PER_CU': '2'}),
+    ('lean8_c16k', {'DPEMU_DDS_CHUNK': '16384'}),
+    ('lean8_c32k', {}),
+    ('lean8_c8k', {'DPEMU_DDS_CHUNK': '8192'}),
+    ('lean8_c24k', {'DPEMU_DDS_CHUNK': '24576'}),
+    ('lean4_c16k', {'DPEMU_DDS_SPT': '4', 'DPEMU_DDS_CHUNK': '16384'}),
+    ('general_xy_c32k', {'DPEMU_DDS_YFORM': '0'}),
+    ('general_xy_c16k', {'DPEMU_DDS_YFORM': '0', 'DPEMU_DDS_CHUNK': '16384'}),
+    ('general_xy_noidx_c32k', {'DPEMU_DDS_YFORM': '0', 'DPEMU_DDS_INDEX': '0'}),
 ]
-KNOBS = ('DPEMU_DDS_SEG', 'DPEMU_DDS_SEG_CHUNK', 'DPEMU_DDS_SEG_PER_CU', 'DPEMU_DDS_PROBE', 'DPEMU_DDS_ROWS', 'DPEMU_DDS_CHUNK')
+KNOBS = ('DPEMU_DDS_SPT', 'DPEMU_DDS_YFORM', 'DPEMU_DDS_INDEX', 'DPEMU_DDS_SEG', 'DPEMU_DDS_SEG_CHUNK', 'DPEMU_DDS_SEG_PER_CU', 'DPEMU_DDS_PROBE', 'DPEMU_DDS_ROWS', 'DPEMU_DDS_CHUNK')
 for name, knobs in VARIANTS:
     for k in KNOBS:
         os.environ.pop(k, None)
@@ -41,7 +39,7 @@ for name, knobs in VARIANTS:
     ctx[name] = Emulator(0)
 for k in KNOBS:
     os.environ.pop(k, None)
-emu = ctx['seg_c32k']
+emu = ctx[VARIANTS[0][0]]
 emu.load(ps)
 cfg = _abi.make_config(8, n_groups=ps.n_groups, event_cap=512, meas_cap=4)
 ev = alloc_device_outputs(cfg, n_seq, want=('summary', 'ev_main', 'ev_amp'))

@@ -82,6 +82,26 @@ __global__ void __launch_bounds__(BLOCK) persist_k(uint32_t *iq, uint64_t total)
     }
 }
 
+// one 16-B store per thread, WG of B threads: the torch elementwise-fill shape
+template <int B>
+__global__ void __launch_bounds__(B) fill1_k(uint32_t *iq, uint64_t total)
+{
+    const uint64_t j = ((uint64_t)blockIdx.x * B + threadIdx.x) * 4;
+    if (j + 3 < total) st<false>(iq + j, (uint32_t)j);
+}
+
+// U 16-B row stores per thread (each instruction 1 KiB dense per wave), WG of 256
+template <int U>
+__global__ void __launch_bounds__(BLOCK) fillU_k(uint32_t *iq, uint64_t total)
+{
+    const uint64_t b = (uint64_t)blockIdx.x * (U * 4 * BLOCK);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t j = b + 4 * threadIdx.x + (uint64_t)u * 4 * BLOCK;
+        if (j + 3 < total) st<false>(iq + j, (uint32_t)j);
+    }
+}
+
 static double timeit(void (*launch)(void *), void *a, uint64_t bytes)
 {
     hipEvent_t e0, e1;
@@ -117,6 +137,17 @@ int main(int argc, char **argv)
         fflush(stdout);
     };
     const uint32_t chunks = (g.ns + 32767) / 32768;
+    {
+        const uint64_t tot = (uint64_t)g.nch * g.ns;
+        report("fill1_64", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fill1_k<64><<<(uint32_t)((t / 4 + 63) / 64), 64>>>(g.iq, t); });
+        report("fill1_128", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fill1_k<128><<<(uint32_t)((t / 4 + 127) / 128), 128>>>(g.iq, t); });
+        report("fill1_256", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fill1_k<256><<<(uint32_t)((t / 4 + 255) / 256), 256>>>(g.iq, t); });
+        report("fill1_512", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fill1_k<512><<<(uint32_t)((t / 4 + 511) / 512), 512>>>(g.iq, t); });
+        report("fillU_2", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fillU_k<2><<<(uint32_t)((t + 2047) / 2048), BLOCK>>>(g.iq, t); });
+        report("fillU_4", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fillU_k<4><<<(uint32_t)((t + 4095) / 4096), BLOCK>>>(g.iq, t); });
+        report("fillU_8", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fillU_k<8><<<(uint32_t)((t + 8191) / 8192), BLOCK>>>(g.iq, t); });
+        (void)tot;
+    }
     report("chunk_contig", [](void *) { chunk_k<false, false><<<dim3((g.ns + 32767) / 32768, g.nch), BLOCK>>>(g.iq, g.ns, 32768); });
     report("chunk_rows", [](void *) { chunk_k<false, true><<<dim3((g.ns + 32767) / 32768, g.nch), BLOCK>>>(g.iq, g.ns, 32768); });
     report("chunk_contig_nt", [](void *) { chunk_k<true, false><<<dim3((g.ns + 32767) / 32768, g.nch), BLOCK>>>(g.iq, g.ns, 32768); });

@@ -27,13 +27,17 @@ def emu():
     e.close()
 
 
-def make_emu(rows, seg=1):
+def make_emu(rows, seg=1, index=1, yform=1, spt=8):
     """an Emulator whose DDS uses the segment kernel for eligible channels
-    (seg=1, the default) or the chunk kernel for all (seg=0), with `rows`
-    quad rows per thread in the chunk kernel (0 = eight contiguous samples);
-    DPEMU_DDS_SEG / DPEMU_DDS_ROWS are read once, at dpemu_create"""
+    (seg=1) or the chunk kernel for all (seg=0), with `rows` quad rows per
+    thread in the chunk kernel (0 = eight contiguous samples), fed by the
+    per-channel event index (index=1, the default) or compacting events in
+    every workgroup (index=0), the chunk kernel's quad sweep in Y form
+    (yform=1, the default; rows apply to the X/Y form only); the knobs are
+    read once, at dpemu_create"""
     import os
-    knobs = {'DPEMU_DDS_ROWS': str(rows), 'DPEMU_DDS_SEG': str(seg)}
+    knobs = {'DPEMU_DDS_ROWS': str(rows), 'DPEMU_DDS_SEG': str(seg), 'DPEMU_DDS_INDEX': str(index),
+             'DPEMU_DDS_YFORM': str(yform), 'DPEMU_DDS_SPT': str(spt)}
     old = {k: os.environ.get(k) for k in knobs}
     os.environ.update(knobs)
     try:
@@ -46,8 +50,10 @@ def make_emu(rows, seg=1):
                 os.environ[k] = v
 
 
-@pytest.fixture(scope='module', params=[(0, 1), (0, 0), (1, 0), (2, 0), (4, 0)],
-                ids=lambda r: 'seg' if r[1] else 'chunk_rows{}'.format(r[0]))
+@pytest.fixture(scope='module', params=[(0, 0, 1, 1, 8), (0, 0, 1, 1, 4), (0, 1, 1, 1, 8), (0, 0, 1, 0, 8),
+                                        (2, 0, 1, 0, 8), (0, 1, 0, 1, 8), (0, 0, 0, 1, 8)],
+                ids=lambda r: ('seg' if r[1] else 'chunk_rows{}'.format(r[0])) + ('' if r[2] else '_noindex')
+                + ('' if r[3] or r[1] else '_xy') + ('_spt4' if r[4] == 4 else ''))
 def emu_path(request):
     e = make_emu(*request.param)
     yield e
