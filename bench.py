@@ -157,11 +157,13 @@ def dds_leg(emu, args, world, rank, stream):
     res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
            'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s',
            'ms_per_step': dt / args.steps * 1e3, 'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
+           'step': 'dds_index_kernel (per-channel event index) + dds_chunk_kernel; kernel_ms and the roofline '
+                   'hold dds_chunk_kernel alone, value and ms_per_step the whole step',
            'config': {'workload': 'config5_dds_rb8', 'sequences_per_gpu': n, 'channels_per_gpu': plan.n_channels,
                       'samples_per_channel': n_samples, 'rb_depth': 200},
            'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                         'frac': gbs / HBM_PEAK_GBS, 'traffic': traffic, 'bytes_per_launch': samples * 4,
-                        'kernel': 'dpemu::dds_index_kernel + dpemu::dds_chunk_kernel<8> (one HIP-event bracket)'}}
+                        'kernel': 'dpemu::dds_chunk_kernel<4>'}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host_ev = {k: v.cpu().numpy() for k, v in ev.items()}
         res['cpu_baseline'] = dds_cpu_baseline(plan, host_ev, n_samples, args.cpu_seconds * 2 / 3)

@@ -15,22 +15,26 @@
 //     and sweeps its chunk with no global loads in the loop: on gfx950 stores
 //     count in vmcnt, and a load in the loop would make every tile wait for
 //     the previous tile's stores.  A pulse's fields are decoded once per
-//     thread, the carrier once per 8 samples.  The production instance
-//     (LSPT = 8, the "lean" kernel) holds only that path plus the generic
-//     per-sample sweep, so it fits 64 VGPRs (8 waves per SIMD).
+//     thread, the carrier once per 4 or 8 samples.  The production
+//     instances (LSPT = 4 / 8, the "lean" kernel) hold only that path plus
+//     the generic per-sample sweep, so they fit 64 VGPRs (8 waves per SIMD).
+//     Default: LSPT = 4 (each thread one 16-B store per tile, 1 KiB dense
+//     per wave-instruction).
 //
-// Store layout: thread-contiguous 8 samples.  A/B history (scripts/ab_dds.py,
-// config 5, 1.72 GB per launch, medians; a torch fill of the same buffer
-// takes 0.25 ms):
+// Store layout: thread-contiguous 4 (default) or 8 samples.  A/B history
+// (scripts/ab_dds.py, config 5, 1.72 GB per launch, medians incl. the index
+// kernel's 0.018 ms; a torch fill of the same buffer takes 0.245-0.25 ms):
 //   * every workgroup compacting its own events (slot-major loads, one line
 //     per event) vs the index kernel: 0.36 vs 0.35 ms at 32 Ki-sample chunks;
 //     the index is what makes shorter chunks affordable;
-//   * lean kernel, 16 Ki-sample chunks: 0.344 ms; 8 / 24 / 32 / 64 Ki: 0.41 /
-//     0.36 / 0.37 / 0.47; 4 samples per thread per tile: 0.367;
+//   * lean kernel, 16 Ki-sample chunks: LSPT 4: 0.322-0.342 ms; LSPT 8:
+//     0.325-0.349 walking the strobes, 0.332-0.336 with the per-chunk cycle
+//     table (fewer VALU, 8 KiB more LDS: fewer resident workgroups);
+//     8 / 24 / 32 Ki chunks: 0.37-0.45 / 0.36 / 0.36-0.37;
 //   * the general kernel (89 VGPRs, 5 waves per SIMD), X/Y form: 0.352-0.358
 //     at 32 Ki chunks, 0.397 at 16 Ki;
-//   * the probes with the same grid and prologue but zero stores take 0.33-
-//     0.35 ms and bare chunk-shaped stores 0.29-0.30 (scripts/micro/
+//   * the same grid and prologue with zero stores: 0.343 ms (general kernel,
+//     16 Ki); bare chunk-shaped stores 0.29-0.30 (scripts/micro/
 //     store_probe.hip): short 1-D fill-shaped workgroups (4-16 KiB) reach
 //     6.5-7.0 TB/s, 128-KiB chunks 5.6-6.0, persistent grids 4.8-5.4.  The
 //     kernel sits on its store pattern, not on its arithmetic;
@@ -46,6 +50,8 @@
 #include "kernels.h"
 
 namespace dpemu {
+
+constexpr uint32_t DDS_CYC_CHUNK_MAX = 64 * BLOCK;   // the lean kernel's cycle table: 8 entries per thread, spc >= 8
 
 #ifndef LWAVES
 #define LWAVES 8            // waves per SIMD the lean chunk kernel is register-budgeted for
@@ -235,6 +241,8 @@ struct QuadArgs {
     uint32_t freq_len;
     uint32_t *out;
     uint32_t c_end;                 // end of this workgroup's samples
+    const uint32_t *cyc;            // optional cycle table: entry n - n_first = (strobe + 1) | (reset + 1) << 16
+    uint32_t n_first;
 };
 
 // Quad sweep: a thread's SPT consecutive samples (SPT | spc) share one
@@ -348,8 +356,14 @@ __device__ __forceinline__ void sweep_quad_y(const QuadArgs &q, uint32_t j_first
     const uint32_t *envp = q.env;
     for (uint32_t j0 = j_first; j0 < q.c_end; j0 += SPT * BLOCK) {
         const uint32_t n = j0 >> q.spc_sh;
-        while (si + 1 < q.n_st && q.st_t[si + 1] <= n) si++;
-        while (ri + 1 < q.n_rs && q.rs_t[ri + 1] <= n) ri++;
+        if (q.cyc) {                                // one LDS word instead of walking the strobes
+            const uint32_t w = q.cyc[n - q.n_first];
+            si = (int)(w & 0xFFFFu) - 1;
+            ri = (int)(w >> 16) - 1;
+        } else {
+            while (si + 1 < q.n_st && q.st_t[si + 1] <= n) si++;
+            while (ri + 1 < q.n_rs && q.rs_t[ri + 1] <= n) ri++;
+        }
         uint32_t v[SPT];
 #pragma unroll
         for (int s = 0; s < SPT; s++) v[s] = 0;
@@ -385,7 +399,7 @@ __device__ __forceinline__ void sweep_quad_y(const QuadArgs &q, uint32_t j_first
                 a16 = q.st_amp[si];
             }
         }
-        if (act) {
+        if (act && j0 - base < lim) {               // (a finished pulse plays zeros)
             const uint32_t t_ref = ri >= 0 ? q.rs_t[ri] : 0u;
             const uint32_t idx = (F0 * (n - t_ref) + ph15) >> 20;
             const int32_t c = q.lut[(idx + 1024) & 4095], sn = q.lut[idx];
@@ -654,9 +668,62 @@ dds_chunk_kernel(const DDSParams p)
         return;
     }
     const bool quad = staged && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
+    const uint32_t n_c0 = c_begin >> spc_sh;     // the chunk's first cycle (power-of-two spc)
+    uint32_t *s_cyc = nullptr;
+    if (LEAN && LSPT == 8 && quad && !bad && (spc & 7u) == 0 && p.chunk <= DDS_CYC_CHUNK_MAX && p.cyc) {
+        // cycle table of the chunk (<= chunk / 8 cycles): entry r = (1 + latest strobe at or
+        // before cycle n_first + r) | (1 + latest reset) << 16, window indices, 0 = none.
+        // Scatter each strobe / reset to its cycle (strobe and reset times are
+        // strictly increasing; only window entry 0 can precede the chunk), then
+        // an inclusive max-scan of both halves at once (v_pk_max_u16).
+        s_cyc = reinterpret_cast<uint32_t *>(s_dyn + dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds));
+        const uint32_t n_last = (c_end - 1) >> spc_sh;
+        uint16_t *c16 = reinterpret_cast<uint16_t *>(s_cyc);
+        reinterpret_cast<uint4 *>(s_cyc)[2 * tid] = make_uint4(0, 0, 0, 0);   // 8 entries per thread
+        reinterpret_cast<uint4 *>(s_cyc)[2 * tid + 1] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        for (int i = (int)tid; i < n_st; i += BLOCK) {
+            const uint32_t t = s_st_t[i];
+            if (t <= n_last) c16[2 * (t > n_c0 ? t - n_c0 : 0u)] = (uint16_t)(i + 1);
+        }
+        for (int i = (int)tid; i < n_rs; i += BLOCK) {
+            const uint32_t t = s_rs_t[i];
+            if (t <= n_last) c16[2 * (t > n_c0 ? t - n_c0 : 0u) + 1] = (uint16_t)(i + 1);
+        }
+        __syncthreads();
+        constexpr uint32_t PER = 8;                  // entries per thread (chunk / 8 <= 8 * BLOCK)
+        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+        uint32_t e[PER];
+        const uint4 w0 = reinterpret_cast<const uint4 *>(s_cyc)[2 * tid];
+        const uint4 w1 = reinterpret_cast<const uint4 *>(s_cyc)[2 * tid + 1];
+        e[0] = w0.x; e[1] = w0.y; e[2] = w0.z; e[3] = w0.w; e[4] = w1.x; e[5] = w1.y; e[6] = w1.z; e[7] = w1.w;
+        auto pmax = [](uint32_t a, uint32_t b) {
+            return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(us2, a),
+                                                                         __builtin_bit_cast(us2, b)));
+        };
+#pragma unroll
+        for (uint32_t k = 1; k < PER; k++) e[k] = pmax(e[k], e[k - 1]);
+        const uint32_t wl = tid & 63, wv = tid >> 6;
+        uint32_t m = e[PER - 1];
+#pragma unroll
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(m, off);
+            if (wl >= off) m = pmax(m, y);
+        }
+        if (wl == 63) s_tmp[wv] = m;
+        uint32_t ex = __shfl_up(m, 1);
+        if (wl == 0) ex = 0;
+        __syncthreads();
+        for (uint32_t k = 0; k < wv; k++) ex = pmax(ex, s_tmp[k]);
+#pragma unroll
+        for (uint32_t k = 0; k < PER; k++) e[k] = pmax(e[k], ex);
+        reinterpret_cast<uint4 *>(s_cyc)[2 * tid] = make_uint4(e[0], e[1], e[2], e[3]);
+        reinterpret_cast<uint4 *>(s_cyc)[2 * tid + 1] = make_uint4(e[4], e[5], e[6], e[7]);
+        __syncthreads();
+    }
     if (quad && (LEAN || yf) && !bad) {
         const QuadArgs q{s_lut, s_st_t, s_st_env, s_st_pf, s_st_amp, s_rs_t, n_st, n_rs, spc, spc_sh, interp, int_sh,
-                         s_env, env_len, s_freq, freq_len, out, c_end};
+                         s_env, env_len, s_freq, freq_len, out, c_end, s_cyc, n_c0};
         if (LSPT != 4 && (spc & 7u) == 0) {
             if (interp == 1) sweep_quad_y<8, true>(q, c_begin + 8 * tid);
             else sweep_quad_y<8, false>(q, c_begin + 8 * tid);
@@ -668,7 +735,7 @@ dds_chunk_kernel(const DDSParams p)
     }
     if (!LEAN && quad && !yf) {
         const QuadArgs q{s_lut, s_st_t, s_st_env, s_st_pf, s_st_amp, s_rs_t, n_st, n_rs, spc, spc_sh, interp, int_sh,
-                         s_env, env_len, s_freq, freq_len, out, c_end};
+                         s_env, env_len, s_freq, freq_len, out, c_end, nullptr, 0};
         switch (p.rows) {
         case 1: sweep_rows<1>(q, c_begin); break;
         case 2: sweep_rows<2>(q, c_begin); break;
@@ -723,7 +790,7 @@ dds_chunk_kernel(const DDSParams p)
 // strobes / resets its sweep can see: from the latest one at or before the
 // chunk's first cycle to the latest one at or before its last cycle.  The
 // chunk kernel then loads only its window, coalesced.
-__global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) dds_index_kernel(const DDSParams p)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn);
@@ -1066,16 +1133,20 @@ static hipError_t opt_in_lds(const void *fn, uint32_t bytes, uint32_t *granted)
     return e;
 }
 
+hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
+{
+    if (!p.n_channels || !p.n_samples || !p.xs) return hipSuccess;
+    const uint32_t ilds = p.ev_lds * 18;
+    static uint32_t granted = 0;
+    const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_index_kernel), ilds, &granted);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), ilds, stream, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, bool any_chunk, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    if (p.xs) {                             // the event index of every channel (both paths)
-        const uint32_t ilds = p.ev_lds * 18;
-        static uint32_t igranted = 0;
-        const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_index_kernel), ilds, &igranted);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), ilds, stream, p);
-    }
     if (any_seg && ps.n_seg) {
         const uint32_t lds = dds_seg_lds_bytes(ps.ev_lds, ps.env_lds, ps.freq_lds, ps.chunk) + ps.lds_pad;
         static uint32_t granted = 0;
@@ -1097,8 +1168,10 @@ hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, boo
     }
     if (any_chunk) {
         const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
-        const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) + p.lds_pad;
         const bool lean = p.xs && p.yform && !p.rows && !p.probe;
+        // lean SPT-8 kernel: + the cycle table (chunk / 8 u32 entries, 8 per thread)
+        const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) + p.lds_pad +
+                             (lean && p.spt != 4 && p.cyc ? 32 * BLOCK : 0u);
         const void *fn = !lean ? reinterpret_cast<const void *>(dds_chunk_kernel<0>)
                          : p.spt == 4 ? reinterpret_cast<const void *>(dds_chunk_kernel<4>)
                                       : reinterpret_cast<const void *>(dds_chunk_kernel<8>);

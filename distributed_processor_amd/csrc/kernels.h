@@ -159,6 +159,7 @@ struct DDSParams {
     uint32_t rows;                 // quad rows per thread per tile (1, 2, 4); 0 = 8 contiguous samples
     uint32_t probe;                // measurement probes (DPEMU_DDS_PROBE): 3 / 4 = bare stores,
                                    // thread-contiguous / rows layout; 0 = normal
+    uint32_t cyc;                  // lean chunk kernel: per-chunk cycle table (0 = walk the strobes)
     uint32_t spt;                  // lean chunk kernel: samples per thread per tile (4 or 8)
     uint32_t yform;                // chunk kernel: Y-form quad sweep (pair-staged tables; 0 = X/Y form)
     uint32_t lds_pad;              // extra dynamic LDS per workgroup (DPEMU_DDS_LDSPAD, occupancy A/B)
@@ -178,7 +179,7 @@ constexpr uint32_t DDS_ENV_LDS_MAX = 8192;   // words: tables up to 32 KiB are s
 constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;  // words: 128 freq entries
 
 // dynamic LDS bytes of dds_chunk_kernel
-inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_lds)
+__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_lds)
 {
     return 4096 * 2 + ev_lds * 18 + (env_lds + freq_lds) * 4;
 }
@@ -199,6 +200,8 @@ constexpr uint32_t DDS_SEG_FLAG = 0x100;        // descriptor word 1: channel ru
 constexpr uint32_t DDS_SEG_CHUNK = 1u << 15;    // samples per sub-chunk (group table) on the segment path
 constexpr uint32_t DDS_SEG_ENV_MAX = 4096;      // staged env words (pairs counted) on the segment path
 
+// the event index (p.xs; the synthesis kernels of launch_dds read it)
+hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream);
 // p: chunk-kernel parameters; ps: segment-kernel parameters (same buffers)
 hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, bool any_chunk, hipStream_t stream);
 

@@ -27,7 +27,7 @@ import sys
 # summary key -> kernel-name substrings (the interpreter is interp_kernel or, for
 # branch-free programs, straight_kernel)
 KERNELS = {'interp': ('interp_kernel', 'straight_kernel'), 'dds': ('dds_kernel', 'dds_chunk_kernel'),
-           'hist_reduce': ('hist_reduce_kernel',)}
+           'dds_index': ('dds_index_kernel',), 'hist_reduce': ('hist_reduce_kernel',)}
 
 
 # wave64 integer-VALU instructions per second, whole chip: the best rate of

@@ -27,7 +27,7 @@ def emu():
     e.close()
 
 
-def make_emu(rows, seg=1, index=1, yform=1, spt=8):
+def make_emu(rows, seg=1, index=1, yform=1, spt=4):
     """an Emulator whose DDS uses the segment kernel for eligible channels
     (seg=1) or the chunk kernel for all (seg=0), with `rows` quad rows per
     thread in the chunk kernel (0 = eight contiguous samples), fed by the
@@ -50,10 +50,10 @@ def make_emu(rows, seg=1, index=1, yform=1, spt=8):
                 os.environ[k] = v
 
 
-@pytest.fixture(scope='module', params=[(0, 0, 1, 1, 8), (0, 0, 1, 1, 4), (0, 1, 1, 1, 8), (0, 0, 1, 0, 8),
-                                        (2, 0, 1, 0, 8), (0, 1, 0, 1, 8), (0, 0, 0, 1, 8)],
+@pytest.fixture(scope='module', params=[(0, 0, 1, 1, 4), (0, 0, 1, 1, 8), (0, 1, 1, 1, 4), (0, 0, 1, 0, 4),
+                                        (2, 0, 1, 0, 4), (0, 1, 0, 1, 4), (0, 0, 0, 1, 4)],
                 ids=lambda r: ('seg' if r[1] else 'chunk_rows{}'.format(r[0])) + ('' if r[2] else '_noindex')
-                + ('' if r[3] or r[1] else '_xy') + ('_spt4' if r[4] == 4 else ''))
+                + ('' if r[3] or r[1] else '_xy') + ('_spt8' if r[4] == 8 else ''))
 def emu_path(request):
     e = make_emu(*request.param)
     yield e
