@@ -99,6 +99,20 @@ __device__ __forceinline__ Carrier carrier(const int16_t *lut, uint32_t theta, i
     return carrier_cs(lut[(idx + 1024) & 4095], lut[idx], amp);
 }
 
+// the Q15 table is exactly antisymmetric (sin[i + 2048] = -sin[i]: built from
+// the first quadrant, dpemu_dds_sin_lut), so the lean kernel stages half of it
+__device__ __forceinline__ int32_t lut_half(const int16_t *lut, uint32_t i)
+{
+    const int32_t v = lut[i & 2047u];
+    return (i & 2048u) ? -v : v;
+}
+
+__device__ __forceinline__ Carrier carrier_half(const int16_t *lut, uint32_t theta, int32_t amp)
+{
+    const uint32_t idx = theta >> 20;
+    return carrier_cs(lut_half(lut, (idx + 1024) & 4095), lut_half(lut, idx), amp);
+}
+
 // a = symsat((a0 (x) R_k + 2^14) >> 15)
 __device__ __forceinline__ Carrier rotate(Carrier a0, uint32_t rw)
 {
@@ -341,7 +355,7 @@ __device__ __forceinline__ void sweep_quad(const QuadArgs &q, uint32_t j_first)
 // or single words (E' formed per word), so a sample costs 2 dot2 + pack +
 // max for the rotation and 2 dot2 + pack for the mix.  Needs every staged
 // eq, rq != -32768 (the workgroup's tables; else the generic sweep runs).
-template <int SPT, bool PAIRS>
+template <int SPT, bool PAIRS, bool HALF>
 __device__ __forceinline__ void sweep_quad_y(const QuadArgs &q, uint32_t j_first)
 {
     const uint32_t k0 = j_first & (q.spc - 1);
@@ -402,7 +416,8 @@ __device__ __forceinline__ void sweep_quad_y(const QuadArgs &q, uint32_t j_first
         if (act && j0 - base < lim) {               // (a finished pulse plays zeros)
             const uint32_t t_ref = ri >= 0 ? q.rs_t[ri] : 0u;
             const uint32_t idx = (F0 * (n - t_ref) + ph15) >> 20;
-            const int32_t c = q.lut[(idx + 1024) & 4095], sn = q.lut[idx];
+            const int32_t c = HALF ? lut_half(q.lut, (idx + 1024) & 4095) : q.lut[(idx + 1024) & 4095];
+            const int32_t sn = HALF ? lut_half(q.lut, idx) : q.lut[idx];
             const uint32_t y0 = pack16((c * a16 + (1 << 15)) >> 16, (sn * a16 + (1 << 15)) >> 16);
             uint32_t E[SPT], Ep[SPT];
             const uint32_t d0 = j0 - base;
@@ -566,8 +581,10 @@ dds_chunk_kernel(const DDSParams p)
     // dynamic LDS (dds_lds_bytes): sine table | compacted strobes / resets |
     // staged env table | staged freq table
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    // (lean: half the sine table, dds_lds_bytes - 4096)
+    constexpr uint32_t LUT_BYTES = LEAN ? 4096 : 8192;
     int16_t *s_lut = reinterpret_cast<int16_t *>(s_dyn);
-    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn + 8192);
+    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn + LUT_BYTES);
     uint32_t *s_st_env = s_st_t + p.ev_lds;
     uint32_t *s_st_pf = s_st_env + p.ev_lds;
     uint32_t *s_rs_t = s_st_pf + p.ev_lds;
@@ -596,7 +613,7 @@ dds_chunk_kernel(const DDSParams p)
     // window, 11: none of them, 12: none and no index kernel
     const uint32_t pr = p.probe;
     if (pr != 8 && pr < 11)
-        for (uint32_t i = tid; i < 4096 / 8; i += BLOCK)
+        for (uint32_t i = tid; i < LUT_BYTES / 16; i += BLOCK)
             reinterpret_cast<uint4 *>(s_lut)[i] = reinterpret_cast<const uint4 *>(p.sin_lut)[i];
     bool bad = false;                       // a staged eq or rq is -32768: no Y form
     if (pr == 9 || pr >= 11) {
@@ -676,7 +693,7 @@ dds_chunk_kernel(const DDSParams p)
         // Scatter each strobe / reset to its cycle (strobe and reset times are
         // strictly increasing; only window entry 0 can precede the chunk), then
         // an inclusive max-scan of both halves at once (v_pk_max_u16).
-        s_cyc = reinterpret_cast<uint32_t *>(s_dyn + dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds));
+        s_cyc = reinterpret_cast<uint32_t *>(s_dyn + dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) - (8192 - LUT_BYTES));
         const uint32_t n_last = (c_end - 1) >> spc_sh;
         uint16_t *c16 = reinterpret_cast<uint16_t *>(s_cyc);
         reinterpret_cast<uint4 *>(s_cyc)[2 * tid] = make_uint4(0, 0, 0, 0);   // 8 entries per thread
@@ -721,15 +738,20 @@ dds_chunk_kernel(const DDSParams p)
         reinterpret_cast<uint4 *>(s_cyc)[2 * tid + 1] = make_uint4(e[4], e[5], e[6], e[7]);
         __syncthreads();
     }
+    if (LEAN && p.probe == 13) {            // probe (A/B only): the lean kernel's prologue + zero stores
+        const uint32_t z[4] = {0, 0, 0, (uint32_t)(n_st + n_rs) & 0u};
+        for (uint32_t j0 = c_begin + 4 * tid; j0 < c_end; j0 += 4 * BLOCK) store4(out, j0, c_end, z);
+        return;
+    }
     if (quad && (LEAN || yf) && !bad) {
         const QuadArgs q{s_lut, s_st_t, s_st_env, s_st_pf, s_st_amp, s_rs_t, n_st, n_rs, spc, spc_sh, interp, int_sh,
                          s_env, env_len, s_freq, freq_len, out, c_end, s_cyc, n_c0};
         if (LSPT != 4 && (spc & 7u) == 0) {
-            if (interp == 1) sweep_quad_y<8, true>(q, c_begin + 8 * tid);
-            else sweep_quad_y<8, false>(q, c_begin + 8 * tid);
+            if (interp == 1) sweep_quad_y<8, true, LEAN>(q, c_begin + 8 * tid);
+            else sweep_quad_y<8, false, LEAN>(q, c_begin + 8 * tid);
         } else {
-            if (interp == 1) sweep_quad_y<4, true>(q, c_begin + 4 * tid);
-            else sweep_quad_y<4, false>(q, c_begin + 4 * tid);
+            if (interp == 1) sweep_quad_y<4, true, LEAN>(q, c_begin + 4 * tid);
+            else sweep_quad_y<4, false, LEAN>(q, c_begin + 4 * tid);
         }
         return;
     }
@@ -773,7 +795,8 @@ dds_chunk_kernel(const DDSParams p)
                 if ((!L || es < 4 * L) && widx < env_len && 16 * fi + 15 < freq_len) {
                     const uint32_t *fr = p.freq + freq_off + 16 * fi;
                     const uint32_t t_ref = ri >= 0 ? s_rs_t[ri] : 0u;
-                    const Carrier a0 = carrier(s_lut, fr[0] * (n - t_ref) + (phase << 15), s_st_amp[si]);
+                    const Carrier a0 = LEAN ? carrier_half(s_lut, fr[0] * (n - t_ref) + (phase << 15), s_st_amp[si])
+                                            : carrier(s_lut, fr[0] * (n - t_ref) + (phase << 15), s_st_amp[si]);
                     o = mix(p.env[env_off + widx], k ? rotate(a0, fr[k]) : a0);
                 }
             }
@@ -1168,9 +1191,9 @@ hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, boo
     }
     if (any_chunk) {
         const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
-        const bool lean = p.xs && p.yform && !p.rows && !p.probe;
+        const bool lean = p.xs && p.yform && !p.rows && (!p.probe || p.probe == 13);
         // lean SPT-8 kernel: + the cycle table (chunk / 8 u32 entries, 8 per thread)
-        const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) + p.lds_pad +
+        const uint32_t lds = dds_lds_bytes(p.ev_lds, p.env_lds, p.freq_lds) + p.lds_pad - (lean ? 4096u : 0u) +
                              (lean && p.spt != 4 && p.cyc ? 32 * BLOCK : 0u);
         const void *fn = !lean ? reinterpret_cast<const void *>(dds_chunk_kernel<0>)
                          : p.spt == 4 ? reinterpret_cast<const void *>(dds_chunk_kernel<4>)

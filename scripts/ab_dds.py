@@ -22,12 +22,11 @@ elems = tuple(int(c) for c in (sys.argv[4] if len(sys.argv) > 4 else '01'))
 ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
 ctx = {}
 VARIANTS = [  # name, env knobs (read once, at dpemu_create)
-    ('lean4_c16k', {'DPEMU_DDS_SPT': '4'}),
-    ('lean4_c8k', {'DPEMU_DDS_SPT': '4', 'DPEMU_DDS_CHUNK': '8192'}),
-    ('lean4_c32k', {'DPEMU_DDS_SPT': '4', 'DPEMU_DDS_CHUNK': '32768'}),
-    ('lean4_c24k', {'DPEMU_DDS_SPT': '4', 'DPEMU_DDS_CHUNK': '24576'}),
+    ('lean4_c16k', {}),
+    ('probe_lean4_c16k', {'DPEMU_DDS_PROBE': '13'}),
+    ('lean4_c8k', {'DPEMU_DDS_CHUNK': '8192'}),
     ('lean8_c16k_walk', {'DPEMU_DDS_SPT': '8', 'DPEMU_DDS_CYC': '0'}),
-    ('lean4_c16k_b', {'DPEMU_DDS_SPT': '4'}),
+    ('lean4_c16k_b', {}),
 ]
 KNOBS = ('DPEMU_DDS_CYC', 'DPEMU_DDS_SPT', 'DPEMU_DDS_YFORM', 'DPEMU_DDS_INDEX', 'DPEMU_DDS_SEG', 'DPEMU_DDS_SEG_CHUNK', 'DPEMU_DDS_SEG_PER_CU', 'DPEMU_DDS_PROBE', 'DPEMU_DDS_ROWS', 'DPEMU_DDS_CHUNK')
 for name, knobs in VARIANTS:
