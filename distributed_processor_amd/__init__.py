@@ -6,6 +6,6 @@ distproc programs on hand-written CDNA4 HIP kernels through the C ABI in
 ``include/dpemu.h``.
 """
 
-from . import isa, hwconfig  # noqa: F401
+from . import isa, hwconfig, lint  # noqa: F401
 
-__all__ = ['isa', 'hwconfig']
+__all__ = ['isa', 'hwconfig', 'lint']
