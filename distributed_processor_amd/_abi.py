@@ -4,13 +4,14 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_CORES = 64
 MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
 
 ST_DONE, ST_MAX_CYCLES, ST_HUNG_OPCODE, ST_DEADLOCK = 1, 2, 3, 4
 F_LATE, F_EVENT_OVF, F_TRACE_OVF, F_MEAS_OVF, F_DOUBLE_STROBE, F_GUARD = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 FPROC_MEAS, FPROC_LUT = 0, 1
+MEAS_STATE, MEAS_READOUT = 0, 1
 EV_STROBE, EV_PULSE_RESET = 0, 1
 TRACE_QCLK_LOAD, TRACE_QCLK_RST = 16, 17
 MAX_CYCLES_LIMIT = 2 ** 31 - 64
@@ -32,8 +33,10 @@ class Config(C.Structure):
                 ('fproc_mode', C.c_uint32), ('meas_elem', C.c_uint32), ('meas_latency', C.c_uint32),
                 ('sync_latency', C.c_uint32), ('exec_flags', C.c_uint32),
                 ('sync_mask', C.c_uint64), ('seed', C.c_uint64),
-                ('lut_mask', C.c_uint32), ('reserved1', C.c_uint32),
-                ('p1_threshold', C.c_uint32 * MAX_CORES), ('lut_table', C.c_uint64 * 256)]
+                ('lut_mask', C.c_uint32), ('meas_model', C.c_uint32),
+                ('p1_threshold', C.c_uint32 * MAX_CORES), ('lut_table', C.c_uint64 * 256),
+                ('ro_sep', C.c_int32), ('ro_sigma', C.c_uint32), ('ro_thr', C.c_int32),
+                ('reserved2', C.c_uint32)]
 
 
 class Outputs(C.Structure):
@@ -54,8 +57,10 @@ DEFAULT_LUT_TABLE = (0b00000, 0b00100, 0b10000, 0b01000)   # meas_lut.sv:17-20
 def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 20,
                 event_cap=64, trace_cap=0, meas_cap=8, fproc_mode=FPROC_MEAS, meas_elem=2,
                 meas_latency=64, sync_latency=1, sync_mask=0, seed=0x5EED, p1=0.5,
-                lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE, exec_flags=0):
-    """Validated Config.  p1: float or per-core list of P(meas = 1)."""
+                lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE, exec_flags=0, readout=None):
+    """Validated Config.  p1: float or per-core list of P(state = 1).
+    readout: None (outcome = prepared state) or dict(sep=, sigma=, thr=) for the
+    readout model of include/dpemu.h (sigma a float noise scale, stored Q16)."""
     C_ = int(cores_per_shot)
     if C_ < 1 or C_ > MAX_CORES or (C_ & (C_ - 1)):
         raise ValueError('cores_per_shot must be a power of two in [1, 64]')
@@ -88,6 +93,13 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
         cfg.p1_threshold[c] = prob_to_threshold(p)
     for i, v in enumerate(lut_table):
         cfg.lut_table[i] = int(v)
+    if readout is not None:
+        sep, thr = int(readout.get('sep', 0)), int(readout.get('thr', 0))
+        sigma = int(round(float(readout.get('sigma', 0.0)) * 65536))
+        if not (-2 ** 31 <= sep < 2 ** 31 and -2 ** 31 <= thr < 2 ** 31 and 0 <= sigma < 2 ** 32):
+            raise ValueError('readout sep / thr must fit int32 and sigma * 2^16 uint32')
+        cfg.meas_model = MEAS_READOUT
+        cfg.ro_sep, cfg.ro_sigma, cfg.ro_thr = sep, sigma, thr
     return cfg
 
 

@@ -295,6 +295,8 @@ static int validate(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t n_shots, b
     if (cfg->meas_latency < 1 || cfg->meas_latency > (1u << 20) || cfg->sync_latency < 1 ||
         cfg->sync_latency > (1u << 20))
         return fail(ctx, DPEMU_E_INVALID, "meas_latency / sync_latency must be in [1, 2^20]");
+    if (cfg->meas_model != DPEMU_MEAS_STATE && cfg->meas_model != DPEMU_MEAS_READOUT)
+        return fail(ctx, DPEMU_E_INVALID, "meas_model must be DPEMU_MEAS_STATE or DPEMU_MEAS_READOUT");
     if ((uint64_t)cfg->max_cycles + cfg->meas_latency + 16 >= 0x80000000ull)
         return fail(ctx, DPEMU_E_INVALID, "max_cycles + meas_latency must stay below 2^31");
     if (cfg->meas_cap > 32) return fail(ctx, DPEMU_E_INVALID, "meas_cap > 32");
@@ -354,6 +356,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     const uint64_t all = (C >= 64) ? ~0ull : ((1ull << C) - 1);
     p.sync_mask = cfg->sync_mask ? (cfg->sync_mask & all) : all;
     p.seed = cfg->seed;
+    p.meas_model = cfg->meas_model; p.ro_sep = cfg->ro_sep; p.ro_thr = cfg->ro_thr; p.ro_sigma = cfg->ro_sigma;
     p.lut_mask = cfg->lut_mask;
     const uint64_t guard = (uint64_t)C * (cfg->max_cycles / 3u + 4u) + 1024u;
     p.iter_guard = guard > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)guard;

@@ -38,8 +38,8 @@ __device__ __forceinline__ uint32_t event_word(uint32_t pe, uint32_t kind)
     return (pe & 0x0FFFFFFFu) | (kind << 28);
 }
 
-// Philox4x32-10, output word 0 (counter = shot_lo, shot_hi, core, m; key = seed)
-__device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m)
+// Philox4x32-10, output words 0..2 (counter = shot_lo, shot_hi, core, m; key = seed)
+__device__ __forceinline__ uint3 philox3(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m)
 {
     uint32_t c0 = (uint32_t)shot, c1 = (uint32_t)(shot >> 32), c2 = core, c3 = m;
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -51,7 +51,23 @@ __device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t shot, uin
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
-    return c0;
+    return make_uint3(c0, c1, c2);
+}
+
+// measurement outcome (oracle/philox.c oracle_meas_bit; include/dpemu.h): the
+// prepared state against thr, or with meas_model READOUT the discriminated
+// readout x = +-(ro_sep * amp >> 16) + (z * ro_sigma >> 16) > ro_thr, z the
+// centred Irwin-Hall(4) sum of the 16-bit halves of Philox words 1 and 2
+__device__ __forceinline__ uint32_t meas_bit(const KParams &p, uint64_t shot, uint32_t core, uint32_t m,
+                                             uint32_t thr, uint32_t amp)
+{
+    const uint3 r = philox3(p.seed, shot, core, m);
+    const uint32_t state = (thr == 0xFFFFFFFFu) || (r.x < thr);
+    if (p.meas_model != DPEMU_MEAS_READOUT) return state;
+    const int64_t z = (int64_t)((r.y & 0xFFFFu) + (r.y >> 16) + (r.z & 0xFFFFu) + (r.z >> 16)) - 131070;
+    const int64_t s = ((int64_t)p.ro_sep * (int64_t)(amp & 0xFFFFu)) >> 16;
+    const int64_t x = (state ? s : -s) + ((z * (int64_t)p.ro_sigma) >> 16);
+    return x > (int64_t)p.ro_thr;
 }
 
 __device__ __forceinline__ uint64_t group_bits(uint64_t ballot, uint32_t lane_in_wave, uint32_t C)

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DPEMU_ABI_VERSION 1
+#define DPEMU_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------- */
 #define DPEMU_OK            0
@@ -104,10 +104,22 @@ typedef struct dpemu_config {
     uint64_t sync_mask;        /* participant cores (bit c); 0 = all C cores             */
     uint64_t seed;             /* Philox4x32-10 key                                      */
     uint32_t lut_mask;         /* meas_lut mask (nonzero), meas_lut.sv:16                */
-    uint32_t reserved1;
-    uint32_t p1_threshold[DPEMU_MAX_CORES]; /* P(meas=1) = thr/2^32; 0xFFFFFFFF = always 1 */
+    uint32_t meas_model;       /* DPEMU_MEAS_STATE: outcome = prepared state; DPEMU_MEAS_READOUT:
+                                  the discriminated readout signal (ro_* below)            */
+    uint32_t p1_threshold[DPEMU_MAX_CORES]; /* P(state=1) = thr/2^32; 0xFFFFFFFF = always 1 */
     uint64_t lut_table[256];   /* meas_lut table: lut_out = table[addr], bit c -> core c */
+    /* readout model (meas_model = DPEMU_MEAS_READOUT), per readout strobe with amp word A:
+     *   z = Irwin-Hall(4) of the 16-bit halves of Philox words 1, 2, minus 131070
+     *   x = (state ? +1 : -1) * ((ro_sep * A) >> 16) + ((z * ro_sigma) >> 16)   (int64)
+     *   outcome = x > ro_thr                                                       */
+    int32_t  ro_sep;           /* half the state separation at full readout amplitude    */
+    uint32_t ro_sigma;         /* noise scale, Q16 (noise sigma = ro_sigma / 2^16 * 37837.6) */
+    int32_t  ro_thr;           /* discriminator threshold                                */
+    uint32_t reserved2;
 } dpemu_config;
+
+#define DPEMU_MEAS_STATE   0
+#define DPEMU_MEAS_READOUT 1
 
 /*
  * Per-lane summary, 8 x u32:

@@ -25,6 +25,12 @@ extern "C" {
 uint32_t oracle_alu(uint32_t ctrl, uint32_t in0, uint32_t in1);
 void oracle_pulse_reg(uint32_t pr[5], const uint32_t lc[4], uint32_t reg_in, int write_en);
 uint32_t oracle_philox_u32(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m);
+void oracle_philox4(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m, uint32_t out[4]);
+/* outcome of measurement m of (shot, core): the prepared state drawn against
+ * thr, or (meas_model READOUT) the discriminated readout of a pulse with amp
+ * word `amp` (include/dpemu.h, dpemu_config) */
+uint32_t oracle_meas_bit(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m, uint32_t thr, uint32_t amp,
+                         uint32_t meas_model, int32_t ro_sep, uint32_t ro_sigma, int32_t ro_thr);
 
 /* ---- per-clock model ---------------------------------------------------- */
 typedef struct {
@@ -75,6 +81,10 @@ typedef struct {
     uint32_t lut_mask;
     uint32_t p1_threshold[DPEMU_MAX_CORES];
     uint64_t lut_table[256];
+    uint32_t meas_model;
+    int32_t ro_sep;
+    uint32_t ro_sigma;
+    int32_t ro_thr;
 } oracle_shot_cfg;
 
 #define RTL_MQ 64

@@ -370,9 +370,8 @@ void rtl_shot_step(rtl_shot *s, const rtl_ext_inputs *ext)
         const rtl_core_comb *o = &s->core[c].comb;
         if (o->cstrobe && s->cfg.meas_elem != 0xFF && (o->cfg & 3) == s->cfg.meas_elem) {
             uint32_t m = s->n_meas[c]++;
-            uint32_t r = oracle_philox_u32(s->cfg.seed, s->shot, c, m);
-            uint32_t thr = s->cfg.p1_threshold[c];
-            int bit = (thr == 0xFFFFFFFFu) || (r < thr);
+            int bit = (int)oracle_meas_bit(s->cfg.seed, s->shot, c, m, s->cfg.p1_threshold[c], o->amp,
+                                           s->cfg.meas_model, s->cfg.ro_sep, s->cfg.ro_sigma, s->cfg.ro_thr);
             rtl_meas_q *q = &s->mq[c];
             q->t[q->tail % RTL_MQ] = s->cycle + s->cfg.meas_latency;
             q->bit[q->tail % RTL_MQ] = (uint8_t)bit;

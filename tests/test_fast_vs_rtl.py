@@ -19,13 +19,13 @@ HORIZON = 6000
 EV_CAP, TR_CAP, MEAS_CAP = 128, 128, 16
 
 
-def run_both(case, n_shots=4, seed=0x5EED, meas_latency=20, sync_latency=1, sync_mask=0, shot0=0):
+def run_both(case, n_shots=4, seed=0x5EED, meas_latency=20, sync_latency=1, sync_mask=0, shot0=0, readout=None):
     C = case['ncores']
     mode = _abi.FPROC_MEAS if case['mode'] == 'meas' else _abi.FPROC_LUT
     cfg = _abi.make_config(C, n_groups=case['n_groups'], shots_per_group=1, max_cycles=HORIZON,
                            event_cap=EV_CAP, trace_cap=TR_CAP, meas_cap=MEAS_CAP, fproc_mode=mode,
                            meas_latency=meas_latency, sync_latency=sync_latency, sync_mask=sync_mask,
-                           seed=seed, p1=0.5)
+                           seed=seed, p1=0.5, readout=readout)
     words, offs, ni = pack_programs(case['progs'])
     fast = oracle.fast_run(cfg, words, offs, ni, case['table'], shot0, n_shots)
     scfg = oracle.shot_cfg_from_config(cfg)
@@ -129,3 +129,14 @@ def test_fuzz_partial_sync_mask(seed):
     case = random_case(3000 + seed, ncores=4, mode='meas', allow_late=False, allow_hang=False)
     cfg, fast, rtl = run_both(case, n_shots=2, sync_mask=0b0111, sync_latency=1 + seed % 4)
     compare(cfg, fast, rtl, 2)
+
+
+@pytest.mark.parametrize('seed', range(16))
+def test_fuzz_readout_model(seed):
+    """meas_model READOUT (include/dpemu.h): outcomes from the discriminated
+    readout of each strobe's amp word, driving fproc branches in both models"""
+    case = random_case(4000 + seed, ncores=[1, 2, 4][seed % 3], mode=['meas', 'lut'][seed % 2],
+                       allow_late=False, allow_hang=False)
+    ro = dict(sep=[40000, 5000, -30000, 0][seed % 4], sigma=[0.5, 1.0, 0.1, 2.0][seed % 4], thr=[0, 1000, -500][seed % 3])
+    cfg, fast, rtl = run_both(case, n_shots=3, meas_latency=1 + seed % 9, readout=ro)
+    compare(cfg, fast, rtl, 3)

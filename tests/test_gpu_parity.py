@@ -213,6 +213,36 @@ def test_config3_active_reset(emu):
     assert 0.45 < flip.mean() < 0.55
 
 
+def test_config3_active_reset_readout_model(emu):
+    """config 3 with meas_model READOUT: reset branches follow the discriminated
+    readout (state + noise) instead of the state; GPU = oracle_fast bit for bit"""
+    ps = ProgramSet(workloads.config3_active_reset(8))
+    cfg = _abi.make_config(8, max_cycles=50000, event_cap=16, trace_cap=16, meas_cap=4,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, p1=0.2,
+                           readout=dict(sep=30000, sigma=0.6, thr=2000))
+    g, f = run_pair(emu, ps, cfg, 4000, shot0=7 * 10 ** 8)
+    compare_all(g, f)
+    s = _abi.unpack_summary(g['summary'])
+    assert (s['status'] == _abi.ST_DONE).all()
+
+
+@pytest.mark.parametrize('seed', range(12))
+def test_fuzz_readout_model(emu, seed):
+    """fuzzed programs (fproc branches on readout outcomes, meas and LUT modes)
+    under meas_model READOUT, on both interpreter kernels"""
+    C = [1, 2, 4, 8][seed % 4]
+    case = random_case(5000 + seed, ncores=C, mode=['meas', 'lut'][seed % 2], straight=seed % 3 == 2)
+    mode = _abi.FPROC_MEAS if case['mode'] == 'meas' else _abi.FPROC_LUT
+    groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
+    ps = ProgramSet(groups, cores_per_shot=C)
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=6000, event_cap=64, trace_cap=64, meas_cap=16,
+                           fproc_mode=mode, meas_latency=1 + seed % 13, seed=seed, p1=0.4,
+                           readout=dict(sep=[25000, -8000, 60000][seed % 3], sigma=[0.7, 1.5, 0.2][seed % 3],
+                                        thr=[0, -1500, 900][seed % 3]))
+    g, f = run_pair(emu, ps, cfg, 257, shot0=seed * 977)
+    compare_all(g, f, 'readout seed {}'.format(seed))
+
+
 def test_config4_rb(emu):
     ps = ProgramSet(workloads.config4_rb(n_seq=24, depth=40))
     cfg = _abi.make_config(2, n_groups=24, shots_per_group=5, max_cycles=200000, event_cap=160,
