@@ -193,7 +193,10 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
-        dist.init_process_group('nccl')
+        # RCCL; DPEMU_BENCH_BACKEND=gloo rehearses the multi-rank path with
+        # several ranks on fewer GPUs (never for measurement)
+        dist.init_process_group(os.environ.get('DPEMU_BENCH_BACKEND', 'nccl'))
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
 
     from distributed_processor_amd import _abi, sharding
@@ -210,14 +213,32 @@ def main():
     out = alloc_device_outputs(cfg, n, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'))
     stream = torch.cuda.current_stream()
     shot0, n = sharding.weak_shard(n, rank)
+    # double-buffered histogram: batch k's all-reduce (the path's only exchange,
+    # RCCL) runs on RCCL's stream while batch k+1's kernel runs
+    hists = [out['hist'], torch.zeros_like(out['hist'])]
+    pending = [None, None]
+    n_steps = [0]
 
     def step():
+        b = n_steps[0] % 2
+        n_steps[0] += 1
+        if pending[b] is not None:
+            pending[b].wait()                          # this buffer's previous exchange is done
+            pending[b] = None
+        out['hist'] = hists[b]
         out['hist'].zero_()
         emu.run_device(cfg, n, shot0, out, stream)
-        sharding.allreduce_histogram(out['hist'])     # the path's only exchange (RCCL)
+        pending[b] = sharding.allreduce_histogram(out['hist'], async_op=True)
+
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
 
     emu.kernel_timing(True)                           # HIP events around the interpreter kernel
@@ -227,6 +248,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

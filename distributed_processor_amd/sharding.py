@@ -52,16 +52,22 @@ def world_size(group=None) -> int:
     return dist.get_world_size(group) if dist is not None else 1
 
 
-def allreduce_histogram(hist, group=None):
+def allreduce_histogram(hist, group=None, async_op=False):
     """Sum the int64 outcome histogram over ranks, in place (no-op on one
-    rank).  ``hist``: torch.int64 tensor on the backend's device."""
+    rank).  ``hist``: torch.int64 tensor on the backend's device.  With
+    ``async_op`` the collective is only enqueued (on RCCL's stream, after the
+    work already queued on the current stream) and its work handle returned
+    (None on one rank): ``handle.wait()`` orders later work on the current
+    stream after it, so the exchange of one batch overlaps the next batch's
+    kernel."""
     import torch
     if hist.dtype != torch.int64:
         raise TypeError('histogram must be int64, got {}'.format(hist.dtype))
     if world_size(group) > 1:
         dist = _dist()
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
-    return hist
+        work = dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        return work if async_op else hist
+    return None if async_op else hist
 
 
 def gather_sample(t, group=None):

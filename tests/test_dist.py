@@ -49,7 +49,11 @@ def _rank_main(rank, world, port, out_dir):
         out = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, begin, n, threads=1,
                               want=('summary', 'hist'))
         hist = torch.from_numpy(out['hist'].astype(np.int64))
+        h2 = hist.clone()
+        work = sharding.allreduce_histogram(h2, async_op=True)     # the bench's overlapped form
         sharding.allreduce_histogram(hist)
+        work.wait()
+        assert torch.equal(h2, hist)
         lanes = sharding.sample_lanes(n, cfg.cores_per_shot, N_SAMPLE)
         sample = torch.from_numpy(out['summary'][lanes].astype(np.int64))
         gathered = sharding.gather_sample(sample)
@@ -89,6 +93,7 @@ def test_sample_lanes_whole_shots():
 def test_single_rank_collectives_are_identity():
     h = torch.arange(6, dtype=torch.int64)
     assert sharding.allreduce_histogram(h) is h and h.tolist() == list(range(6))
+    assert sharding.allreduce_histogram(h, async_op=True) is None        # one rank: nothing to wait for
     assert sharding.gather_sample(h).shape == (1, 6)
     assert sharding.max_over_ranks(2.5) == 2.5
     with pytest.raises(TypeError):
