@@ -8,6 +8,9 @@ timeline, lane summaries, measurement records and the outcome histogram to
 HBM; with N > 1 ranks the histograms are all-reduced over RCCL (the path's
 only exchange).  Shots shard by global index (weak scaling).
 
+Active-reset leg (config 3, under "active_reset"): fproc_meas branching and
+sync barriers on the general interpreter kernel, 1.25*10^6 shots per GPU.
+
 DDS leg (config 5, reported under "dds" on the same line): the config-4 RB
 timelines (8 cores, depth 200) synthesised to int16 I/Q on 16 channels per
 sequence at 16 samples/clk; GSamples/s (whole job) and the DDS kernel's HBM
@@ -171,6 +174,82 @@ def dds_leg(emu, args, world, rank, stream):
     return res
 
 
+def active_reset_leg(emu, args, world, rank, stream):
+    """config 3 (BASELINE configs[2]): 8-core active reset -- readout, fproc_meas
+    branch to a conditional X180, sync barriers -- 10^7 shots per step over 8
+    GPUs, i.e. 1.25*10^6 shots per GPU (weak).  Runs on the general
+    interpreter kernel (fproc + sync).  Returns the 'active_reset' sub-object."""
+    import torch
+    from distributed_processor_amd import _abi, sharding, workloads
+    from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
+    ps = ProgramSet(workloads.config3_active_reset(8))
+    emu.load(ps)
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5)
+    n_per = args.ar_shots
+    out = alloc_device_outputs(cfg, n_per, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'))
+    shot0, n = sharding.weak_shard(n_per, rank)
+
+    def step():
+        out['hist'].zero_()
+        emu.run_device(cfg, n, shot0, out, stream)
+        sharding.allreduce_histogram(out['hist'])
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    emu.kernel_times()
+    emu.kernel_timing(True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
+    emu.kernel_timing(False)
+    kt = emu.kernel_times()
+    kernel_ms = float(np.mean(kt))
+    summ = out['summary'].cpu().numpy().view(np.uint32)
+    s = _abi.unpack_summary(summ)
+    assert (s['status'] == _abi.ST_DONE).all(), 'config 3: not every lane reached DONE'
+    assert int(out['hist'].sum().item()) == n * world
+    alg = float(bytes_per_lane(summ, cfg).sum())
+    gbs = alg / (kernel_ms * 1e-3) / 1e9
+    res = {'metric': 'emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
+                     '1.25e6 shots/GPU)',
+           'value': n * 8 * world * args.steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * args.steps / dt,
+           'ms_per_step': dt / args.steps * 1e3, 'kernel_ms': kernel_ms, 'kernel': 'dpemu::' + emu.last_kernel(),
+           'instructions_per_s': float(s['n_instr'].astype(np.float64).sum()) * world * args.steps / dt,
+           'config': {'workload': 'config3_active_reset_8core', 'shots_per_gpu': n,
+                      'global_shots_per_step': n * world},
+           'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                        'frac': gbs / HBM_PEAK_GBS, 'bytes_per_launch': alg}}
+    pmc = os.path.join(REPO, 'profiles', PROFILE_TAG + '_active_reset_pmc.json')
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            prof = json.load(f)
+        res['roofline']['traffic'] = prof.get('hbm_bytes_per_launch')
+        res['roofline']['valu'] = {k: prof.get(k) for k in ('valu_insts_per_wave', 'valu_issue_pct',
+                                                            'valu_lane_util_pct', 'duration_ns', 'kernel')}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        threads = min(len(os.sched_getaffinity(0)), 16)
+        want = ('summary', 'ev_main', 'ev_amp', 'meas', 'hist')
+        done, chunk, t0 = 0, 20000, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds / 3:
+            oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, done, chunk, threads, want)
+            done += chunk
+        dtc = time.perf_counter() - t0
+        res['cpu_baseline'] = {'value': done * 8 / dtc, 'unit': 'core-shots/s', 'cores': threads, 'kind': 'port',
+                               'sample': '{} shots x 8 cores of config 3, oracle_fast (OpenMP), {:.1f} s'.format(
+                                   done, dtc)}
+    del out
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -184,6 +263,7 @@ def main():
     ap.add_argument('--exec-flags', type=int, default=0, help='DPEMU_X_* execution knobs')
     ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
     ap.add_argument('--no-dds', action='store_true')
+    ap.add_argument('--ar-shots', type=int, default=1250000, help='config-3 shots per GPU per step (0: skip the leg)')
     args = ap.parse_args()
 
     import torch
@@ -316,6 +396,8 @@ def main():
         result['cpu_baseline'] = cpu_baseline(ps, cfg, args.cpu_seconds)
     if not args.no_dds:
         result['dds'] = dds_leg(emu, args, world, rank, stream)
+    if args.ar_shots > 0:
+        result['active_reset'] = active_reset_leg(emu, args, world, rank, stream)
     if rank == 0:
         print(json.dumps(result), flush=True)
     emu.close()

@@ -24,9 +24,9 @@ import json
 import os
 import sys
 
-# summary key -> kernel-name substrings (the interpreter is interp_kernel or, for
-# branch-free programs, straight_kernel)
-KERNELS = {'interp': ('interp_kernel', 'straight_kernel'), 'dds': ('dds_kernel', 'dds_chunk_kernel'),
+# summary key -> kernel-name substrings: the bench's config 2 runs on
+# straight_kernel (branch-free programs), config 3 on the general interp_kernel
+KERNELS = {'interp': ('straight_kernel',), 'active_reset': ('interp_kernel',), 'dds': ('dds_kernel', 'dds_chunk_kernel'),
            'dds_index': ('dds_index_kernel',), 'hist_reduce': ('hist_reduce_kernel',)}
 
 
