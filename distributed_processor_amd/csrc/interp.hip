@@ -224,7 +224,12 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         bool any_run_grp = true;
         bool released = false;
         if constexpr (SYNC || XMEAS) {
+            // wave-uniform guards: gmin only matters to a pending fproc_meas read (or the
+            // LUT leader), the barrier only while some lane waits in SYNC -- most iterations
+            // of a branching program skip both group reductions
+            const bool need_g = LUT || __any(is_fproc);
             if constexpr (SYNC) {
+              if (need_g || __any(mode == M_SYNC)) {
                 // barrier: complete when every participant is in SYNC_WAIT
                 const uint32_t key = is_part ? ((mode == M_SYNC) ? wait_d : (mode == M_RUN) ? t
                                              : (mode == M_LUT) ? wait_d + 5u : INF32) : 0u;
@@ -246,13 +251,16 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                     released = true;
                 }
                 // strobe bound of a waiting participant
-                uint32_t bound = INF32;
-                if (mode == M_RUN) bound = t + 2u;
-                else if (mode == M_LUT) bound = wait_d + 7u;
-                else if (mode == M_SYNC && is_part && maxkey != INF32)
-                    bound = maxkey + p.sync_latency + 5u;
-                gmin = group_reduce<0>(bound, C);
-            } else {
+                if (need_g) {
+                    uint32_t bound = INF32;
+                    if (mode == M_RUN) bound = t + 2u;
+                    else if (mode == M_LUT) bound = wait_d + 7u;
+                    else if (mode == M_SYNC && is_part && maxkey != INF32)
+                        bound = maxkey + p.sync_latency + 5u;
+                    gmin = group_reduce<0>(bound, C);
+                }
+              }
+            } else if (need_g) {
                 const uint32_t bound = (mode == M_RUN) ? t + 2u : (mode == M_LUT) ? wait_d + 7u : INF32;
                 gmin = group_reduce<0>(bound, C);
             }
