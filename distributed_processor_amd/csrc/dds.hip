@@ -6,7 +6,7 @@
 // formats).  HBM-write-bound by design: 4 B per output sample.
 //
 // Two launches per synthesis:
-//   * dds_index_kernel (one workgroup per channel) compacts the lane's strobes
+//   * dds_index_kernel (one wave per channel) compacts the lane's strobes
 //     of the channel's element and its pulse_resets (time-sorted: a core emits
 //     them in time order) once, channel-contiguous, plus each chunk's window;
 //   * dds_chunk_kernel, grid (sample chunks, channels).  A workgroup loads its
@@ -806,40 +806,73 @@ dds_chunk_kernel(const DDSParams p)
     }
 }
 
-// Event index of the chunk path: one workgroup per channel compacts the
+// Event index of the chunk path: one wave per channel compacts the
 // lane's strobes of the channel's element and its pulse_resets once (instead
 // of once per chunk: the slot-major event loads are one 16-B line access per
 // event), writes them channel-contiguous, and for every chunk the window of
 // strobes / resets its sweep can see: from the latest one at or before the
 // chunk's first cycle to the latest one at or before its last cycle.  The
 // chunk kernel then loads only its window, coalesced.
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) dds_index_kernel(const DDSParams p)
+__global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
 {
+    // one wave per channel, BLOCK / 64 channels per workgroup, no workgroup
+    // barrier: each lane issues all its event loads (8 per lane cover 512
+    // events) before the wave compacts them with ballot / popc straight into
+    // the global index; the strobe / reset times also go to the wave's LDS
+    // slice for the window searches
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn);
-    uint32_t *s_st_env = s_st_t + p.ev_lds;
-    uint32_t *s_st_pf = s_st_env + p.ev_lds;
-    uint32_t *s_rs_t = s_st_pf + p.ev_lds;
-    uint16_t *s_st_amp = reinterpret_cast<uint16_t *>(s_rs_t + p.ev_lds);
-    __shared__ uint32_t s_tmp[2 * (BLOCK / 64)];
-    __shared__ uint32_t s_cnt[2];
-
-    const uint32_t tid = threadIdx.x, ch = blockIdx.x;
+    const uint32_t wl = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t ch = blockIdx.x * (BLOCK / 64) + wv;
+    if (ch >= p.n_channels) return;                         // the whole wave
+    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn) + (uint64_t)wv * 2 * p.ev_lds;
+    uint32_t *s_rs_t = s_st_t + p.ev_lds;
     const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
     const uint32_t lane = d[0], elem = d[1] & 3u, spc = d[2];
-    int n_st, n_rs;
-    compact_events(
-        p, lane, elem,
-        [&](uint32_t i, const uint4 &ev, uint32_t amp) {
-            s_st_t[i] = ev.x; s_st_env[i] = ev.z & 0xFFFFFFu; s_st_pf[i] = ev.w; s_st_amp[i] = (uint16_t)amp;
-        },
-        s_rs_t, s_tmp, s_cnt, &n_st, &n_rs);
+    const uint32_t n_ev = min(p.summary[8ull * lane + 2], p.event_cap);
     uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
     uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
-    for (int i = (int)tid; i < n_st; i += BLOCK) xs[i] = make_uint4(s_st_t[i], s_st_env[i], s_st_pf[i], s_st_amp[i]);
-    for (int i = (int)tid; i < n_rs; i += BLOCK) xr[i] = s_rs_t[i];
+    const uint64_t below = wl ? (~0ull >> (64 - wl)) : 0ull;
+    uint32_t ns = 0, nr = 0;
+    constexpr int K = 8;
+    for (uint32_t e0 = 0; e0 < n_ev; e0 += 64 * K) {
+        uint4 ev[K];
+        uint32_t am[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint32_t e = e0 + 64 * k + wl;
+            ev[k] = make_uint4(0, 0, 0, 0);
+            am[k] = 0;
+            if (e < n_ev) {
+                ev[k] = p.ev_main[(uint64_t)e * p.n_lanes + lane];
+                am[k] = p.ev_amp[(uint64_t)e * p.n_lanes + lane];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint32_t e = e0 + 64 * k + wl;
+            const uint32_t kind = ev[k].z >> 28;
+            const bool is_st = e < n_ev && kind == 0u && ((ev[k].z >> 24) & 3u) == elem;
+            const bool is_rs = e < n_ev && kind == 1u;
+            const uint64_t bs = __ballot(is_st), br = __ballot(is_rs);
+            if (is_st) {
+                const uint32_t i = ns + (uint32_t)__popcll(bs & below);
+                xs[i] = make_uint4(ev[k].x, ev[k].z & 0xFFFFFFu, ev[k].w, am[k]);
+                s_st_t[i] = ev[k].x;
+            }
+            if (is_rs) {
+                const uint32_t i = nr + (uint32_t)__popcll(br & below);
+                xr[i] = ev[k].x;
+                s_rs_t[i] = ev[k].x;
+            }
+            ns += (uint32_t)__popcll(bs);
+            nr += (uint32_t)__popcll(br);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the wave's LDS writes before its reads
+    __builtin_amdgcn_wave_barrier();
+    const int n_st = (int)ns, n_rs = (int)nr;
     const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
-    for (uint32_t c = tid; c < chunks; c += BLOCK) {
+    for (uint32_t c = wl; c < chunks; c += 64) {
         const uint64_t c0 = (uint64_t)c * p.chunk, c1 = min(c0 + p.chunk, (uint64_t)p.n_samples) - 1;
         const uint32_t n0 = (uint32_t)(c0 / spc), n1 = (uint32_t)(c1 / spc);
         const int s0 = last_le(s_st_t, n_st, n0), s1 = last_le(s_st_t, n_st, n1);
@@ -1159,11 +1192,12 @@ static hipError_t opt_in_lds(const void *fn, uint32_t bytes, uint32_t *granted)
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples || !p.xs) return hipSuccess;
-    const uint32_t ilds = p.ev_lds * 18;
+    const uint32_t ilds = (BLOCK / 64) * 2 * p.ev_lds * 4;   // per wave: strobe and reset times
     static uint32_t granted = 0;
     const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_index_kernel), ilds, &granted);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), ilds, stream, p);
+    hipLaunchKernelGGL(dds_index_kernel, dim3((p.n_channels + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), ilds,
+                       stream, p);
     return hipGetLastError();
 }
 
