@@ -524,9 +524,11 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 
         // ---------------- deadlock: a shot with no progress can never progress ----------------
         if constexpr (SYNC || LUT) {
-            const uint64_t prog = __ballot(executed || released);
-            if (group_bits(prog, wl, C) == 0ull && (mode == M_SYNC || mode == M_LUT))
-                finish(ST_DEADLOCK, wait_d);
+            if (__any(mode == M_SYNC || mode == M_LUT)) {       // wave-uniform: only waiting lanes can deadlock
+                const uint64_t prog = __ballot(executed || released);
+                if (group_bits(prog, wl, C) == 0ull && (mode == M_SYNC || mode == M_LUT))
+                    finish(ST_DEADLOCK, wait_d);
+            }
         }
         if constexpr (FPROC || XMEAS) wave_fence();
     }
