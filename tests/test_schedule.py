@@ -1,0 +1,286 @@
+"""Scheduling restatement (distributed_processor_amd.schedule) vs the reference.
+
+Pinned by:
+* the scheduling asserts of the reference's ``test_compiler.py:75-98``
+  (``test_basic_schedule``) and its user-schedule lint verdicts (``:561-606``);
+* the compiler goldens ``test_linear_compile_out`` / ``test_pulse_compile_out``
+  (``test_compiler.py:100-122, 330-352``): gate-level program -> schedule ->
+  compile reproduces the golden pulse statements, and -> assemble reproduces
+  the reference GlobalAssembler's bytes (``tests/golden/asm_programs.json``);
+* a property: every straight-line schedule, assembled to machine code, runs
+  without a late pulse on the RTL latencies -- checked by the machine-code
+  linter, by ``oracle_fast`` and (``-m gpu``) by the emulator on cuda:0.
+The gate table is the Q0/Q1 part of the reference's ``qubitcfg.json``
+(``tests/golden/qchip_q01.json``, made by ``make_qchip_subset.py``).
+Control-flow cases (branch merge, loop ``delta_t``, hold -> idle) are
+hand-computed from ``ir/passes.py:616-735``: parity unpinned by a reference
+output, as the reference compiler is not importable here.
+"""
+
+import json
+import math
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from distributed_processor_amd import _abi, hwconfig as hw, isa, lint
+from distributed_processor_amd import assembler as am
+from distributed_processor_amd import schedule as sc
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+with open(os.path.join(GOLDEN, 'qchip_q01.json')) as f:
+    TABLE = sc.GateTable(json.load(f))
+# the fpga_config of test_compiler.py:77-81 (pulse_load_clks default 3)
+TEST_FPGA = hw.FPGAConfig(alu_instr_clks=2, fpga_clk_period=2.e-9, jump_cond_clks=3, jump_fproc_clks=4,
+                          pulse_regwrite_clks=1)
+
+
+def golden_inputs(name):
+    from tests.test_assembler import program
+    return program(name)
+
+
+def pulse_times(prog):
+    return [i.start_time for i in prog.blocks['block_0']['instructions'] if i.name == 'pulse']
+
+
+def scheduled_block(program, cfg=TEST_FPGA):
+    instrs = sc.resolve_freqs(sc.resolve_virtual_z(sc.resolve_gates(program, TABLE)), TABLE)
+    prog = sc.ScheduleIR({'block_0': instrs})
+    sc.Schedule(cfg).run_pass(prog)
+    return prog
+
+
+def test_basic_schedule():
+    """test_compiler.py:75-98"""
+    program = [{'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1']},
+               {'name': 'X90Z90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q0']},
+               {'name': 'X90', 'qubit': ['Q1']}, {'name': 'read', 'qubit': ['Q0']}]
+    assert pulse_times(scheduled_block(program))[:6] == [5, 5, 21, 37, 13, 53]
+
+
+def env_equal(a, b):
+    if isinstance(a, np.ndarray) or isinstance(b, np.ndarray):
+        return np.array_equal(np.asarray(a), np.asarray(b))
+    return a == b
+
+
+PULSE_PROGRAM = [{'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1']},
+                 {'name': 'X90Z90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q0']},
+                 {'name': 'X90', 'qubit': ['Q1']},
+                 {'name': 'pulse', 'phase': np.pi / 2, 'freq': 'Q0.freq', 'env': np.ones(100),
+                  'twidth': 24.e-9, 'amp': 0.5, 'dest': 'Q0.qdrv'},
+                 {'name': 'read', 'qubit': ['Q0']}]
+LINEAR_PROGRAM = [{'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1']},
+                  {'name': 'read', 'qubit': ['Q0']}]
+GOLDEN_CASES = {'test_linear_compile_out': LINEAR_PROGRAM, 'test_pulse_compile_out': PULSE_PROGRAM}
+
+
+@pytest.mark.parametrize('name', sorted(GOLDEN_CASES))
+def test_compile_matches_golden_statements(name):
+    """test_compiler.py:100-122 (pulse) and :330-352 (linear): the compiled
+    per-core statements equal the golden's, field by field"""
+    got = sc.compile_straight(GOLDEN_CASES[name], TABLE, TEST_FPGA).program
+    want = golden_inputs(name)
+    assert sorted(got) == sorted(want)
+    for grp, stmts in want.items():
+        g = got[grp]
+        assert [s['op'] for s in g] == [s['op'] for s in stmts], grp
+        for a, b in zip(g, stmts):
+            assert sorted(a) == sorted(b), (a, b)
+            for k in b:
+                if k == 'env':
+                    assert env_equal(a[k], b[k]), (grp, k)
+                elif isinstance(b[k], float):
+                    assert math.isclose(a[k], b[k], rel_tol=0, abs_tol=1e-12), (grp, k, a[k], b[k])
+                else:
+                    assert a[k] == b[k], (grp, k, a[k], b[k])
+
+
+@pytest.mark.parametrize('name', sorted(GOLDEN_CASES))
+def test_schedule_compile_assemble_bytes(name):
+    """gate program -> schedule -> compile -> assemble is byte-identical to the
+    reference GlobalAssembler on the golden (DDSElementConfig)"""
+    with open(os.path.join(GOLDEN, 'asm_programs.json')) as f:
+        exp = json.load(f)['programs'][name]['dds_elem']
+    compiled = sc.compile_straight(GOLDEN_CASES[name], TABLE, TEST_FPGA)
+    chans = hw.load_channel_configs(os.path.join(GOLDEN, 'channel_config.json'))
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        got = am.GlobalAssembler(compiled, chans, hw.DDSElementConfig).get_assembled_program()
+    assert sorted(got) == sorted(exp)
+    for core, want in exp.items():
+        assert got[core]['cmd_buf'].hex() == want['cmd_buf'], core
+        assert [b.hex() for b in got[core]['env_buffers']] == want['env_buffers'], core
+        assert [b.hex() for b in got[core]['freq_buffers']] == want['freq_buffers'], core
+
+
+def user_pulses(times):
+    dests = ['Q0.qdrv', 'Q0.rdrv', 'Q0.qdrv', 'Q1.qdrv']
+    freqs = ['Q0.freq', 'Q0.freq', 'Q0.freq', 1234234]
+    return [{'name': 'pulse', 'phase': 'np.pi/2', 'freq': f, 'env': np.ones(100), 'twidth': 24.e-9,
+             'amp': 0.5, 'dest': d, 'start_time': t} for d, f, t in zip(dests, freqs, times)]
+
+
+def test_user_schedule_lint():
+    """test_compiler.py:561-606: schedule=False runs LintSchedule instead"""
+    prog = sc.compile_straight(user_pulses([5, 8, 11, 5]), TABLE, TEST_FPGA, schedule=False).program
+    q0 = prog[('Q0.qdrv', 'Q0.rdrv', 'Q0.rdlo')]
+    assert [s['start_time'] for s in q0 if s['op'] == 'pulse'] == [5, 8, 11]
+    with pytest.raises(Exception, match='start time too early'):
+        sc.compile_straight(user_pulses([5, 6, 11, 5]), TABLE, TEST_FPGA, schedule=False)
+
+
+def test_hold_becomes_idle():
+    """passes.py:709-724: hold(64 after rdlo) -> idle at rdlo end + 64; the next
+    gate's barrier waits for idle end + pulse_load_clks"""
+    cfg = hw.FPGAConfig()
+    instrs = sc.resolve_gates([{'name': 'read', 'qubit': ['Q0']}], TABLE)
+    instrs.append(sc.Instr('hold', nclks=64, ref_chans=['Q0.rdlo'],
+                           scope={'Q0.qdrv', 'Q0.rdrv', 'Q0.rdlo'}))
+    instrs += sc.resolve_gates([{'name': 'X90', 'qubit': ['Q0']}], TABLE)
+    prog = sc.ScheduleIR({'block_0': sc.resolve_freqs(instrs, TABLE)})
+    sc.Schedule(cfg).run_pass(prog)
+    il = prog.blocks['block_0']['instructions']
+    assert [i.name for i in il] == ['pulse', 'pulse', 'idle', 'pulse']
+    assert [il[0].start_time, il[1].start_time] == [5, 305]
+    assert il[2].end_time == 305 + 1000 + 64
+    assert il[3].start_time == 305 + 1000 + 64 + 3
+    # a hold whose target already passed is dropped (passes.py:714, >=)
+    instrs = [sc.Instr('pulse', dest='Q0.qdrv', twidth=2e-9, freq=1e9, phase=0, amp=1, env=None),
+              sc.Instr('hold', nclks=0, ref_chans=['Q0.qdrv'], scope={'Q0.qdrv'})]
+    prog = sc.ScheduleIR({'block_0': instrs})
+    sc.Schedule(cfg).run_pass(prog)
+    assert [i.name for i in prog.blocks['block_0']['instructions']] == ['pulse']
+
+
+def P(dest, tw, **kw):
+    return sc.Instr('pulse', dest=dest, twidth=tw * 2e-9, freq=1e9, phase=0.0, amp=1.0, env=None, **kw)
+
+
+def test_branch_merge_and_loop():
+    """passes.py:616-653 on a hand-built CFG: a merge block starts after the
+    later predecessor; a *_loopctrl block registers the loop start, its
+    loopctrl jump_cond sets delta_t and resets the end time to the loop start"""
+    cfg = hw.FPGAConfig()
+    Q0 = {'Q0.qdrv', 'Q0.rdrv', 'Q0.rdlo'}
+    blocks = {
+        'block_0': [P('Q0.qdrv', 10), sc.Instr('jump_fproc', scope=Q0, cond_lhs=1, alu_cond='eq',
+                                                 jump_label='true_0', func_id=0)],
+        'false_0': [P('Q0.qdrv', 20), sc.Instr('jump_i', scope=Q0, jump_label='end_0')],
+        'true_0': [P('Q0.qdrv', 4)],
+        'end_0': [sc.Instr('barrier', scope=Q0), P('Q0.rdrv', 7)],
+        'body_loopctrl': [P('Q0.qdrv', 6), sc.Instr('alu', scope=Q0),
+                          sc.Instr('jump_cond', scope=Q0, jump_type='loopctrl', jump_label='body_loopctrl')],
+        'post_0': [P('Q0.qdrv', 1)],
+    }
+    edges = [('block_0', 'false_0'), ('block_0', 'true_0'), ('false_0', 'end_0'), ('true_0', 'end_0'),
+             ('end_0', 'body_loopctrl'), ('body_loopctrl', 'post_0')]
+    prog = sc.ScheduleIR(blocks, edges)
+    sc.Schedule(cfg).run_pass(prog)
+    t = {n: [i.start_time for i in b['instructions'] if i.name == 'pulse'] for n, b in prog.blocks.items()}
+    # block_0: pulse @5 (qdrv busy to 15); jump_fproc: last_end 8 + 8 = 16
+    assert t['block_0'] == [5]
+    assert t['false_0'] == [16] and t['true_0'] == [16]
+    # false_0 ends: qdrv 36, last_end 19 + 5 = 24; true_0: qdrv 20, last_end 19
+    assert t['end_0'] == [36]                   # barrier: max over Q0 channel times of both branches
+    loop = prog.loops['body_loopctrl']
+    assert loop['start_time'] == 36 + 7         # rdrv busy until 43
+    assert t['body_loopctrl'] == [39]           # qdrv free at 36, core at 36 + 3
+    # body: qdrv to 45; last_end 42 + 5 (alu) + 5 (jump_cond) = 52 -> delta_t 52 - 43
+    assert loop['delta_t'] == 9
+    assert t['post_0'] == [43]                  # loopctrl block ends at the loop start
+    # LintSchedule accepts its own output
+    sc.LintSchedule(cfg).run_pass(prog)
+
+
+def test_cfg_errors():
+    with pytest.raises(ValueError, match='unknown block'):
+        sc.ScheduleIR({'a': []}, [('a', 'b')])
+    with pytest.raises(ValueError, match='cycle'):
+        sc.ScheduleIR({'a': [P('Q0.qdrv', 1)], 'b': [P('Q0.qdrv', 1)]},
+                      [('a', 'b'), ('b', 'a')]).topological_order()
+    with pytest.raises(NotImplementedError):
+        sc.resolve_gates([{'name': 'Y-90', 'qubit': ['Q1']}], TABLE)
+    with pytest.raises(Exception, match='resolve gates'):
+        sc.Schedule(hw.FPGAConfig()).run_pass(sc.ScheduleIR({'b': [sc.Instr('gate', scope=set())]}))
+
+
+def test_core_scoper_patterns():
+    s = sc.CoreScoper(['Q0.qdrv', 'Q12.rdlo', 'C0.x'], [('{qubit}.qdrv', '{qubit}.rdrv', '{qubit}.rdlo')])
+    assert s.proc_groupings == {'Q0.qdrv': ('Q0.qdrv', 'Q0.rdrv', 'Q0.rdlo'),
+                                'Q12.rdlo': ('Q12.qdrv', 'Q12.rdrv', 'Q12.rdlo')}
+    assert sc._num('numpy.pi/2.0') == math.pi / 2 and sc._num('-np.pi*3') == -3 * math.pi
+    with pytest.raises(ValueError):
+        sc._num('__import__("os")')
+
+
+GATES = {'Q0': ['X90', 'X90Z90', 'Z90', 'read', 'X90_ef', 'rabi'], 'Q1': ['X90', 'read', 'X90_ef', 'rabi']}
+
+
+def random_program(rng, n):
+    prog = []
+    for _ in range(n):
+        r = rng.random()
+        q = ['Q0', 'Q1'][rng.integers(2)]
+        if r < 0.1:
+            prog.append({'name': 'delay', 't': float(rng.integers(1, 200)) * 2e-9, 'qubit': [q]})
+        elif r < 0.15:
+            prog.append({'name': 'barrier', 'qubit': ['Q0', 'Q1']})
+        elif r < 0.3:
+            prog.append({'name': 'pulse', 'phase': float(rng.random()), 'freq': q + '.freq',
+                         'env': {'env_func': 'square', 'paradict': {'phase': 0.0, 'amplitude': 1.0}},
+                         'twidth': float(rng.integers(1, 40)) * 2e-9, 'amp': 0.5,
+                         'dest': q + ['.qdrv', '.rdrv'][rng.integers(2)]})
+        else:
+            prog.append({'name': GATES[q][rng.integers(len(GATES[q]))], 'qubit': [q]})
+    return prog
+
+
+def assembled_cases(n_cases=24, seed=7):
+    rng = np.random.default_rng(seed)
+    chans = hw.load_channel_configs(os.path.join(GOLDEN, 'channel_config.json'))
+    for k in range(n_cases):
+        cfg = hw.FPGAConfig() if k % 2 else TEST_FPGA
+        compiled = sc.compile_straight(random_program(rng, int(rng.integers(3, 25))), TABLE, cfg)
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            asm = am.GlobalAssembler(compiled, chans, hw.DDSElementConfig).get_assembled_program()
+        yield k, compiled, asm
+
+
+def test_schedules_are_never_late_cpu():
+    """every pulse of a scheduled straight-line program is issued on time by
+    the RTL: exact linter verdict and oracle_fast agree (no DPEMU_F_LATE),
+    and every scheduled start_time appears in the machine code in order"""
+    from tests.test_lint import oracle_flags
+    n = 0
+    for k, compiled, asm in assembled_cases():
+        for core, prog in asm.items():
+            words = isa.bytes_to_words(prog['cmd_buf'])
+            rep = lint.lint_program(words)
+            assert rep.exact and not rep.late, (k, core, [str(f) for f in rep.findings])
+            assert not oracle_flags([words])[0] & _abi.F_LATE, (k, core)
+            n += 1
+    assert n >= 24
+
+
+@pytest.mark.gpu
+def test_schedules_are_never_late_gpu():
+    """the same property with the emulator on cuda:0 executing the programs"""
+    from distributed_processor_amd.emulator import Emulator, ProgramSet
+    from tests.test_lint import MAX_CYCLES
+    with Emulator(0) as emu:
+        for k, compiled, asm in assembled_cases():
+            progs = [isa.bytes_to_words(asm[c]['cmd_buf']) for c in sorted(asm)]
+            C = len(progs)
+            emu.load(ProgramSet([progs], cores_per_shot=C))
+            cfg = _abi.make_config(C, max_cycles=MAX_CYCLES, event_cap=64, trace_cap=16, meas_cap=16, seed=k)
+            s = emu.run(1, 0, cfg=cfg, outputs=('summary',)).arrays['summary']
+            summ = _abi.unpack_summary(np.asarray(s).view(np.uint32))
+            assert not (summ['flags'] & _abi.F_LATE).any(), k
+            assert (summ['status'] == _abi.ST_DONE).all(), k
+            n_pulses = [sum(st['op'] == 'pulse' for st in compiled.program[g]) for g in sorted(asm)]
+            assert summ['n_events'].tolist() == n_pulses, k
