@@ -251,19 +251,35 @@ def assembled_cases(n_cases=24, seed=7):
         yield k, compiled, asm
 
 
+def pulse_counts(compiled, asm, chans):
+    """pulse statements per assembled core key (the phase_reset adds one event)"""
+    core_of = {str(chans[g[0]].core_ind): g for g in compiled.program}
+    return [sum(st['op'] == 'pulse' for st in compiled.program[core_of[c]]) for c in sorted(asm)]
+
+
 def test_schedules_are_never_late_cpu():
     """every pulse of a scheduled straight-line program is issued on time by
-    the RTL: exact linter verdict and oracle_fast agree (no DPEMU_F_LATE),
-    and every scheduled start_time appears in the machine code in order"""
-    from tests.test_lint import oracle_flags
+    the RTL: the exact linter verdict and oracle_fast agree (no DPEMU_F_LATE,
+    every core done, one event per pulse plus the phase_reset)"""
+    import oracle
+    from tests.progfuzz import pack_programs
+    from tests.test_lint import MAX_CYCLES
+    chans = hw.load_channel_configs(os.path.join(GOLDEN, 'channel_config.json'))
     n = 0
     for k, compiled, asm in assembled_cases():
-        for core, prog in asm.items():
-            words = isa.bytes_to_words(prog['cmd_buf'])
+        progs = [isa.bytes_to_words(asm[c]['cmd_buf']) for c in sorted(asm)]
+        for c, words in zip(sorted(asm), progs):
             rep = lint.lint_program(words)
-            assert rep.exact and not rep.late, (k, core, [str(f) for f in rep.findings])
-            assert not oracle_flags([words])[0] & _abi.F_LATE, (k, core)
-            n += 1
+            assert rep.exact and not rep.late, (k, c, [str(f) for f in rep.findings])
+        C = len(progs)
+        cfg = _abi.make_config(C, max_cycles=MAX_CYCLES, event_cap=64, trace_cap=16, meas_cap=16, seed=k)
+        words, offs, ni = pack_programs(progs)
+        f = oracle.fast_run(cfg, words, offs, ni, np.arange(C, dtype=np.uint32), 0, 1, want=('summary',))
+        summ = _abi.unpack_summary(f['summary'])
+        assert not (summ['flags'] & _abi.F_LATE).any(), k
+        assert (summ['status'] == _abi.ST_DONE).all(), k
+        assert summ['n_events'].tolist() == [p + 1 for p in pulse_counts(compiled, asm, chans)], k
+        n += C
     assert n >= 24
 
 
@@ -272,6 +288,7 @@ def test_schedules_are_never_late_gpu():
     """the same property with the emulator on cuda:0 executing the programs"""
     from distributed_processor_amd.emulator import Emulator, ProgramSet
     from tests.test_lint import MAX_CYCLES
+    chans = hw.load_channel_configs(os.path.join(GOLDEN, 'channel_config.json'))
     with Emulator(0) as emu:
         for k, compiled, asm in assembled_cases():
             progs = [isa.bytes_to_words(asm[c]['cmd_buf']) for c in sorted(asm)]
@@ -282,5 +299,4 @@ def test_schedules_are_never_late_gpu():
             summ = _abi.unpack_summary(np.asarray(s).view(np.uint32))
             assert not (summ['flags'] & _abi.F_LATE).any(), k
             assert (summ['status'] == _abi.ST_DONE).all(), k
-            n_pulses = [sum(st['op'] == 'pulse' for st in compiled.program[g]) for g in sorted(asm)]
-            assert summ['n_events'].tolist() == n_pulses, k
+            assert summ['n_events'].tolist() == [p + 1 for p in pulse_counts(compiled, asm, chans)], k
