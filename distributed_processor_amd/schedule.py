@@ -28,12 +28,21 @@ a ``hold`` whose target is already passed is dropped (``>=``,
 ``passes.py:714``), and a loop-control block's end time is the loop's start
 time (``:641-649``).
 
+* A control-flow front end, ``compile_circuit``: ``flatten``
+  (FlattenProgram, ``ir/passes.py:62-124``), ``make_basic_blocks``
+  (``:135-178``), ``scope_blocks`` (ScopeProgram, ``:207-234``),
+  ``generate_cfg`` (``:368-388``), ``resolve_virtual_z_cfg`` (``:439-491``)
+  and ``resolve_fproc_channels`` (hold insertion, ``:532-552``) for
+  ``branch_fproc`` circuits.  Variables (declare / set_var / alu /
+  branch_var / register loops) are not restated.
+
 Parity: ``tests/test_schedule.py`` reproduces the reference's scheduling
 asserts (``python/test/test_compiler.py:75-98``), its user-schedule lint
-verdicts (``:561-606``) and, end to end through ``assembler.py``, the pulse
-statements of the straight-line compiler goldens
-(``test_outputs/test_linear_compile_out.txt``,
-``test_pulse_compile_out.txt``) -- the latter byte for byte after assembly.
+verdicts (``:561-606``) and, end to end through ``assembler.py``, five
+compiler goldens (``test_outputs/test_linear_compile_out.txt``,
+``test_pulse_compile_out.txt``, ``test_multirst_cfg.txt``,
+``test_multirst_fproc_res_cfg.txt``, ``test_fproc_hold.txt``): the compiled
+statements field by field, and the assembled bytes exactly.
 """
 
 from __future__ import annotations
@@ -120,9 +129,16 @@ class QubitScoper:
         self._mapping = mapping
 
     def get_scope(self, qubits) -> set:
+        """a qubit name maps to all its channels; a channel name to itself"""
         if isinstance(qubits, str):
             qubits = [qubits]
-        return {m.format(qubit=q) for q in qubits for m in self._mapping}
+        out = set()
+        for q in qubits:
+            if any(_pattern_regex(m).match(q) for m in self._mapping):
+                out.add(q)
+            else:
+                out |= {m.format(qubit=q) for m in self._mapping}
+        return out
 
 
 # ---------------------------------------------------------------- program
@@ -385,6 +401,11 @@ def resolve_gates(program: Sequence[dict], table: GateTable,
     scoper = QubitScoper(qubit_grouping)
     out: List[Instr] = []
     for st in program:
+        if isinstance(st, Instr):                # flattened control flow / scoped IR
+            if st.name != 'gate':
+                out.append(st)
+                continue
+            st = {'name': st.gate, 'qubit': st.qubit}
         name = st['name']
         if name in ('pulse',):
             d = dict(st)
@@ -395,10 +416,10 @@ def resolve_gates(program: Sequence[dict], table: GateTable,
             out.append(Instr('virtual_z', freq=st.get('freq', '{}.freq'.format(q)), phase=_num(st['phase']),
                              scope=scoper.get_scope(st['qubit'])))
         elif name in ('barrier', 'delay'):
-            scope = set(st['scope']) if 'scope' in st else scoper.get_scope(st['qubit'])
+            scope = scoper.get_scope(st['scope']) if 'scope' in st else scoper.get_scope(st['qubit'])
             out.append(Instr(name, scope=scope, **({'t': st['t']} if name == 'delay' else {})))
         elif name in ('branch_fproc', 'branch_var', 'loop', 'jump_fproc', 'jump_cond'):
-            raise NotImplementedError('control flow: build a ScheduleIR of basic blocks instead')
+            raise NotImplementedError('control flow: use compile_circuit (flatten -> basic blocks)')
         else:
             qubits = st['qubit'] if isinstance(st['qubit'], (list, tuple)) else [st['qubit']]
             out.append(Instr('barrier', scope=scoper.get_scope(qubits)))
@@ -505,4 +526,238 @@ def compile_straight(program: Sequence[dict], table: GateTable, fpga_config: FPG
     instrs = resolve_freqs(resolve_virtual_z(resolve_gates(program, table, qubit_grouping)), table)
     prog = ScheduleIR({'block_0': instrs})
     (Schedule if schedule else LintSchedule)(fpga_config, proc_grouping).run_pass(prog)
-    return CompiledProgram(compile_blocks(prog, proc_grouping), fpga_config)
+    out = CompiledProgram(compile_blocks(prog, proc_grouping), fpga_config)
+    out.ir = prog
+    return out
+
+
+# ---------------------------------------------------------------- control flow
+def flatten(program: Sequence, label_prefix: str = '') -> List[Instr]:
+    """``ir/passes.py:62-124``: ``branch_fproc`` / ``branch_var`` / ``loop``
+    -> jumps and labels (false block inline, true block after it; an empty
+    true block jumps straight to the end label).  Gates become ``gate``
+    instructions for ``resolve_gates``."""
+    out: List[Instr] = []
+    branchind = 0
+    for st in program:
+        st = copy.deepcopy(st)
+        name = st['name'] if isinstance(st, dict) else st.name
+        if name in ('branch_fproc', 'branch_var'):
+            true_b = flatten(st['true'], 'true_' + label_prefix)
+            false_b = flatten(st['false'], 'false_' + label_prefix)
+            lbl_false = '{}false_{}'.format(label_prefix, branchind)
+            lbl_end = '{}end_{}'.format(label_prefix, branchind)
+            lbl_true = '{}true_{}'.format(label_prefix, branchind) if true_b else lbl_end
+            if name == 'branch_fproc':
+                out.append(Instr('jump_fproc', alu_cond=st['alu_cond'], cond_lhs=st['cond_lhs'],
+                                 func_id=st['func_id'], scope=st['scope'], jump_label=lbl_true))
+            else:
+                out.append(Instr('jump_cond', alu_cond=st['alu_cond'], cond_lhs=st['cond_lhs'],
+                                 cond_rhs=st['cond_rhs'], scope=st['scope'], jump_label=lbl_true))
+            out.append(Instr('jump_label', label=lbl_false, scope=st['scope']))
+            out += false_b
+            out.append(Instr('jump_i', jump_label=lbl_end, scope=st['scope']))
+            if true_b:
+                out.append(Instr('jump_label', label=lbl_true, scope=st['scope']))
+                out += true_b
+            out.append(Instr('jump_label', label=lbl_end, scope=st['scope']))
+            branchind += 1
+        elif name == 'loop':
+            body = flatten(st['body'], 'loop_body_' + label_prefix)
+            lbl = '{}loop_{}_loopctrl'.format(label_prefix, branchind)
+            out.append(Instr('jump_label', label=lbl, scope=st['scope']))
+            out.append(Instr('barrier', qubit=st['scope']))
+            out += body
+            out.append(Instr('loop_end', loop_label=lbl, scope=st['scope']))
+            out.append(Instr('jump_cond', cond_lhs=st['cond_lhs'], cond_rhs=st['cond_rhs'],
+                             alu_cond=st['alu_cond'], jump_label=lbl, scope=st['scope'], jump_type='loopctrl'))
+            branchind += 1
+        elif isinstance(st, Instr):
+            out.append(st)
+        elif name == 'pulse':
+            d = dict(st)
+            d['phase'] = _num(d['phase'])
+            out.append(instr(d))
+        elif name in ('virtual_z', 'virtualz', 'barrier', 'delay'):
+            d = dict(st)
+            if name in ('virtual_z', 'virtualz'):
+                q = d['qubit'][0] if isinstance(d['qubit'], (list, tuple)) else d['qubit']
+                out.append(Instr('virtual_z', freq=d.get('freq', '{}.freq'.format(q)), phase=_num(d['phase']),
+                                 qubit=d['qubit']))
+            else:
+                out.append(Instr(name, scope=d.get('scope'), qubit=d.get('qubit'),
+                                 **({'t': d['t']} if name == 'delay' else {})))
+        else:
+            out.append(Instr('gate', gate=name, qubit=st['qubit']))
+    return out
+
+
+def make_basic_blocks(flat: Sequence[Instr]) -> 'OrderedDict[str, List[Instr]]':
+    """``ir/passes.py:135-178``: split at jumps (each jump is its own
+    ``<block>_ctrl`` / ``<loop label>_ctrl`` block) and labels (a label starts
+    a block named after it).  Blocks come back in the reference's source
+    order (``blocknames_by_ind``: by ``ind``, ties in first-insertion order);
+    empty blocks are dropped."""
+    nodes: 'OrderedDict[str, list]' = OrderedDict([('block_0', [None, 0])])
+
+    def add(name, instrs, ind):
+        if name in nodes:
+            nodes[name][0], nodes[name][1] = instrs, ind
+        else:
+            nodes[name] = [instrs, ind]
+
+    cur_name, cur, blockname_ind, block_ind = 'block_0', [], 1, 0
+    for st in flat:
+        if st.name in ('jump_fproc', 'jump_cond', 'jump_i'):
+            add(cur_name, cur, block_ind)
+            block_ind += 1
+            if st.jump_label.split('_')[-1] == 'loopctrl':
+                ctrl = '{}_ctrl'.format(st.jump_label)
+            else:
+                ctrl = '{}_ctrl'.format(cur_name)
+            add(ctrl, [st], block_ind)
+            block_ind += 1
+            cur_name, cur = 'block_{}'.format(blockname_ind), []
+            blockname_ind += 1
+        elif st.name == 'jump_label':
+            add(cur_name, cur, block_ind)
+            cur, cur_name = [st], st.label
+        elif st.name in ('branch_fproc', 'branch_var', 'loop'):
+            raise Exception('{}: must flatten all control flow before forming blocks'.format(st))
+        else:
+            cur.append(st)
+    add(cur_name, cur, block_ind)
+    order = sorted((n for n in nodes if nodes[n][0]), key=lambda n: nodes[n][1])
+    return OrderedDict((n, nodes[n][0]) for n in order)
+
+
+def scope_blocks(blocks, qubit_grouping=DEFAULT_QUBIT_GROUPING) -> Dict[str, set]:
+    """``ir/passes.py:207-234`` (ScopeProgram): instruction scopes (qubits ->
+    channels), block scopes, and unscoped barrier / delay / idle -> the whole
+    program's scope."""
+    scoper = QubitScoper(qubit_grouping)
+    scopes = {}
+    for name, instrs in blocks.items():
+        scope = set()
+        for ins in instrs:
+            if ins.scope is not None:
+                ins.scope = scoper.get_scope(ins.scope)
+                scope |= ins.scope
+            elif ins.qubit is not None:
+                ins.scope = scoper.get_scope(ins.qubit)
+                scope |= ins.scope
+            elif ins.dest is not None:
+                scope |= scoper.get_scope(ins.dest)
+        scopes[name] = scope
+    everything = set().union(*scopes.values()) if scopes else set()
+    for instrs in blocks.values():
+        for ins in instrs:
+            if ins.name in ('barrier', 'delay', 'idle') and ins.scope is None:
+                ins.scope = set(everything)
+    return scopes
+
+
+def generate_cfg(blocks, scopes) -> List[Tuple[str, str]]:
+    """``ir/passes.py:368-388``: per channel, an edge from the last block
+    that touched it; conditional jumps add an edge to their target (loop
+    control jumps do not, keeping the graph a DAG); ``jump_i`` adds its target
+    and ends the fall-through."""
+    edges: List[Tuple[str, str]] = []
+
+    def edge(a, b):
+        if (a, b) not in edges:
+            edges.append((a, b))
+
+    last = {d: None for d in set().union(*scopes.values())} if scopes else {}
+    for name, instrs in blocks.items():
+        for d in scopes[name]:
+            if last[d] is not None:
+                edge(last[d], name)
+        tail = instrs[-1]
+        if tail.name in ('jump_fproc', 'jump_cond'):
+            if tail.jump_type != 'loopctrl':
+                edge(name, tail.jump_label)
+            for d in scopes[name]:
+                last[d] = name
+        elif tail.name == 'jump_i':
+            edge(name, tail.jump_label)
+            for d in scopes[name]:
+                last[d] = None
+        else:
+            for d in scopes[name]:
+                last[d] = name
+    return edges
+
+
+def resolve_virtual_z_cfg(prog: ScheduleIR):
+    """``ir/passes.py:439-491``: virtual-z phases accumulate along the CFG;
+    predecessors must agree on every frequency's phase."""
+    for node in prog.topological_order():
+        acc: Dict[object, float] = {}
+        for pred in prog.predecessors(node):
+            for f, ph in prog.blocks[pred]['ending_zphases'].items():
+                if f in acc and acc[f] != ph:
+                    raise ValueError('Phase mismatch in {} at {} predecessor {} ({} rad)'.format(f, node, pred, ph))
+                acc[f] = ph
+        block = prog.blocks[node]
+        kept = []
+        for ins in block['instructions']:
+            if ins.name == 'pulse':
+                if ins.freq in acc:
+                    ins.phase += acc[ins.freq]
+                kept.append(ins)
+            elif ins.name == 'virtual_z':
+                acc[ins.freq] = acc.get(ins.freq, 0) + ins.phase
+            else:
+                kept.append(ins)
+        block['instructions'] = kept
+        block['ending_zphases'] = acc
+
+
+def resolve_fproc_channels(prog: ScheduleIR, fpga_config: FPGAConfig):
+    """``ir/passes.py:532-552``: a named fproc channel (``'Q0.meas'``) puts a
+    ``hold`` (``hold_nclks`` after its ``hold_after_chans``) before the
+    instruction that reads it, and lowers ``func_id`` to the channel id."""
+    for node in prog.topological_order():
+        il = prog.blocks[node]['instructions']
+        i = 0
+        while i < len(il):
+            ins = il[i]
+            if ins.name in ('read_fproc', 'jump_fproc', 'alu_fproc'):
+                if ins.func_id in fpga_config.fproc_channels:
+                    ch = fpga_config.fproc_channels[ins.func_id]
+                    il.insert(i, Instr('hold', nclks=ch.hold_nclks, ref_chans=list(ch.hold_after_chans),
+                                       scope=set(ins.scope)))
+                    i += 1
+                    ins.func_id = ch.id
+                elif not isinstance(ins.func_id, int):
+                    raise AssertionError('func_id {!r} is neither a named fproc channel nor an int'
+                                         .format(ins.func_id))
+            i += 1
+
+
+def compile_circuit(program: Sequence, table: GateTable, fpga_config: FPGAConfig, schedule: bool = True,
+                    proc_grouping=DEFAULT_PROC_GROUPING,
+                    qubit_grouping=DEFAULT_QUBIT_GROUPING) -> CompiledProgram:
+    """QubiC circuit with ``branch_fproc`` control flow -> CompiledProgram, in
+    the reference's pass order (``compiler.py:149-174``): FlattenProgram,
+    MakeBasicBlocks, ScopeProgram, ResolveGates, GenerateCFG, ResolveVirtualZ,
+    ResolveFreqs, ResolveFPROCChannels, Schedule (or LintSchedule), compile.
+    Variables (``declare`` / ``set_var`` / ``alu`` / ``branch_var`` / register
+    loops) are not restated."""
+    blocks = make_basic_blocks(flatten(program))
+    scopes = scope_blocks(blocks, qubit_grouping)
+    edges = generate_cfg(blocks, scopes)
+    prog = ScheduleIR(OrderedDict((n, resolve_gates(il, table, qubit_grouping)) for n, il in blocks.items()),
+                      edges)
+    for n, s in scopes.items():
+        prog.blocks[n]['scope'] = s
+    prog.scope = set().union(*scopes.values()) if scopes else set()
+    resolve_virtual_z_cfg(prog)
+    for b in prog.blocks.values():
+        resolve_freqs(b['instructions'], table)
+    resolve_fproc_channels(prog, fpga_config)
+    (Schedule if schedule else LintSchedule)(fpga_config, proc_grouping).run_pass(prog)
+    out = CompiledProgram(compile_blocks(prog, proc_grouping), fpga_config)
+    out.ir = prog
+    return out

@@ -75,14 +75,39 @@ PULSE_PROGRAM = [{'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1
                  {'name': 'read', 'qubit': ['Q0']}]
 LINEAR_PROGRAM = [{'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1']},
                   {'name': 'read', 'qubit': ['Q0']}]
-GOLDEN_CASES = {'test_linear_compile_out': LINEAR_PROGRAM, 'test_pulse_compile_out': PULSE_PROGRAM}
+
+def two_resets(func0, func1):
+    return [{'name': 'X90', 'qubit': ['Q0']},
+            {'name': 'branch_fproc', 'alu_cond': 'eq', 'cond_lhs': 1, 'func_id': func0,
+             'true': [], 'false': [{'name': 'X90', 'qubit': ['Q0']}], 'scope': ['Q0']},
+            {'name': 'branch_fproc', 'alu_cond': 'eq', 'cond_lhs': 1, 'func_id': func1,
+             'true': [], 'false': [{'name': 'X90', 'qubit': ['Q1']}], 'scope': ['Q1']},
+            {'name': 'X90', 'qubit': ['Q1']}]
+
+
+# golden name -> (program, fpga_config, compile function); programs from
+# test_compiler.py:330-352 (linear), :100-122 (pulse), :224-255 (multirst_cfg),
+# :257-291 (multirst_fproc_res_cfg), :293-330 (fproc_hold)
+GOLDEN_CASES = {
+    'test_linear_compile_out': (LINEAR_PROGRAM, TEST_FPGA, sc.compile_straight),
+    'test_pulse_compile_out': (PULSE_PROGRAM, TEST_FPGA, sc.compile_straight),
+    'test_multirst_cfg': (two_resets(1, 0), TEST_FPGA, sc.compile_circuit),
+    'test_multirst_fproc_res_cfg': (two_resets('Q0.meas', 'Q1.meas'), hw.FPGAConfig(), sc.compile_circuit),
+    'test_fproc_hold': ([{'name': 'X90', 'qubit': ['Q0']}, {'name': 'read', 'qubit': ['Q0']},
+                         {'name': 'X90', 'qubit': ['Q0']}, {'name': 'read', 'qubit': ['Q1']}]
+                        + two_resets('Q0.meas', 'Q1.meas')[1:], hw.FPGAConfig(), sc.compile_circuit),
+}
+
+
+def compile_case(name):
+    prog, cfg, fn = GOLDEN_CASES[name]
+    return fn(prog, TABLE, cfg)
 
 
 @pytest.mark.parametrize('name', sorted(GOLDEN_CASES))
 def test_compile_matches_golden_statements(name):
-    """test_compiler.py:100-122 (pulse) and :330-352 (linear): the compiled
-    per-core statements equal the golden's, field by field"""
-    got = sc.compile_straight(GOLDEN_CASES[name], TABLE, TEST_FPGA).program
+    """the compiled per-core statements equal the golden's, field by field"""
+    got = compile_case(name).program
     want = golden_inputs(name)
     assert sorted(got) == sorted(want)
     for grp, stmts in want.items():
@@ -99,13 +124,62 @@ def test_compile_matches_golden_statements(name):
                     assert a[k] == b[k], (grp, k, a[k], b[k])
 
 
+def test_straight_and_circuit_front_ends_agree():
+    """compile_circuit on a branch-free program = compile_straight"""
+    for prog in (LINEAR_PROGRAM, PULSE_PROGRAM):
+        a = sc.compile_straight(prog, TABLE, TEST_FPGA).program
+        b = sc.compile_circuit(prog, TABLE, TEST_FPGA).program
+        assert sorted(a) == sorted(b)
+        for g in a:
+            assert [(s['op'], s.get('start_time')) for s in a[g]] == [(s['op'], s.get('start_time')) for s in b[g]]
+
+
+def test_fproc_res_lints_clean():
+    """test_compiler.py:270-272: LintSchedule accepts the scheduled program"""
+    blocks = sc.make_basic_blocks(sc.flatten(two_resets('Q0.meas', 'Q1.meas')))
+    assert list(blocks) == ['block_0', 'block_0_ctrl', 'false_0', 'false_0_ctrl', 'end_0', 'end_0_ctrl',
+                            'false_1', 'false_1_ctrl', 'end_1']
+    compiled = sc.compile_circuit(two_resets('Q0.meas', 'Q1.meas'), TABLE, hw.FPGAConfig())
+    sc.LintSchedule(hw.FPGAConfig()).run_pass(compiled.ir)
+    with pytest.raises(Exception, match='too early'):      # the RTL needs more than 1 clk per jump
+        sc.LintSchedule(hw.FPGAConfig(jump_fproc_clks=30)).run_pass(compiled.ir)
+
+
+def assemble(compiled):
+    chans = hw.load_channel_configs(os.path.join(GOLDEN, 'channel_config.json'))
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        return am.GlobalAssembler(compiled, chans, hw.DDSElementConfig).get_assembled_program()
+
+
+@pytest.mark.parametrize('func_ids', [(1, 0), ('Q0.meas', 'Q1.meas')])
+def test_branch_schedules_vs_rtl_latencies(func_ids):
+    """a schedule made with jump_fproc_clks = 4 (test_compiler.py's
+    fpga_config) puts a pulse behind a jump_fproc earlier than the RTL can
+    decode it (8 clks): oracle_fast flags DPEMU_F_LATE and the machine-code
+    linter says ``late``.  With the reference's default FPGAConfig and with
+    the RTL's exact latencies no lane is late."""
+    from tests.test_lint import oracle_flags
+    exact = hw.FPGAConfig(**{k: v for k, v in hw.EXACT_LATENCIES.items()
+                             if k in ('alu_instr_clks', 'jump_cond_clks', 'jump_fproc_clks', 'pulse_load_clks')})
+    for cfg, want_late in ((TEST_FPGA, True), (hw.FPGAConfig(), False), (exact, False)):
+        asm = assemble(sc.compile_circuit(two_resets(*func_ids), TABLE, cfg))
+        late = []
+        for core in sorted(asm):
+            words = isa.bytes_to_words(asm[core]['cmd_buf'])
+            flag = bool(oracle_flags([words])[0] & _abi.F_LATE)
+            assert flag == lint.lint_program(words).late, (cfg.jump_fproc_clks, core)
+            late.append(flag)
+        assert any(late) == want_late, (cfg.jump_fproc_clks, late)
+
+
 @pytest.mark.parametrize('name', sorted(GOLDEN_CASES))
 def test_schedule_compile_assemble_bytes(name):
     """gate program -> schedule -> compile -> assemble is byte-identical to the
     reference GlobalAssembler on the golden (DDSElementConfig)"""
     with open(os.path.join(GOLDEN, 'asm_programs.json')) as f:
         exp = json.load(f)['programs'][name]['dds_elem']
-    compiled = sc.compile_straight(GOLDEN_CASES[name], TABLE, TEST_FPGA)
+    compiled = compile_case(name)
     chans = hw.load_channel_configs(os.path.join(GOLDEN, 'channel_config.json'))
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')
@@ -300,3 +374,17 @@ def test_schedules_are_never_late_gpu():
             assert not (summ['flags'] & _abi.F_LATE).any(), k
             assert (summ['status'] == _abi.ST_DONE).all(), k
             assert summ['n_events'].tolist() == [p + 1 for p in pulse_counts(compiled, asm, chans)], k
+        # branch programs: the GPU's F_LATE verdict per core = oracle_fast's
+        from tests.test_lint import oracle_flags
+        for cfg in (TEST_FPGA, hw.FPGAConfig()):
+            for func_ids in ((1, 0), ('Q0.meas', 'Q1.meas')):
+                asm = assemble(sc.compile_circuit(two_resets(*func_ids), TABLE, cfg))
+                for core in sorted(asm):
+                    words = isa.bytes_to_words(asm[core]['cmd_buf'])
+                    emu.load(ProgramSet([[words]], cores_per_shot=1))
+                    rc = _abi.make_config(1, max_cycles=MAX_CYCLES, event_cap=64, trace_cap=16, meas_cap=16,
+                                          seed=0)
+                    s = emu.run(1, 0, cfg=rc, outputs=('summary',)).arrays['summary']
+                    flags = _abi.unpack_summary(np.asarray(s).view(np.uint32))['flags']
+                    assert (flags & _abi.F_LATE).tolist() == (oracle_flags([words]) & _abi.F_LATE).tolist(), \
+                        (cfg.jump_fproc_clks, func_ids, core)
