@@ -33,16 +33,20 @@ time (``:641-649``).
   (``:135-178``), ``scope_blocks`` (ScopeProgram, ``:207-234``),
   ``generate_cfg`` (``:368-388``), ``resolve_virtual_z_cfg`` (``:439-491``)
   and ``resolve_fproc_channels`` (hold insertion, ``:532-552``) for
-  ``branch_fproc`` circuits.  Variables (declare / set_var / alu /
-  branch_var / register loops) are not restated.
+  ``branch_fproc`` / ``branch_var`` / ``loop`` circuits, with ``declare``,
+  ``set_var``, ``alu``, ``read_fproc`` / ``alu_fproc`` compiled as in
+  ``compiler.py:283-320``.  Not restated: hardware virtual z
+  (``bind_phase``, ResolveHWVirtualZ ``:390-437``) and RescopeVars
+  (``:554-593``, which only widens a variable's scope when it is used
+  outside the scope it was declared in).
 
 Parity: ``tests/test_schedule.py`` reproduces the reference's scheduling
 asserts (``python/test/test_compiler.py:75-98``), its user-schedule lint
-verdicts (``:561-606``) and, end to end through ``assembler.py``, five
-compiler goldens (``test_outputs/test_linear_compile_out.txt``,
-``test_pulse_compile_out.txt``, ``test_multirst_cfg.txt``,
-``test_multirst_fproc_res_cfg.txt``, ``test_fproc_hold.txt``): the compiled
-statements field by field, and the assembled bytes exactly.
+verdicts (``:561-606``) and, end to end through ``assembler.py``, eight of
+the nine compiler goldens (linear, pulse, multirst_cfg,
+multirst_fproc_res_cfg, fproc_hold, simple_loop, compound_loop,
+nested_loop; all but hw_virtualz): the compiled statements field by field,
+and the assembled bytes exactly.
 """
 
 from __future__ import annotations
@@ -501,6 +505,30 @@ def compile_blocks(prog: ScheduleIR, proc_grouping=DEFAULT_PROC_GROUPING) -> Dic
             elif ins.name == 'loop_end':
                 for g in scoper.get_groups_bydest(ins.scope):
                     progs[g].append({'op': 'inc_qclk', 'in0': -prog.loops[ins.loop_label]['delta_t']})
+            elif ins.name == 'declare':                              # compiler.py:283-287
+                dtype = (ins.dtype, 0) if ins.dtype in ('phase', 'amp') else ins.dtype
+                for g in scoper.get_groups_bydest(ins.scope):
+                    progs[g].append({'op': 'declare_reg', 'name': ins.var, 'dtype': dtype})
+            elif ins.name == 'alu':
+                for g in scoper.get_groups_bydest(ins.scope):
+                    progs[g].append({'op': 'reg_alu', 'in0': ins.lhs, 'in1_reg': ins.rhs,
+                                     'alu_op': ins.op, 'out_reg': ins.out})
+            elif ins.name == 'set_var':
+                for g in scoper.get_groups_bydest(ins.scope):
+                    progs[g].append({'op': 'reg_alu', 'in0': ins.value, 'in1_reg': ins.var,
+                                     'alu_op': 'id0', 'out_reg': ins.var})
+            elif ins.name == 'read_fproc':
+                for g in scoper.get_groups_bydest(ins.scope):
+                    progs[g].append({'op': 'alu_fproc', 'in0': 0, 'alu_op': 'id1',
+                                     'func_id': ins.func_id, 'out_reg': ins.var})
+            elif ins.name == 'alu_fproc':
+                for g in scoper.get_groups_bydest(ins.scope):
+                    progs[g].append({'op': 'alu_fproc', 'in0': ins.lhs, 'alu_op': ins.op,
+                                     'func_id': ins.func_id, 'out_reg': ins.out})
+            elif ins.name == 'jump_cond':
+                for g in scoper.get_groups_bydest(ins.scope):
+                    progs[g].append({'op': 'jump_cond', 'in0': ins.cond_lhs, 'alu_op': ins.alu_cond,
+                                     'jump_label': ins.jump_label, 'in1_reg': ins.cond_rhs})
             else:
                 raise Exception('{} not yet implemented'.format(ins.name))
     for g in progs:
@@ -532,6 +560,10 @@ def compile_straight(program: Sequence[dict], table: GateTable, fpga_config: FPG
 
 
 # ---------------------------------------------------------------- control flow
+# circuit statements that are already IR instructions (ir/instructions.py)
+_IR_STATEMENTS = ('declare', 'set_var', 'alu', 'read_fproc', 'alu_fproc', 'hold', 'idle', 'jump_label',
+                  'jump_i', 'jump_cond', 'jump_fproc')
+
 def flatten(program: Sequence, label_prefix: str = '') -> List[Instr]:
     """``ir/passes.py:62-124``: ``branch_fproc`` / ``branch_var`` / ``loop``
     -> jumps and labels (false block inline, true block after it; an empty
@@ -574,6 +606,8 @@ def flatten(program: Sequence, label_prefix: str = '') -> List[Instr]:
             branchind += 1
         elif isinstance(st, Instr):
             out.append(st)
+        elif name in _IR_STATEMENTS:
+            out.append(instr(st))
         elif name == 'pulse':
             d = dict(st)
             d['phase'] = _num(d['phase'])
@@ -739,12 +773,12 @@ def resolve_fproc_channels(prog: ScheduleIR, fpga_config: FPGAConfig):
 def compile_circuit(program: Sequence, table: GateTable, fpga_config: FPGAConfig, schedule: bool = True,
                     proc_grouping=DEFAULT_PROC_GROUPING,
                     qubit_grouping=DEFAULT_QUBIT_GROUPING) -> CompiledProgram:
-    """QubiC circuit with ``branch_fproc`` control flow -> CompiledProgram, in
+    """QubiC circuit with control flow (``branch_fproc`` / ``branch_var`` /
+    ``loop``) -> CompiledProgram, in
     the reference's pass order (``compiler.py:149-174``): FlattenProgram,
     MakeBasicBlocks, ScopeProgram, ResolveGates, GenerateCFG, ResolveVirtualZ,
     ResolveFreqs, ResolveFPROCChannels, Schedule (or LintSchedule), compile.
-    Variables (``declare`` / ``set_var`` / ``alu`` / ``branch_var`` / register
-    loops) are not restated."""
+    ``bind_phase`` (hardware virtual z) and RescopeVars are not restated."""
     blocks = make_basic_blocks(flatten(program))
     scopes = scope_blocks(blocks, qubit_grouping)
     edges = generate_cfg(blocks, scopes)

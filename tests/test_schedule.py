@@ -99,6 +99,37 @@ GOLDEN_CASES = {
 }
 
 
+LOOP_FPGA = hw.FPGAConfig(alu_instr_clks=2, fpga_clk_period=2.e-9, jump_cond_clks=3, jump_fproc_clks=4,
+                          pulse_load_clks=4, pulse_regwrite_clks=1)       # test_compiler.py:418-423
+PREAMBLE = [{'name': 'X90', 'qubit': ['Q0']}, {'name': 'read', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1']}]
+X90X90_Q0 = [{'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q0']}]
+
+
+def loop(var, body, scope):
+    return {'name': 'loop', 'cond_lhs': 10, 'cond_rhs': var, 'alu_cond': 'ge', 'scope': scope, 'body': body}
+
+
+def declare(var):
+    return {'name': 'declare', 'var': var, 'dtype': 'int', 'scope': ['Q0']}
+
+
+TAIL = [{'name': 'CR', 'qubit': ['Q1', 'Q0']}, {'name': 'X90', 'qubit': ['Q1']}]
+# test_compiler.py:376-414 (simple), :416-455 (compound), :457-516 (nested)
+GOLDEN_CASES['test_simple_loop'] = (
+    PREAMBLE + [{'name': 'Z90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q0']}, declare('loopind'),
+                loop('loopind', X90X90_Q0, ['Q0']), {'name': 'read', 'qubit': ['Q0']},
+                {'name': 'X90', 'qubit': ['Q1']}], TEST_FPGA, sc.compile_circuit)
+GOLDEN_CASES['test_compound_loop'] = (
+    PREAMBLE + [declare('loopind'), loop('loopind', X90X90_Q0, ['Q0', 'Q1'])] + TAIL, LOOP_FPGA,
+    sc.compile_circuit)
+GOLDEN_CASES['test_nested_loop'] = (
+    PREAMBLE + [declare('loopind'), declare('loopind2'),
+                loop('loopind', X90X90_Q0 + [loop('loopind2', [{'name': 'X90', 'qubit': ['Q1']},
+                                                              {'name': 'read', 'qubit': ['Q0']}],
+                                                   ['Q0', 'Q1'])], ['Q0', 'Q1'])] + TAIL, LOOP_FPGA,
+    sc.compile_circuit)
+
+
 def compile_case(name):
     prog, cfg, fn = GOLDEN_CASES[name]
     return fn(prog, TABLE, cfg)
@@ -178,9 +209,15 @@ def test_schedule_compile_assemble_bytes(name):
     """gate program -> schedule -> compile -> assemble is byte-identical to the
     reference GlobalAssembler on the golden (DDSElementConfig)"""
     with open(os.path.join(GOLDEN, 'asm_programs.json')) as f:
-        exp = json.load(f)['programs'][name]['dds_elem']
+        exp = json.load(f)['programs'][name]
     compiled = compile_case(name)
     chans = hw.load_channel_configs(os.path.join(GOLDEN, 'channel_config.json'))
+    if 'reference_error' in exp:          # the reference GlobalAssembler raised on it (AssertionError)
+        with pytest.raises(Exception), warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            am.GlobalAssembler(compiled, chans, hw.DDSElementConfig).get_assembled_program()
+        return
+    exp = exp['dds_elem']
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')
         got = am.GlobalAssembler(compiled, chans, hw.DDSElementConfig).get_assembled_program()
