@@ -35,18 +35,18 @@ time (``:641-649``).
   and ``resolve_fproc_channels`` (hold insertion, ``:532-552``) for
   ``branch_fproc`` / ``branch_var`` / ``loop`` circuits, with ``declare``,
   ``set_var``, ``alu``, ``read_fproc`` / ``alu_fproc`` compiled as in
-  ``compiler.py:283-320``.  Not restated: hardware virtual z
-  (``bind_phase``, ResolveHWVirtualZ ``:390-437``) and RescopeVars
-  (``:554-593``, which only widens a variable's scope when it is used
-  outside the scope it was declared in).
+  ``compiler.py:283-320``, variable registration (``:253-283``) and
+  hardware virtual z (``bind_phase``, ResolveHWVirtualZ ``:405-437``).  Not
+  restated: RescopeVars (``:554-593``, which only widens a variable's scope
+  when it is used outside the scope it was declared in).
 
 Parity: ``tests/test_schedule.py`` reproduces the reference's scheduling
 asserts (``python/test/test_compiler.py:75-98``), its user-schedule lint
-verdicts (``:561-606``) and, end to end through ``assembler.py``, eight of
-the nine compiler goldens (linear, pulse, multirst_cfg,
-multirst_fproc_res_cfg, fproc_hold, simple_loop, compound_loop,
-nested_loop; all but hw_virtualz): the compiled statements field by field,
-and the assembled bytes exactly.
+verdicts (``:561-606``) and, end to end through ``assembler.py``, all nine
+compiler goldens of ``python/test/test_outputs`` (linear, pulse,
+multirst_cfg, multirst_fproc_res_cfg, fproc_hold, simple_loop,
+compound_loop, nested_loop, hw_virtualz): the compiled statements field by
+field, and the assembled bytes exactly (or the reference's rejection).
 """
 
 from __future__ import annotations
@@ -561,7 +561,7 @@ def compile_straight(program: Sequence[dict], table: GateTable, fpga_config: FPG
 
 # ---------------------------------------------------------------- control flow
 # circuit statements that are already IR instructions (ir/instructions.py)
-_IR_STATEMENTS = ('declare', 'set_var', 'alu', 'read_fproc', 'alu_fproc', 'hold', 'idle', 'jump_label',
+_IR_STATEMENTS = ('declare', 'bind_phase', 'set_var', 'alu', 'read_fproc', 'alu_fproc', 'hold', 'idle', 'jump_label',
                   'jump_i', 'jump_cond', 'jump_fproc')
 
 def flatten(program: Sequence, label_prefix: str = '') -> List[Instr]:
@@ -748,6 +748,49 @@ def resolve_virtual_z_cfg(prog: ScheduleIR):
         block['ending_zphases'] = acc
 
 
+def register_vars(blocks) -> Dict[str, dict]:
+    """``ir/passes.py:253-283`` (the variable half of RegisterVarsAndFreqs):
+    declared variables with their scope, and register instructions scoped by
+    the variables they touch"""
+    vars_: Dict[str, dict] = {}
+    for instrs in blocks.values():
+        for ins in instrs:
+            if ins.name == 'declare':
+                vars_[ins.var] = {'scope': set(ins.scope or ()), 'dtype': ins.dtype}
+            elif ins.name == 'alu':
+                ins.scope = vars_[ins.rhs]['scope'] | (vars_[ins.lhs]['scope'] if isinstance(ins.lhs, str) else set())
+                if not vars_[ins.out]['scope'] <= ins.scope:
+                    raise AssertionError('alu output {} is scoped wider than its inputs'.format(ins.out))
+            elif ins.name in ('set_var', 'read_fproc'):
+                ins.scope = set(vars_[ins.var]['scope'])
+            elif ins.name == 'alu_fproc' and isinstance(ins.lhs, str):
+                ins.scope = set(vars_[ins.rhs]['scope'])
+    return vars_
+
+
+def resolve_hw_virtual_z(prog: ScheduleIR, vars_: Dict[str, dict]):
+    """``ir/passes.py:405-437``: ``bind_phase`` binds a frequency's phase to
+    a register (initialised by a set_var 0); virtual z on a bound frequency
+    becomes an ``alu add`` on that register, and pulses on it take the
+    register as their phase."""
+    bound: Dict[object, str] = {}
+    for node in prog.topological_order():
+        il = prog.blocks[node]['instructions']
+        for i, ins in enumerate(il):
+            if ins.name == 'bind_phase':
+                bound[ins.freq] = ins.var
+                il[i] = Instr('set_var', value=0, var=ins.var, scope=set(vars_[ins.var]['scope']))
+            elif ins.name == 'virtual_z' and ins.freq in bound:
+                var = bound[ins.freq]
+                if ins.scope is not None and not set(ins.scope) <= vars_[var]['scope']:
+                    raise AssertionError('virtual z on {} outside the scope of {}'.format(ins.freq, var))
+                il[i] = Instr('alu', op='add', lhs=ins.phase, rhs=var, out=var, scope=set(vars_[var]['scope']))
+            elif ins.name == 'pulse' and ins.freq in bound:
+                ins.phase = bound[ins.freq]
+            elif ins.name == 'gate':
+                raise Exception('All Gate instructions must be resolved before running this pass!')
+
+
 def resolve_fproc_channels(prog: ScheduleIR, fpga_config: FPGAConfig):
     """``ir/passes.py:532-552``: a named fproc channel (``'Q0.meas'``) puts a
     ``hold`` (``hold_nclks`` after its ``hold_after_chans``) before the
@@ -778,15 +821,17 @@ def compile_circuit(program: Sequence, table: GateTable, fpga_config: FPGAConfig
     the reference's pass order (``compiler.py:149-174``): FlattenProgram,
     MakeBasicBlocks, ScopeProgram, ResolveGates, GenerateCFG, ResolveVirtualZ,
     ResolveFreqs, ResolveFPROCChannels, Schedule (or LintSchedule), compile.
-    ``bind_phase`` (hardware virtual z) and RescopeVars are not restated."""
+    RescopeVars is not restated."""
     blocks = make_basic_blocks(flatten(program))
     scopes = scope_blocks(blocks, qubit_grouping)
+    vars_ = register_vars(blocks)
     edges = generate_cfg(blocks, scopes)
     prog = ScheduleIR(OrderedDict((n, resolve_gates(il, table, qubit_grouping)) for n, il in blocks.items()),
                       edges)
     for n, s in scopes.items():
         prog.blocks[n]['scope'] = s
     prog.scope = set().union(*scopes.values()) if scopes else set()
+    resolve_hw_virtual_z(prog, vars_)
     resolve_virtual_z_cfg(prog)
     for b in prog.blocks.values():
         resolve_freqs(b['instructions'], table)

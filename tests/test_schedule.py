@@ -129,6 +129,19 @@ GOLDEN_CASES['test_nested_loop'] = (
                                                    ['Q0', 'Q1'])], ['Q0', 'Q1'])] + TAIL, LOOP_FPGA,
     sc.compile_circuit)
 
+# test_compiler.py:518-559: a phase register bound to Q0.freq (hardware virtual z)
+GOLDEN_CASES['test_hw_virtualz_out'] = (
+    [{'name': 'declare', 'var': 'q0_phase', 'scope': ['Q0'], 'dtype': 'phase'},
+     {'name': 'bind_phase', 'var': 'q0_phase', 'freq': 'Q0.freq'},
+     {'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1']},
+     {'name': 'virtual_z', 'qubit': 'Q0', 'phase': np.pi / 2},
+     {'name': 'X90', 'qubit': ['Q0']}, {'name': 'read', 'qubit': ['Q0']}], TEST_FPGA, sc.compile_circuit)
+
+
+def test_every_compiler_golden_covered():
+    with open(os.path.join(GOLDEN, 'asm_inputs.json')) as f:
+        assert sorted(json.load(f)['programs']) == sorted(GOLDEN_CASES)
+
 
 def compile_case(name):
     prog, cfg, fn = GOLDEN_CASES[name]
