@@ -36,9 +36,8 @@ time (``:641-649``).
   ``branch_fproc`` / ``branch_var`` / ``loop`` circuits, with ``declare``,
   ``set_var``, ``alu``, ``read_fproc`` / ``alu_fproc`` compiled as in
   ``compiler.py:283-320``, variable registration (``:253-283``) and
-  hardware virtual z (``bind_phase``, ResolveHWVirtualZ ``:405-437``).  Not
-  restated: RescopeVars (``:554-593``, which only widens a variable's scope
-  when it is used outside the scope it was declared in).
+  hardware virtual z (``bind_phase``, ResolveHWVirtualZ ``:405-437``) and
+  RescopeVars (``:563-593``).
 
 Parity: ``tests/test_schedule.py`` reproduces the reference's scheduling
 asserts (``python/test/test_compiler.py:75-98``), its user-schedule lint
@@ -756,13 +755,16 @@ def register_vars(blocks) -> Dict[str, dict]:
     for instrs in blocks.values():
         for ins in instrs:
             if ins.name == 'declare':
-                vars_[ins.var] = {'scope': set(ins.scope or ()), 'dtype': ins.dtype}
+                if ins.scope is None:
+                    ins.scope = set()
+                # the variable shares the declare's scope set, as register_var does (ir.py)
+                vars_[ins.var] = {'scope': ins.scope, 'dtype': ins.dtype}
             elif ins.name == 'alu':
                 ins.scope = vars_[ins.rhs]['scope'] | (vars_[ins.lhs]['scope'] if isinstance(ins.lhs, str) else set())
                 if not vars_[ins.out]['scope'] <= ins.scope:
                     raise AssertionError('alu output {} is scoped wider than its inputs'.format(ins.out))
             elif ins.name in ('set_var', 'read_fproc'):
-                ins.scope = set(vars_[ins.var]['scope'])
+                ins.scope = vars_[ins.var]['scope']
             elif ins.name == 'alu_fproc' and isinstance(ins.lhs, str):
                 ins.scope = set(vars_[ins.rhs]['scope'])
     return vars_
@@ -789,6 +791,33 @@ def resolve_hw_virtual_z(prog: ScheduleIR, vars_: Dict[str, dict]):
                 ins.phase = bound[ins.freq]
             elif ins.name == 'gate':
                 raise Exception('All Gate instructions must be resolved before running this pass!')
+
+
+def rescope_vars(prog: ScheduleIR, vars_: Dict[str, dict]):
+    """``ir/passes.py:563-593`` (RescopeVars): a variable used as a pulse
+    phase on a channel outside its scope, or in a conditional jump scoped
+    wider than it, widens its scope; the declare / set_var / alu
+    instructions of that block are rescoped to the variable's scope."""
+    for node in prog.topological_order():
+        il = prog.blocks[node]['instructions']
+        rescope = False
+        for ins in il:
+            if ins.name == 'pulse':
+                if isinstance(ins.phase, str) and ins.phase in vars_ and ins.dest not in vars_[ins.phase]['scope']:
+                    rescope = True
+                    vars_[ins.phase]['scope'].add(ins.dest)
+            elif ins.name in ('jump_cond', 'jump_fproc'):
+                sides = [ins.cond_lhs] + ([ins.cond_rhs] if ins.name == 'jump_cond' else [])
+                for v in sides:
+                    if isinstance(v, str) and v in vars_ and not set(ins.scope) <= vars_[v]['scope']:
+                        vars_[v]['scope'] = vars_[v]['scope'] | set(ins.scope)
+                        rescope = True
+        if rescope:
+            for ins in il:
+                if ins.name in ('declare', 'set_var'):
+                    ins.scope = vars_[ins.var]['scope']
+                elif ins.name in ('alu', 'rc_alu'):
+                    ins.scope = vars_[ins.out]['scope']
 
 
 def resolve_fproc_channels(prog: ScheduleIR, fpga_config: FPGAConfig):
@@ -820,8 +849,8 @@ def compile_circuit(program: Sequence, table: GateTable, fpga_config: FPGAConfig
     ``loop``) -> CompiledProgram, in
     the reference's pass order (``compiler.py:149-174``): FlattenProgram,
     MakeBasicBlocks, ScopeProgram, ResolveGates, GenerateCFG, ResolveVirtualZ,
-    ResolveFreqs, ResolveFPROCChannels, Schedule (or LintSchedule), compile.
-    RescopeVars is not restated."""
+    ResolveHWVirtualZ, ResolveFreqs, ResolveFPROCChannels, RescopeVars,
+    Schedule (or LintSchedule), compile."""
     blocks = make_basic_blocks(flatten(program))
     scopes = scope_blocks(blocks, qubit_grouping)
     vars_ = register_vars(blocks)
@@ -836,6 +865,7 @@ def compile_circuit(program: Sequence, table: GateTable, fpga_config: FPGAConfig
     for b in prog.blocks.values():
         resolve_freqs(b['instructions'], table)
     resolve_fproc_channels(prog, fpga_config)
+    rescope_vars(prog, vars_)
     (Schedule if schedule else LintSchedule)(fpga_config, proc_grouping).run_pass(prog)
     out = CompiledProgram(compile_blocks(prog, proc_grouping), fpga_config)
     out.ir = prog

@@ -438,3 +438,17 @@ def test_schedules_are_never_late_gpu():
                     flags = _abi.unpack_summary(np.asarray(s).view(np.uint32))['flags']
                     assert (flags & _abi.F_LATE).tolist() == (oracle_flags([words]) & _abi.F_LATE).tolist(), \
                         (cfg.jump_fproc_clks, func_ids, core)
+
+
+def test_rescope_vars_widens_phase_register():
+    """passes.py:563-593 (hand-derived): a phase register declared on Q0 but
+    bound to Q1.freq is used by a Q1 pulse, so its declare / set_var are
+    rescoped to Q1's core too and the pulse waits for the set_var there"""
+    prog = [{'name': 'declare', 'var': 'q_phase', 'scope': ['Q0'], 'dtype': 'phase'},
+            {'name': 'bind_phase', 'var': 'q_phase', 'freq': 'Q1.freq'},
+            {'name': 'X90', 'qubit': ['Q1']}]
+    got = sc.compile_circuit(prog, TABLE, TEST_FPGA).program
+    q0, q1 = got[('Q0.qdrv', 'Q0.rdrv', 'Q0.rdlo')], got[('Q1.qdrv', 'Q1.rdrv', 'Q1.rdlo')]
+    assert [s['op'] for s in q0] == ['phase_reset', 'declare_reg', 'reg_alu', 'done_stb']
+    assert [s['op'] for s in q1] == ['phase_reset', 'declare_reg', 'reg_alu', 'pulse', 'done_stb']
+    assert q1[3]['phase'] == 'q_phase' and q1[3]['start_time'] == 5 + TEST_FPGA.alu_instr_clks
