@@ -452,3 +452,87 @@ def test_rescope_vars_widens_phase_register():
     assert [s['op'] for s in q0] == ['phase_reset', 'declare_reg', 'reg_alu', 'done_stb']
     assert [s['op'] for s in q1] == ['phase_reset', 'declare_reg', 'reg_alu', 'pulse', 'done_stb']
     assert q1[3]['phase'] == 'q_phase' and q1[3]['start_time'] == 5 + TEST_FPGA.alu_instr_clks
+
+
+def random_circuit(rng, decls, depth=0):
+    """gates, fproc branches on the cores' own measurements and counted loops
+    (a loop register incremented in the body, so every shot terminates).
+    Declarations go to ``decls`` (the program head): as in the reference
+    assembler, a jump label cannot land on a declare_reg."""
+    prog = []
+    for _ in range(int(rng.integers(2, 7))):
+        q = ['Q0', 'Q1'][rng.integers(2)]
+        r = rng.random()
+        if r < 0.2 and depth < 2:
+            prog.append({'name': 'read', 'qubit': [q]})
+            prog.append({'name': 'branch_fproc', 'alu_cond': 'eq', 'cond_lhs': int(rng.integers(2)),
+                         'func_id': q + '.meas', 'scope': [q],
+                         'true': random_circuit(rng, decls, depth + 1) if rng.random() < 0.5 else [],
+                         'false': [{'name': 'X90', 'qubit': [q]}]})
+        elif r < 0.3 and depth < 2:
+            var = 'i{}'.format(len(decls))
+            decls.append({'name': 'declare', 'var': var, 'dtype': 'int', 'scope': ['Q0', 'Q1']})
+            # scoped explicitly: the block's scope comes from ScopeProgram, which
+            # runs before variables are registered (passes.py:207-223, 278-279)
+            prog.append({'name': 'set_var', 'var': var, 'value': 0, 'scope': ['Q0', 'Q1']})
+            body = [{'name': 'X90', 'qubit': [q]},
+                    {'name': 'alu', 'op': 'add', 'lhs': 1, 'rhs': var, 'out': var}]
+            prog.append({'name': 'loop', 'cond_lhs': int(rng.integers(1, 4)), 'cond_rhs': var, 'alu_cond': 'ge',
+                         'scope': ['Q0', 'Q1'], 'body': body})
+        else:
+            gates = GATES[q] if depth == 0 else [g for g in GATES[q] if 'Z' not in g]
+            prog.append({'name': gates[rng.integers(len(gates))], 'qubit': [q]})
+    return prog
+
+
+def test_conditional_virtual_z_is_rejected():
+    """passes.py:459-467: branches that leave a frequency at different
+    virtual-z phases cannot merge (software z needs one phase per point; a
+    branch that never touched the frequency does not conflict)"""
+    circ = [{'name': 'Z90', 'qubit': ['Q0']}, {'name': 'read', 'qubit': ['Q0']},
+            {'name': 'branch_fproc', 'alu_cond': 'eq', 'cond_lhs': 1, 'func_id': 'Q0.meas', 'scope': ['Q0'],
+             'true': [{'name': 'Z90', 'qubit': ['Q0']}], 'false': [{'name': 'X90', 'qubit': ['Q0']}]},
+            {'name': 'X90', 'qubit': ['Q0']}]
+    with pytest.raises(ValueError, match='Phase mismatch'):
+        sc.compile_circuit(circ, TABLE, hw.FPGAConfig())
+
+
+def compiled_circuits(n_cases=12, seed=11):
+    rng = np.random.default_rng(seed)
+    for k in range(n_cases):
+        decls = []
+        body = random_circuit(rng, decls)
+        circ = decls + body + [{'name': 'read', 'qubit': ['Q0']}, {'name': 'read', 'qubit': ['Q1']}]
+        yield k, circ, assemble(sc.compile_circuit(circ, TABLE, hw.FPGAConfig()))
+
+
+def circuit_config(C, k):
+    return _abi.make_config(C, max_cycles=1 << 20, event_cap=96, trace_cap=64, meas_cap=16, p1=0.5, seed=k)
+
+
+def test_compiled_circuits_run_on_oracle():
+    """circuit -> compile_circuit -> assemble -> oracle_fast: every lane of
+    every shot finishes, with at least the two closing readouts measured"""
+    import oracle
+    from distributed_processor_amd.emulator import ProgramSet
+    for k, circ, asm in compiled_circuits():
+        ps = ProgramSet([asm])
+        cfg = circuit_config(ps.cores_per_shot, k)
+        f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, 64, want=('summary',))
+        s = _abi.unpack_summary(f['summary'])
+        assert (s['status'] == _abi.ST_DONE).all(), (k, circ)
+        assert (s['n_meas'] >= 1).all(), k
+
+
+@pytest.mark.gpu
+def test_compiled_circuits_gpu_vs_oracle():
+    """the same compiled circuits (branches on measurements, counted loops) on
+    cuda:0, bit-exact against oracle_fast on every output"""
+    from distributed_processor_amd.emulator import Emulator, ProgramSet
+    from tests.test_gpu_parity import compare_all, run_pair
+    with Emulator(0) as emu:
+        for k, circ, asm in compiled_circuits():
+            ps = ProgramSet([asm])
+            g, f = run_pair(emu, ps, circuit_config(ps.cores_per_shot, k), 2000, shot0=97 * k)
+            compare_all(g, f, 'circuit {}'.format(k))
+            assert (_abi.unpack_summary(g['summary'])['status'] == _abi.ST_DONE).all(), k
