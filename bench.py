@@ -46,6 +46,22 @@ def build_workload(n_points=100, n_cores=8):
     return ProgramSet(workloads.config2_ramsey(n_cores=n_cores, n_points=n_points))
 
 
+def kernel_pass(emu, steps, step, drain=None):
+    """Run `steps` more steps with the library's HIP events recorded around
+    each main kernel launch (dpemu_set_kernel_timing), outside the timed
+    region; emu.kernel_times() then holds one duration per launch."""
+    import torch
+    torch.cuda.synchronize()
+    emu.kernel_times()                                # drop earlier records
+    emu.kernel_timing(True)
+    for _ in range(steps):
+        step()
+    if drain is not None:
+        drain()
+    torch.cuda.synchronize()
+    emu.kernel_timing(False)
+
+
 def bytes_per_lane(summary_np, cfg):
     """algorithmic HBM bytes written per lane: 32 B summary + 18 B per event
     (16 B record + 2 B amplitude) + 8 B per measurement record"""
@@ -134,8 +150,6 @@ def dds_leg(emu, args, world, rank, stream):
     for _ in range(args.warmup):
         emu.synthesize(plan, ev, n_samples, iq, stream)
     torch.cuda.synchronize()
-    emu.kernel_times()                                # drop earlier records
-    emu.kernel_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -146,7 +160,7 @@ def dds_leg(emu, args, world, rank, stream):
     if world > 1:
         dist.barrier()
     dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
-    emu.kernel_timing(False)
+    kernel_pass(emu, args.steps, lambda: emu.synthesize(plan, ev, n_samples, iq, stream))
     kt = emu.kernel_times()
     assert len(kt) == args.steps, kt
     kernel_ms = float(np.mean(kt))                    # HIP events around the DDS kernel, same stream
@@ -197,8 +211,6 @@ def active_reset_leg(emu, args, world, rank, stream):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    emu.kernel_times()
-    emu.kernel_timing(True)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -209,7 +221,7 @@ def active_reset_leg(emu, args, world, rank, stream):
     if world > 1:
         torch.distributed.barrier()
     dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
-    emu.kernel_timing(False)
+    kernel_pass(emu, args.steps, step)
     kt = emu.kernel_times()
     kernel_ms = float(np.mean(kt))
     summ = out['summary'].cpu().numpy().view(np.uint32)
@@ -321,7 +333,6 @@ def main():
     drain()
     torch.cuda.synchronize()
 
-    emu.kernel_timing(True)                           # HIP events around the interpreter kernel
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -333,7 +344,10 @@ def main():
     if world > 1:
         dist.barrier()
     dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
-    emu.kernel_timing(False)
+    # the roofline's kernel time: a second pass of the same steps with HIP
+    # events recorded around the interpreter kernel, so the event records stay
+    # out of the timed region (they cost ~4 % of a step)
+    kernel_pass(emu, args.steps, step, drain)
     kt = emu.kernel_times()
     assert len(kt) == args.steps, kt
     kernel_ms = float(np.mean(kt))
