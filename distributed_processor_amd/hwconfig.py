@@ -112,6 +112,15 @@ class FPGAConfig:
     def fpga_clk_freq(self):
         return 1 / self.fpga_clk_period
 
+    @classmethod
+    def rtl_exact(cls, fpga_clk_period=2.e-9, pulse_regwrite_clks=3):
+        """the scheduler constants set to the RTL's decode-to-decode cycle
+        counts (``EXACT_LATENCIES``): schedules made with it never put a pulse
+        before the core can issue it (``tests/test_schedule.py``)"""
+        return cls(fpga_clk_period=fpga_clk_period, pulse_regwrite_clks=pulse_regwrite_clks,
+                   **{k: EXACT_LATENCIES[k] for k in ('alu_instr_clks', 'jump_cond_clks', 'jump_fproc_clks',
+                                                       'pulse_load_clks')})
+
 
 # Decode-to-decode cycle counts of the RTL (ctrl.v; SURVEY.md §2.4).
 EXACT_LATENCIES = {'alu_instr_clks': 4, 'jump_cond_clks': 6, 'jump_fproc_clks': 8,

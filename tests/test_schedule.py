@@ -204,8 +204,8 @@ def test_branch_schedules_vs_rtl_latencies(func_ids):
     linter says ``late``.  With the reference's default FPGAConfig and with
     the RTL's exact latencies no lane is late."""
     from tests.test_lint import oracle_flags
-    exact = hw.FPGAConfig(**{k: v for k, v in hw.EXACT_LATENCIES.items()
-                             if k in ('alu_instr_clks', 'jump_cond_clks', 'jump_fproc_clks', 'pulse_load_clks')})
+    exact = hw.FPGAConfig.rtl_exact()
+    assert (exact.jump_cond_clks, exact.jump_fproc_clks, exact.alu_instr_clks) == (6, 8, 4)
     for cfg, want_late in ((TEST_FPGA, True), (hw.FPGAConfig(), False), (exact, False)):
         asm = assemble(sc.compile_circuit(two_resets(*func_ids), TABLE, cfg))
         late = []
