@@ -4,7 +4,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_CORES = 64
 MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
 
@@ -36,7 +36,7 @@ class Config(C.Structure):
                 ('lut_mask', C.c_uint32), ('meas_model', C.c_uint32),
                 ('p1_threshold', C.c_uint32 * MAX_CORES), ('lut_table', C.c_uint64 * 256),
                 ('ro_sep', C.c_int32), ('ro_sigma', C.c_uint32), ('ro_thr', C.c_int32),
-                ('reserved2', C.c_uint32)]
+                ('ro_win', C.c_uint32)]
 
 
 class Outputs(C.Structure):
@@ -100,6 +100,10 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
             raise ValueError('readout sep / thr must fit int32 and sigma * 2^16 uint32')
         cfg.meas_model = MEAS_READOUT
         cfg.ro_sep, cfg.ro_sigma, cfg.ro_thr = sep, sigma, thr
+        win = int(readout.get('win', 0))
+        if not 0 <= win < 2 ** 12:
+            raise ValueError('readout win must fit the 12-bit envelope-length field')
+        cfg.ro_win = win
     return cfg
 
 

@@ -357,6 +357,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.sync_mask = cfg->sync_mask ? (cfg->sync_mask & all) : all;
     p.seed = cfg->seed;
     p.meas_model = cfg->meas_model; p.ro_sep = cfg->ro_sep; p.ro_thr = cfg->ro_thr; p.ro_sigma = cfg->ro_sigma;
+    p.ro_win = cfg->ro_win;
+    p.ro_wrecip = cfg->ro_win ? (1u << 24) / cfg->ro_win : 0u;
     p.lut_mask = cfg->lut_mask;
     const uint64_t guard = (uint64_t)C * (cfg->max_cycles / 3u + 4u) + 1024u;
     p.iter_guard = guard > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)guard;

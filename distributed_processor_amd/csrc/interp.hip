@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         } else flags |= F_EVENT_OVF;
         n_ev++;
         if (kind == 0 && p.meas_elem != 0xFFu && ((pe >> 24) & 3u) == p.meas_elem) {
-            const uint32_t bit = meas_bit(p, shot, core, n_meas, thr_core, pa);
+            const uint32_t bit = meas_bit(p, shot, core, n_meas, thr_core, pa, pe);
             const uint32_t tv = te + p.meas_latency;
             if constexpr (XMEAS) {
                 if (n_meas < MEAS_LOOKUP) s_mt[n_meas < MT ? n_meas : 0][tid] = (tv << 1) | bit;

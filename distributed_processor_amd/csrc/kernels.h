@@ -125,7 +125,7 @@ struct KParams {
     uint32_t lut_mask;
     uint32_t meas_model;          // DPEMU_MEAS_STATE / DPEMU_MEAS_READOUT (ro_*: include/dpemu.h)
     int32_t ro_sep, ro_thr;
-    uint32_t ro_sigma;
+    uint32_t ro_sigma, ro_win, ro_wrecip;   // ro_wrecip = floor(2^24 / ro_win)
     uint32_t iter_guard;
     uint32_t shot_order, rows;    // 1: group-major thread order (shots_per_group 1, n = rows * n_groups)
     uint32_t prog_lds_words;      // dynamic LDS commands (FEAT_PROG_LDS)

@@ -57,15 +57,21 @@ __device__ __forceinline__ uint3 philox3(uint64_t seed, uint64_t shot, uint32_t 
 // measurement outcome (oracle/philox.c oracle_meas_bit; include/dpemu.h): the
 // prepared state against thr, or with meas_model READOUT the discriminated
 // readout x = +-(ro_sep * amp >> 16) + (z * ro_sigma >> 16) > ro_thr, z the
-// centred Irwin-Hall(4) sum of the 16-bit halves of Philox words 1 and 2
+// centred Irwin-Hall(4) sum of the 16-bit halves of Philox words 1 and 2;
+// with ro_win the separation scales by min(W, ro_win) * floor(2^24 / ro_win)
+// / 2^24, W = the env word's length field (bits 23:12)
 __device__ __forceinline__ uint32_t meas_bit(const KParams &p, uint64_t shot, uint32_t core, uint32_t m,
-                                             uint32_t thr, uint32_t amp)
+                                             uint32_t thr, uint32_t amp, uint32_t env)
 {
     const uint3 r = philox3(p.seed, shot, core, m);
     const uint32_t state = (thr == 0xFFFFFFFFu) || (r.x < thr);
     if (p.meas_model != DPEMU_MEAS_READOUT) return state;
     const int64_t z = (int64_t)((r.y & 0xFFFFu) + (r.y >> 16) + (r.z & 0xFFFFu) + (r.z >> 16)) - 131070;
-    const int64_t s = ((int64_t)p.ro_sep * (int64_t)(amp & 0xFFFFu)) >> 16;
+    int64_t s = ((int64_t)p.ro_sep * (int64_t)(amp & 0xFFFFu)) >> 16;
+    if (p.ro_win) {     // no division on the device: floor(2^24 / ro_win) comes from the host
+        const uint32_t w = (env >> 12) & 0xFFFu;
+        s = (s * (int64_t)((w < p.ro_win ? w : p.ro_win) * p.ro_wrecip)) >> 24;
+    }
     const int64_t x = (state ? s : -s) + ((z * (int64_t)p.ro_sigma) >> 16);
     return x > (int64_t)p.ro_thr;
 }

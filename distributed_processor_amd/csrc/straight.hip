@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         const bool is_meas = ok && kind == 0u && ((pe >> 24) & 3u) == p.meas_elem;   // meas_elem 0xFF: none
         uint32_t bit = 0;
         if (is_meas) {
-            bit = meas_bit(p, shot, core, n_meas, thr, pa);
+            bit = meas_bit(p, shot, core, n_meas, thr, pa, pe);
             if (p.meas && n_meas < p.meas_cap)
                 p.meas[(uint64_t)n_meas * n_lanes + lane] = make_uint2(te + p.meas_latency, bit);
         }

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DPEMU_ABI_VERSION 2
+#define DPEMU_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------- */
 #define DPEMU_OK            0
@@ -111,11 +111,15 @@ typedef struct dpemu_config {
     /* readout model (meas_model = DPEMU_MEAS_READOUT), per readout strobe with amp word A:
      *   z = Irwin-Hall(4) of the 16-bit halves of Philox words 1, 2, minus 131070
      *   x = (state ? +1 : -1) * ((ro_sep * A) >> 16) + ((z * ro_sigma) >> 16)   (int64)
-     *   outcome = x > ro_thr                                                       */
+     *   outcome = x > ro_thr
+     * with ro_win != 0 the separation also scales with the readout window:
+     *   s = (s * (min(W, ro_win) * floor(2^24 / ro_win))) >> 24   (int64)
+     * W = the strobe's envelope-length field (env word bits 23:12, in env words)
+     * -- a window shorter than ro_win integrates less signal                  */
     int32_t  ro_sep;           /* half the state separation at full readout amplitude    */
     uint32_t ro_sigma;         /* noise scale, Q16 (noise sigma = ro_sigma / 2^16 * 37837.6) */
     int32_t  ro_thr;           /* discriminator threshold                                */
-    uint32_t reserved2;
+    uint32_t ro_win;           /* reference readout window (env words); 0 = amplitude only */
 } dpemu_config;
 
 #define DPEMU_MEAS_STATE   0

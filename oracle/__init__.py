@@ -61,7 +61,7 @@ class ShotCfg(C.Structure):
                 ('sync_mask', C.c_uint64), ('seed', C.c_uint64), ('lut_mask', C.c_uint32),
                 ('p1_threshold', C.c_uint32 * 64), ('lut_table', C.c_uint64 * 256),
                 ('meas_model', C.c_uint32), ('ro_sep', C.c_int32), ('ro_sigma', C.c_uint32),
-                ('ro_thr', C.c_int32)]
+                ('ro_thr', C.c_int32), ('ro_win', C.c_uint32)]
 
 
 class LaneOut(C.Structure):
@@ -300,6 +300,7 @@ def shot_cfg_from_config(cfg):
     for i in range(256):
         s.lut_table[i] = cfg.lut_table[i]
     s.meas_model, s.ro_sep, s.ro_sigma, s.ro_thr = cfg.meas_model, cfg.ro_sep, cfg.ro_sigma, cfg.ro_thr
+    s.ro_win = cfg.ro_win
     return s
 
 

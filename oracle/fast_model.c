@@ -99,7 +99,8 @@ static void emit_event(fshot *s, flane *l, uint32_t t, uint32_t kind)
         uint32_t core = l->lane % s->C;
         uint32_t m = l->n_meas;
         uint32_t bit = oracle_meas_bit(cfg->seed, s->shot, core, m, cfg->p1_threshold[core], l->pr[3],
-                                       cfg->meas_model, cfg->ro_sep, cfg->ro_sigma, cfg->ro_thr);
+                                       cfg->meas_model, cfg->ro_sep, cfg->ro_sigma, cfg->ro_thr,
+                                       cfg->ro_win, l->pr[0]);
         uint32_t tv = t + cfg->meas_latency;
         if (m < MEAS_LOOKUP) { l->mt[m] = tv; l->mb[m] = (uint8_t)bit; }
         if (m < cfg->meas_cap) {

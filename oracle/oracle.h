@@ -30,7 +30,8 @@ void oracle_philox4(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m, uin
  * thr, or (meas_model READOUT) the discriminated readout of a pulse with amp
  * word `amp` (include/dpemu.h, dpemu_config) */
 uint32_t oracle_meas_bit(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m, uint32_t thr, uint32_t amp,
-                         uint32_t meas_model, int32_t ro_sep, uint32_t ro_sigma, int32_t ro_thr);
+                         uint32_t meas_model, int32_t ro_sep, uint32_t ro_sigma, int32_t ro_thr,
+                         uint32_t ro_win, uint32_t env);
 
 /* ---- per-clock model ---------------------------------------------------- */
 typedef struct {
@@ -85,6 +86,7 @@ typedef struct {
     int32_t ro_sep;
     uint32_t ro_sigma;
     int32_t ro_thr;
+    uint32_t ro_win;
 } oracle_shot_cfg;
 
 #define RTL_MQ 64

@@ -44,9 +44,11 @@ uint32_t oracle_philox_u32(uint64_t seed, uint64_t shot, uint32_t core, uint32_t
  *             the discriminator axis, x = +-(ro_sep * amp >> 16) + (z * ro_sigma >> 16)
  *             with z = Irwin-Hall(4) of the 16-bit halves of r1, r2, centred
  *             (|z| <= 131070, sigma 37837.6); outcome = x > ro_thr.  A weaker
- *             readout pulse (amp word) separates the states less. */
+ *             readout pulse (amp word) separates the states less; with ro_win
+ *             a window shorter than ro_win env words (env bits 23:12) does too. */
 uint32_t oracle_meas_bit(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m, uint32_t thr, uint32_t amp,
-                         uint32_t meas_model, int32_t ro_sep, uint32_t ro_sigma, int32_t ro_thr)
+                         uint32_t meas_model, int32_t ro_sep, uint32_t ro_sigma, int32_t ro_thr,
+                         uint32_t ro_win, uint32_t env)
 {
     uint32_t r[4];
     oracle_philox4(seed, shot, core, m, r);
@@ -54,6 +56,10 @@ uint32_t oracle_meas_bit(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m
     if (meas_model != DPEMU_MEAS_READOUT) return state;
     int64_t z = (int64_t)(r[1] & 0xFFFFu) + (r[1] >> 16) + (r[2] & 0xFFFFu) + (r[2] >> 16) - 131070;
     int64_t s = ((int64_t)ro_sep * (int64_t)(amp & 0xFFFFu)) >> 16;
+    if (ro_win) {   /* window: (s * min(W, ro_win) * floor(2^24 / ro_win)) >> 24, W = env bits 23:12 */
+        uint32_t w = (env >> 12) & 0xFFFu;
+        s = (s * (int64_t)((w < ro_win ? w : ro_win) * ((1u << 24) / ro_win))) >> 24;
+    }
     int64_t x = (state ? s : -s) + ((z * (int64_t)ro_sigma) >> 16);
     return x > (int64_t)ro_thr;
 }

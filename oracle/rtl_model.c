@@ -371,7 +371,8 @@ void rtl_shot_step(rtl_shot *s, const rtl_ext_inputs *ext)
         if (o->cstrobe && s->cfg.meas_elem != 0xFF && (o->cfg & 3) == s->cfg.meas_elem) {
             uint32_t m = s->n_meas[c]++;
             int bit = (int)oracle_meas_bit(s->cfg.seed, s->shot, c, m, s->cfg.p1_threshold[c], o->amp,
-                                           s->cfg.meas_model, s->cfg.ro_sep, s->cfg.ro_sigma, s->cfg.ro_thr);
+                                           s->cfg.meas_model, s->cfg.ro_sep, s->cfg.ro_sigma, s->cfg.ro_thr,
+                                           s->cfg.ro_win, o->env);
             rtl_meas_q *q = &s->mq[c];
             q->t[q->tail % RTL_MQ] = s->cycle + s->cfg.meas_latency;
             q->bit[q->tail % RTL_MQ] = (uint8_t)bit;

@@ -137,6 +137,7 @@ def test_fuzz_readout_model(seed):
     readout of each strobe's amp word, driving fproc branches in both models"""
     case = random_case(4000 + seed, ncores=[1, 2, 4][seed % 3], mode=['meas', 'lut'][seed % 2],
                        allow_late=False, allow_hang=False)
-    ro = dict(sep=[40000, 5000, -30000, 0][seed % 4], sigma=[0.5, 1.0, 0.1, 2.0][seed % 4], thr=[0, 1000, -500][seed % 3])
+    ro = dict(sep=[40000, 5000, -30000, 0][seed % 4], sigma=[0.5, 1.0, 0.1, 2.0][seed % 4], thr=[0, 1000, -500][seed % 3],
+              win=[0, 7, 300, 4095][(seed // 4) % 4])
     cfg, fast, rtl = run_both(case, n_shots=3, meas_latency=1 + seed % 9, readout=ro)
     compare(cfg, fast, rtl, 3)

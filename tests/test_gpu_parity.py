@@ -238,7 +238,7 @@ def test_fuzz_readout_model(emu, seed):
     cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=6000, event_cap=64, trace_cap=64, meas_cap=16,
                            fproc_mode=mode, meas_latency=1 + seed % 13, seed=seed, p1=0.4,
                            readout=dict(sep=[25000, -8000, 60000][seed % 3], sigma=[0.7, 1.5, 0.2][seed % 3],
-                                        thr=[0, -1500, 900][seed % 3]))
+                                        thr=[0, -1500, 900][seed % 3], win=[0, 40, 900, 4095][seed % 4]))
     g, f = run_pair(emu, ps, cfg, 257, shot0=seed * 977)
     compare_all(g, f, 'readout seed {}'.format(seed))
 
