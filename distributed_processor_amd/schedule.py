@@ -37,7 +37,10 @@ time (``:641-649``).
   ``set_var``, ``alu``, ``read_fproc`` / ``alu_fproc`` compiled as in
   ``compiler.py:283-320``, variable registration (``:253-283``) and
   hardware virtual z (``bind_phase``, ResolveHWVirtualZ ``:405-437``) and
-  RescopeVars (``:563-593``).
+  RescopeVars (``:563-593``).  Addition: a ``sync`` statement
+  (``{'name': 'sync', 'scope': [...], 'barrier_id': id}``, the barrier
+  ``compiler.py:78-82`` documents), scheduled as a qclk restart of its scope
+  (build-defined) and compiled to the assembler's ``sync``.
 
 Parity: ``tests/test_schedule.py`` reproduces the reference's scheduling
 asserts (``python/test/test_compiler.py:75-98``), its user-schedule lint
@@ -290,6 +293,14 @@ class Schedule:
                 else:
                     instructions.pop(i)
                     continue
+            elif ins.name == 'sync':
+                # build-defined (the reference schedules no sync): qclk restarts
+                # at the barrier (hdl: qclk(S+2) = 0), so the scope's channel
+                # and core clocks restart like after reset
+                for d in ins.scope:
+                    cur_t[d] = self._start_nclks
+                for g in groups(ins.scope):
+                    last_end[g] = self._start_nclks
             elif ins.name == 'latch_rc_cycle':                       # :726-730
                 t = max(last_end[g] for g in groups(ins.scope))
                 ins.t = t
@@ -341,6 +352,9 @@ class LintSchedule:
             elif ins.name in cost:
                 for g in self._core_scoper.get_groups_bydest(ins.scope):
                     last_end[g] += cost[ins.name]
+            elif ins.name == 'sync':
+                for g in self._core_scoper.get_groups_bydest(ins.scope):
+                    last_end[g] = START_NCLKS
             elif ins.name == 'idle':
                 for g in self._core_scoper.get_groups_bydest(ins.scope):
                     if ins.end_time < last_end[g]:
@@ -504,6 +518,9 @@ def compile_blocks(prog: ScheduleIR, proc_grouping=DEFAULT_PROC_GROUPING) -> Dic
             elif ins.name == 'loop_end':
                 for g in scoper.get_groups_bydest(ins.scope):
                     progs[g].append({'op': 'inc_qclk', 'in0': -prog.loops[ins.loop_label]['delta_t']})
+            elif ins.name == 'sync':          # the barrier compiler.py:78-82 documents
+                for g in scoper.get_groups_bydest(ins.scope):
+                    progs[g].append({'op': 'sync', 'barrier_id': ins.barrier_id or 0})
             elif ins.name == 'declare':                              # compiler.py:283-287
                 dtype = (ins.dtype, 0) if ins.dtype in ('phase', 'amp') else ins.dtype
                 for g in scoper.get_groups_bydest(ins.scope):
@@ -560,7 +577,7 @@ def compile_straight(program: Sequence[dict], table: GateTable, fpga_config: FPG
 
 # ---------------------------------------------------------------- control flow
 # circuit statements that are already IR instructions (ir/instructions.py)
-_IR_STATEMENTS = ('declare', 'bind_phase', 'set_var', 'alu', 'read_fproc', 'alu_fproc', 'hold', 'idle', 'jump_label',
+_IR_STATEMENTS = ('sync', 'declare', 'bind_phase', 'set_var', 'alu', 'read_fproc', 'alu_fproc', 'hold', 'idle', 'jump_label',
                   'jump_i', 'jump_cond', 'jump_fproc')
 
 def flatten(program: Sequence, label_prefix: str = '') -> List[Instr]:

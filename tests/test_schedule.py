@@ -536,3 +536,57 @@ def test_compiled_circuits_gpu_vs_oracle():
             g, f = run_pair(emu, ps, circuit_config(ps.cores_per_shot, k), 2000, shot0=97 * k)
             compare_all(g, f, 'circuit {}'.format(k))
             assert (_abi.unpack_summary(g['summary'])['status'] == _abi.ST_DONE).all(), k
+
+
+def sync_circuits(n_cases=10, seed=23):
+    """random circuits cut into segments by whole-circuit syncs, scheduled with
+    the RTL's latencies"""
+    rng = np.random.default_rng(seed)
+    for k in range(n_cases):
+        decls, body = [], []
+        for j in range(int(rng.integers(2, 4))):
+            body += random_circuit(rng, decls)
+            body.append({'name': 'sync', 'scope': ['Q0', 'Q1'], 'barrier_id': j})
+        circ = decls + body + [{'name': 'read', 'qubit': ['Q0']}, {'name': 'read', 'qubit': ['Q1']}]
+        yield k, circ, assemble(sc.compile_circuit(circ, TABLE, hw.FPGAConfig.rtl_exact()))
+
+
+def test_sync_statement_schedules_from_the_barrier():
+    """build-defined sync scheduling: qclk restarts at the barrier, so the
+    first pulse after it is placed as after reset; compiled to the assembler's
+    sync statement on every core of its scope"""
+    circ = [{'name': 'read', 'qubit': ['Q0']}, {'name': 'sync', 'scope': ['Q0', 'Q1'], 'barrier_id': 3},
+            {'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1']}]
+    prog = sc.compile_circuit(circ, TABLE, hw.FPGAConfig()).program
+    for g, st in prog.items():
+        ops = [s['op'] for s in st]
+        assert {'op': 'sync', 'barrier_id': 3} in st, g
+        after = [s for s in st[ops.index('sync'):] if s['op'] == 'pulse']
+        assert after and after[0]['start_time'] == sc.START_NCLKS, (g, after)
+
+
+def test_sync_circuits_never_late_cpu():
+    """circuits with syncs, branches and loops scheduled with FPGAConfig.rtl_exact():
+    every shot finishes and no pulse is late on oracle_fast"""
+    import oracle
+    from distributed_processor_amd.emulator import ProgramSet
+    for k, circ, asm in sync_circuits():
+        ps = ProgramSet([asm])
+        cfg = circuit_config(ps.cores_per_shot, k)
+        f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, 64, want=('summary',))
+        s = _abi.unpack_summary(f['summary'])
+        assert (s['status'] == _abi.ST_DONE).all(), (k, circ)
+        assert not (s['flags'] & _abi.F_LATE).any(), (k, circ)
+
+
+@pytest.mark.gpu
+def test_sync_circuits_gpu_vs_oracle():
+    from distributed_processor_amd.emulator import Emulator, ProgramSet
+    from tests.test_gpu_parity import compare_all, run_pair
+    with Emulator(0) as emu:
+        for k, circ, asm in sync_circuits():
+            ps = ProgramSet([asm])
+            g, f = run_pair(emu, ps, circuit_config(ps.cores_per_shot, k), 1500, shot0=31 * k)
+            compare_all(g, f, 'sync circuit {}'.format(k))
+            s = _abi.unpack_summary(g['summary'])
+            assert (s['status'] == _abi.ST_DONE).all() and not (s['flags'] & _abi.F_LATE).any(), k
