@@ -63,11 +63,11 @@ def kernel_pass(emu, steps, step, drain=None):
 
 
 def bytes_per_lane(summary_np, cfg):
-    """algorithmic HBM bytes written per lane: 32 B summary + 18 B per event
-    (16 B record + 2 B amplitude) + 8 B per measurement record"""
+    """algorithmic HBM bytes written per lane: 32 B summary + 16 B per event
+    record + 8 B per measurement record"""
     n_ev = np.minimum(summary_np[:, 2], cfg.event_cap).astype(np.float64)
     n_me = np.minimum(summary_np[:, 5], cfg.meas_cap).astype(np.float64)
-    return 32.0 + 18.0 * n_ev + 8.0 * n_me
+    return 32.0 + 16.0 * n_ev + 8.0 * n_me
 
 
 def cpu_baseline(ps, cfg, target_s=12.0):
@@ -80,7 +80,7 @@ def cpu_baseline(ps, cfg, target_s=12.0):
         pass
     threads = min(threads, 16)
     chunk = 20000
-    want = ('summary', 'ev_main', 'ev_amp', 'meas', 'hist')
+    want = ('summary', 'events', 'meas', 'hist')
     oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, 1000, threads, want)  # warm
     done = 0
     t0 = time.perf_counter()
@@ -113,7 +113,7 @@ def dds_cpu_baseline(plan, host_ev, n_samples, target_s=8.0):
     i = 0
     while time.perf_counter() - t0 < target_s and i < plan.n_channels:
         d = plan.desc[i:i + per]
-        oracle.dds(d, host_ev['summary'], host_ev['ev_main'], host_ev['ev_amp'], plan.env, plan.freq,
+        oracle.dds(d, host_ev['summary'], host_ev['events'], plan.env, plan.freq,
                    n_samples, plan.event_cap, threads)
         done += len(d) * n_samples
         i += per
@@ -135,7 +135,7 @@ def dds_leg(emu, args, world, rank, stream):
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=512, meas_cap=4,
                            meas_latency=64, seed=0x5EED)
     shot0, n = sharding.weak_shard(args.dds_seqs, rank)
-    ev = alloc_device_outputs(cfg, n, want=('summary', 'ev_main', 'ev_amp'))
+    ev = alloc_device_outputs(cfg, n, want=('summary', 'events'))
     emu.run_device(cfg, n, shot0, ev, stream)
     torch.cuda.synchronize()
     summ = ev['summary'].cpu().numpy().view(np.uint32)
@@ -180,7 +180,7 @@ def dds_leg(emu, args, world, rank, stream):
                       'samples_per_channel': n_samples, 'rb_depth': 200},
            'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                         'frac': gbs / HBM_PEAK_GBS, 'traffic': traffic, 'bytes_per_launch': samples * 4,
-                        'kernel': 'dpemu::dds_chunk_kernel<4>'}}
+                        'kernel': 'dpemu::dds_tile_kernel'}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host_ev = {k: v.cpu().numpy() for k, v in ev.items()}
         res['cpu_baseline'] = dds_cpu_baseline(plan, host_ev, n_samples, args.cpu_seconds * 2 / 3)
@@ -201,7 +201,7 @@ def active_reset_leg(emu, args, world, rank, stream):
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
                            meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5)
     n_per = args.ar_shots
-    out = alloc_device_outputs(cfg, n_per, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'))
+    out = alloc_device_outputs(cfg, n_per, want=('summary', 'events', 'meas', 'hist'))
     shot0, n = sharding.weak_shard(n_per, rank)
 
     def step():
@@ -249,7 +249,7 @@ def active_reset_leg(emu, args, world, rank, stream):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle
         threads = min(len(os.sched_getaffinity(0)), 16)
-        want = ('summary', 'ev_main', 'ev_amp', 'meas', 'hist')
+        want = ('summary', 'events', 'meas', 'hist')
         done, chunk, t0 = 0, 20000, time.perf_counter()
         while time.perf_counter() - t0 < args.cpu_seconds / 3:
             oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, done, chunk, threads, want)
@@ -302,7 +302,7 @@ def main():
     cfg = _abi.make_config(8, n_groups=ps.n_groups, shots_per_group=spg, max_cycles=1 << 20, event_cap=8,
                            trace_cap=0, meas_cap=2, meas_latency=64, seed=0x5EED, p1=0.5,
                            exec_flags=args.exec_flags)
-    out = alloc_device_outputs(cfg, n, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'))
+    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
     stream = torch.cuda.current_stream()
     shot0, n = sharding.weak_shard(n, rank)
     # double-buffered histogram: batch k's all-reduce (the path's only exchange,

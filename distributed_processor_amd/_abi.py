@@ -4,7 +4,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_CORES = 64
 MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
 
@@ -15,8 +15,8 @@ MEAS_STATE, MEAS_READOUT = 0, 1
 EV_STROBE, EV_PULSE_RESET = 0, 1
 TRACE_QCLK_LOAD, TRACE_QCLK_RST = 16, 17
 MAX_CYCLES_LIMIT = 2 ** 31 - 64
+MAX_EVENT_CAP = 1 << 20
 X_PROG_LDS = 0x1
-X_GROUP_MAJOR = 0x2
 X_HIST_DIRECT = 0x4
 X_HIST_REPL = 0x8
 X_PROG_MAJOR = 0x10
@@ -40,7 +40,7 @@ class Config(C.Structure):
 
 
 class Outputs(C.Structure):
-    _fields_ = [('summary', C.c_void_p), ('ev_main', C.c_void_p), ('ev_amp', C.c_void_p),
+    _fields_ = [('summary', C.c_void_p), ('events', C.c_void_p),
                 ('trace', C.c_void_p), ('meas', C.c_void_p), ('regs', C.c_void_p),
                 ('hist', C.c_void_p)]
 
@@ -72,6 +72,8 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
         raise ValueError('lut_mask must be nonzero')
     if meas_cap > 32:
         raise ValueError('meas_cap must be <= 32')
+    if not (0 <= event_cap <= MAX_EVENT_CAP and 0 <= trace_cap <= MAX_EVENT_CAP):
+        raise ValueError('event_cap and trace_cap must be <= 2^20')
     cfg = Config()
     cfg.cores_per_shot = C_
     cfg.n_groups = int(n_groups)
@@ -116,17 +118,30 @@ def prob_to_threshold(p):
     return min(int(round(p * 2 ** 32)), 0xFFFFFFFE)
 
 
-def alloc_host_outputs(cfg, n_shots, want=('summary', 'ev_main', 'ev_amp', 'trace', 'meas',
-                                           'regs', 'hist')):
+OUTPUT_NAMES = ('summary', 'events', 'trace', 'meas', 'regs', 'hist')
+
+
+def lane_index(shot_local, core, n_shots):
+    """output lane of (shot - shot_begin, core) in a run of n_shots shots:
+    core-major, L = core * n_shots + shot_local (include/dpemu.h)"""
+    return np.asarray(core) * int(n_shots) + np.asarray(shot_local)
+
+
+def by_shot(arr, cores_per_shot, axis=0):
+    """view of a per-lane array with the lane axis split into (core, shot)"""
+    a = np.asarray(arr)
+    shp = a.shape[:axis] + (cores_per_shot, a.shape[axis] // cores_per_shot) + a.shape[axis + 1:]
+    return a.reshape(shp)
+
+
+def alloc_host_outputs(cfg, n_shots, want=OUTPUT_NAMES):
     """numpy arrays laid out as dpemu_outputs describes (host side)."""
     n_lanes = int(n_shots) * cfg.cores_per_shot
     out = {}
     if 'summary' in want:
         out['summary'] = np.zeros((n_lanes, 8), np.uint32)
-    if 'ev_main' in want and cfg.event_cap:
-        out['ev_main'] = np.zeros((cfg.event_cap, n_lanes, 4), np.uint32)
-    if 'ev_amp' in want and cfg.event_cap:
-        out['ev_amp'] = np.zeros((cfg.event_cap, n_lanes), np.uint16)
+    if 'events' in want and cfg.event_cap:
+        out['events'] = np.zeros((cfg.event_cap, n_lanes, 4), np.uint32)
     if 'trace' in want and cfg.trace_cap:
         out['trace'] = np.zeros((cfg.trace_cap, n_lanes, 4), np.uint32)
     if 'meas' in want and cfg.meas_cap:

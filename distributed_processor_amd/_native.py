@@ -42,10 +42,10 @@ def load_library(path=LIB_PATH):
     L.dpemu_destroy.argtypes = [vp]
     L.dpemu_last_error.argtypes = [vp]
     L.dpemu_last_error.restype = C.c_char_p
-    L.dpemu_load_programs.argtypes = [vp, vp, vp, vp, u32, vp, u32, u32]
+    L.dpemu_load_programs.argtypes = [vp, vp, u64, vp, vp, u32, vp, u32, u32]
     L.dpemu_run.argtypes = [vp, vp, u64, u64, vp, vp]
     L.dpemu_run_host.argtypes = [vp, vp, u64, u64, vp]
-    L.dpemu_dds.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.dpemu_dds.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
     L.dpemu_dds_sin_lut.argtypes = [vp]
     L.dpemu_set_kernel_timing.argtypes = [vp, C.c_int]
     L.dpemu_kernel_times.argtypes = [vp, vp, C.c_int, vp]

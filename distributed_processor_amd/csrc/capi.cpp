@@ -4,6 +4,8 @@
 // cocotb testbench loaded cmd_mem word by word (cocotb/proc/test_proc.py:29-38)
 // and clocked one Verilator toplevel_sim, dpemu_load_programs uploads every
 // assembled program once and dpemu_run executes n_shots x C cores on the GPU.
+// Kernel choice depends only on the loaded programs, the grid size and the
+// caller's exec_flags -- never on the environment.
 
 #include <hip/hip_runtime.h>
 
@@ -13,7 +15,6 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
-#include <cstdlib>
 #include <vector>
 
 #include "kernels.h"
@@ -26,9 +27,10 @@ struct dpemu_ctx {
     // programs
     uint4 *d_uops = nullptr;                // decode_cmd words, program-major (KParams::uops)
     uint4 *d_uops_t = nullptr;              // command-major copy (KParams::fetch), or null
+    uint4 *d_macro = nullptr;               // macro image of branch-free ALU programs (macro.hip), or null
+    uint32_t *d_moff = nullptr;             // its per-program offsets (in macros)
     uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
     uint32_t n_programs = 0, n_groups = 0, C = 0;
-    uint64_t n_quads = 0;
     bool has_fproc = false, has_sync = false, straight = false, linear = false;
     uint32_t max_len = 0;              // longest program (commands)
     std::vector<uint64_t> group_len;   // instructions of all C programs of each group
@@ -42,20 +44,8 @@ struct dpemu_ctx {
     uint32_t *d_ch = nullptr;
     uint32_t ch_cap = 0;
     std::vector<uint32_t> ch_cache;
-    uint32_t dds_rows = 0;                  // DPEMU_DDS_ROWS: quad rows per thread (1, 2, 4; 0 = contiguous 8)
-    uint32_t dds_chunk = DDS_CHUNK;         // DPEMU_DDS_CHUNK: samples per workgroup
-    uint32_t dds_probe = 0;                 // DPEMU_DDS_PROBE: store-pattern probes (A/B only)
-    uint32_t dds_lds_pad = 0;               // DPEMU_DDS_LDSPAD: occupancy A/B
-    uint32_t dds_cyc = 1;                   // DPEMU_DDS_CYC=0: lean kernel walks the strobes (no cycle table)
-    uint32_t dds_spt = 4;                   // DPEMU_DDS_SPT=8: lean chunk kernel with 8 samples per thread per tile
-    uint32_t dds_yform = 1;                 // DPEMU_DDS_YFORM=0: chunk kernel's X/Y-form quad sweep (A/B)
-    uint32_t dds_index = 1;                 // DPEMU_DDS_INDEX=0: chunk workgroups compact events themselves (A/B)
-    void *d_dds_index = nullptr;            // chunk-path event index (dds_index_kernel)
+    void *d_dds_index = nullptr;            // event index of dds_index_kernel
     uint64_t dds_index_cap = 0;
-    uint32_t dds_seg = 0;                   // DPEMU_DDS_SEG=1: eligible channels on the segment kernel (A/B)
-    uint32_t dds_seg_chunk = DDS_SEG_CHUNK; // DPEMU_DDS_SEG_CHUNK: samples per segment-kernel sub-chunk
-    uint32_t dds_seg_per_cu = 0;            // DPEMU_DDS_SEG_PER_CU: segment-kernel workgroups per CU (0 = occupancy)
-    int last_feat = -1;
     std::string last_kernel;                // variant the last dpemu_run launched (dpemu_last_kernel)
     // kernel timing (dpemu_set_kernel_timing): event pairs recorded around main kernels
     bool timing = false;
@@ -63,6 +53,10 @@ struct dpemu_ctx {
     // privatised outcome histograms (R replicas, reduced after the interpreter)
     uint32_t *d_hist_rep = nullptr;
     uint64_t hist_rep_bytes = 0;
+    // call ordering across streams: the last call's stream and an event after its work
+    hipEvent_t ord_ev = nullptr;
+    hipStream_t ord_stream = nullptr;
+    bool ord_valid = false;
 };
 
 static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...) __attribute__((format(printf, 3, 4)));
@@ -83,6 +77,24 @@ static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...)
         if (e_ != hipSuccess)                                                              \
             return fail(ctx, DPEMU_E_DEVICE, "%s: %s", #call, hipGetErrorString(e_));      \
     } while (0)
+
+// Work of one context runs in call order whatever the streams: a call on a
+// stream other than the previous call's first waits for the previous call's
+// work (the scratch buffers -- histogram replicas, DDS index, thresholds, LUT
+// table, channel descriptors -- are shared by the context's calls).
+static hipError_t order_begin(dpemu_ctx *ctx, hipStream_t s)
+{
+    if (ctx->ord_valid && s != ctx->ord_stream) return hipStreamWaitEvent(s, ctx->ord_ev, 0);
+    return hipSuccess;
+}
+
+static hipError_t order_end(dpemu_ctx *ctx, hipStream_t s)
+{
+    const hipError_t e = hipEventRecord(ctx->ord_ev, s);
+    ctx->ord_stream = s;
+    ctx->ord_valid = e == hipSuccess;
+    return e;
+}
 
 // kernel timing: record the start event of a main-kernel launch on `stream`;
 // *stop gets the pair's stop event (null while timing is off)
@@ -107,8 +119,11 @@ static hipError_t timing_start(dpemu_ctx *ctx, hipStream_t stream, hipEvent_t *s
 
 static void free_programs(dpemu_ctx *ctx)
 {
-    (void)hipFree(ctx->d_uops); (void)hipFree(ctx->d_uops_t); (void)hipFree(ctx->d_offsets); (void)hipFree(ctx->d_ninstr); (void)hipFree(ctx->d_table);
-    ctx->d_uops = nullptr; ctx->d_uops_t = nullptr; ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
+    for (void *q : {(void *)ctx->d_uops, (void *)ctx->d_uops_t, (void *)ctx->d_macro, (void *)ctx->d_moff,
+                    (void *)ctx->d_offsets, (void *)ctx->d_ninstr, (void *)ctx->d_table})
+        (void)hipFree(q);
+    ctx->d_uops = ctx->d_uops_t = ctx->d_macro = nullptr;
+    ctx->d_moff = ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
     ctx->n_programs = 0;
 }
 
@@ -125,35 +140,13 @@ int dpemu_create(int device, dpemu_ctx **out)
     if (hipSetDevice(device) != hipSuccess) return DPEMU_E_DEVICE;
     dpemu_ctx *ctx = new dpemu_ctx();
     ctx->device = device;
-    if (const char *e = getenv("DPEMU_DDS_ROWS")) {
-        const uint32_t v = (uint32_t)atoi(e);
-        if (v == 0 || v == 1 || v == 2 || v == 4) ctx->dds_rows = v;
-    }
-    if (const char *e = getenv("DPEMU_DDS_CHUNK")) {
-        const uint32_t v = (uint32_t)atoi(e);
-        if (v >= 8 * BLOCK && (v % (8 * BLOCK)) == 0) ctx->dds_chunk = v;
-    }
-    if (const char *e = getenv("DPEMU_DDS_PROBE")) ctx->dds_probe = (uint32_t)atoi(e);
-    if (const char *e = getenv("DPEMU_DDS_LDSPAD")) ctx->dds_lds_pad = (uint32_t)atoi(e) & ~15u;
-    if (const char *e = getenv("DPEMU_DDS_CYC")) ctx->dds_cyc = (uint32_t)atoi(e) != 0;
-    if (const char *e = getenv("DPEMU_DDS_SPT")) ctx->dds_spt = atoi(e) == 8 ? 8u : 4u;
-    if (const char *e = getenv("DPEMU_DDS_YFORM")) ctx->dds_yform = (uint32_t)atoi(e) != 0;
-    if (const char *e = getenv("DPEMU_DDS_INDEX")) ctx->dds_index = (uint32_t)atoi(e) != 0;
-    if (const char *e = getenv("DPEMU_DDS_SEG")) ctx->dds_seg = (uint32_t)atoi(e) != 0;
-    if (const char *e = getenv("DPEMU_DDS_SEG_PER_CU")) ctx->dds_seg_per_cu = (uint32_t)atoi(e);
-    if (const char *e = getenv("DPEMU_DDS_SEG_CHUNK")) {
-        const uint32_t v = (uint32_t)atoi(e);
-        if (v >= 8 * BLOCK && (v % (8 * BLOCK)) == 0 && v <= (1u << 17)) ctx->dds_seg_chunk = v;
-    }
-    if (hipMalloc(&ctx->d_thr, DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&ctx->d_lut, 256 * sizeof(uint64_t)) != hipSuccess) {
-        delete ctx;
-        return DPEMU_E_NOMEM;
-    }
     std::vector<int16_t> lut(4096);
     dpemu_dds_sin_lut(lut.data());
-    if (hipMalloc(&ctx->d_sin, 4096 * sizeof(int16_t)) != hipSuccess ||
-        hipMemcpy(ctx->d_sin, lut.data(), 4096 * sizeof(int16_t), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMalloc(&ctx->d_thr, DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&ctx->d_lut, 256 * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&ctx->d_sin, 4096 * sizeof(int16_t)) != hipSuccess ||
+        hipMemcpy(ctx->d_sin, lut.data(), 4096 * sizeof(int16_t), hipMemcpyHostToDevice) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ord_ev, hipEventDisableTiming) != hipSuccess) {
         dpemu_destroy(ctx);
         return DPEMU_E_NOMEM;
     }
@@ -165,12 +158,14 @@ int dpemu_destroy(dpemu_ctx *ctx)
 {
     if (!ctx) return DPEMU_E_INVALID;
     (void)hipSetDevice(ctx->device);
+    if (ctx->ord_valid) (void)hipEventSynchronize(ctx->ord_ev);   // the context's work is done with its buffers
     free_programs(ctx);
     (void)hipFree(ctx->d_thr); (void)hipFree(ctx->d_lut); (void)hipFree(ctx->d_sin); (void)hipFree(ctx->d_ch);
     (void)hipFree(ctx->d_dds_index);
     (void)hipFree(ctx->d_hist_rep);
     for (auto *v : {&ctx->ev_used, &ctx->ev_free})
         for (auto &e : *v) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    if (ctx->ord_ev) (void)hipEventDestroy(ctx->ord_ev);
     delete ctx;
     return DPEMU_OK;
 }
@@ -202,22 +197,24 @@ int dpemu_kernel_times(dpemu_ctx *ctx, float *ms, int max_n, int *n_out)
     return DPEMU_OK;
 }
 
-int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *offsets,
+int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words, const uint32_t *offsets,
                         const uint32_t *n_instr, uint32_t n_programs, const uint32_t *prog_table,
                         uint32_t n_groups, uint32_t cores_per_shot)
 {
     if (!ctx) return DPEMU_E_INVALID;
-    if (!words || !offsets || !n_instr || !prog_table || n_programs == 0 || n_groups == 0)
+    if ((!words && n_words) || !offsets || !n_instr || !prog_table || n_programs == 0 || n_groups == 0)
         return fail(ctx, DPEMU_E_INVALID, "load_programs: null array or empty program set");
     const uint32_t C = cores_per_shot;
     if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1)))
         return fail(ctx, DPEMU_E_INVALID, "cores_per_shot %u is not a power of two in [1, 64]", C);
-    uint64_t quads = 0;
+    if ((uint64_t)n_groups * C > 0xFFFFFFFFull) return fail(ctx, DPEMU_E_INVALID, "n_groups * C exceeds 2^32");
     bool fp = false, sy = false, straight = true, linear = true;
     for (uint32_t i = 0; i < n_programs; i++) {
         if (n_instr[i] > 65536u)
             return fail(ctx, DPEMU_E_INVALID, "program %u: %u commands exceed the 2^16-deep cmd_mem", i, n_instr[i]);
-        quads = std::max<uint64_t>(quads, (uint64_t)offsets[i] + n_instr[i]);
+        if ((uint64_t)offsets[i] + n_instr[i] > n_words)
+            return fail(ctx, DPEMU_E_INVALID, "program %u: offset %u + %u commands run past the %llu words",
+                        i, offsets[i], n_instr[i], (unsigned long long)n_words);
     }
     for (uint32_t i = 0; i < n_programs; i++)
         for (uint32_t k = 0; k < n_instr[i]; k++) {
@@ -231,6 +228,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
         if (prog_table[i] >= n_programs)
             return fail(ctx, DPEMU_E_INVALID, "prog_table[%llu] = %u >= n_programs", (unsigned long long)i, prog_table[i]);
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (ctx->ord_valid) HIPCHK(ctx, hipEventSynchronize(ctx->ord_ev));   // earlier runs may still read the old image
     free_programs(ctx);
     HIPCHK(ctx, hipMalloc(&ctx->d_offsets, n_programs * 4));
     HIPCHK(ctx, hipMalloc(&ctx->d_ninstr, n_programs * 4));
@@ -253,8 +251,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     uint32_t max_len = 0;
     for (uint32_t i = 0; i < n_programs; i++) max_len = std::max(max_len, n_instr[i]);
     const uint64_t t_cmds = ((uint64_t)max_len + 1) * n_programs;
-    if (max_len && t_cmds <= std::max<uint64_t>(4 * tot, 4096) &&
-        t_cmds * 16 <= (1ull << 30)) {
+    if (max_len && t_cmds <= std::max<uint64_t>(4 * tot, 4096) && t_cmds * 16 <= (1ull << 30)) {
         std::vector<uint32_t> ut(t_cmds * 4, 0u);
         for (uint32_t pr = 0; pr < n_programs; pr++)
             for (uint32_t k = 0; k < n_instr[pr]; k++)
@@ -268,7 +265,6 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *o
     ctx->n_programs = n_programs;
     ctx->n_groups = n_groups;
     ctx->C = C;
-    ctx->n_quads = quads;
     ctx->has_fproc = fp;
     ctx->has_sync = sy;
     ctx->straight = straight;
@@ -297,9 +293,13 @@ static int validate(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t n_shots, b
         return fail(ctx, DPEMU_E_INVALID, "meas_latency / sync_latency must be in [1, 2^20]");
     if (cfg->meas_model != DPEMU_MEAS_STATE && cfg->meas_model != DPEMU_MEAS_READOUT)
         return fail(ctx, DPEMU_E_INVALID, "meas_model must be DPEMU_MEAS_STATE or DPEMU_MEAS_READOUT");
+    if (cfg->ro_win >= 4096)
+        return fail(ctx, DPEMU_E_INVALID, "ro_win %u must fit the 12-bit envelope-length field", cfg->ro_win);
     if ((uint64_t)cfg->max_cycles + cfg->meas_latency + 16 >= 0x80000000ull)
         return fail(ctx, DPEMU_E_INVALID, "max_cycles + meas_latency must stay below 2^31");
     if (cfg->meas_cap > 32) return fail(ctx, DPEMU_E_INVALID, "meas_cap > 32");
+    if (cfg->event_cap > DPEMU_MAX_EVENT_CAP || cfg->trace_cap > DPEMU_MAX_EVENT_CAP)
+        return fail(ctx, DPEMU_E_INVALID, "event_cap / trace_cap > %u", DPEMU_MAX_EVENT_CAP);
     if (cfg->fproc_mode > 1) return fail(ctx, DPEMU_E_INVALID, "fproc_mode %u", cfg->fproc_mode);
     if (cfg->lut_mask == 0) return fail(ctx, DPEMU_E_INVALID, "lut_mask must be nonzero");
     if (n_shots * cfg->cores_per_shot >= 0x80000000ull)
@@ -313,16 +313,19 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
                     const dpemu_outputs *out, hipStream_t stream)
 {
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, order_begin(ctx, stream));
     const uint32_t C = cfg->cores_per_shot;
+    // run constants, uploaded when they change (stream-ordered: the copy lands
+    // before this call's kernel and after the previous call's)
     std::vector<uint32_t> thr(cfg->p1_threshold, cfg->p1_threshold + DPEMU_MAX_CORES);
     std::vector<uint64_t> lut(cfg->lut_table, cfg->lut_table + 256);
     if (thr != ctx->thr_cache) {
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_thr, thr.data(), thr.size() * 4, hipMemcpyHostToDevice, stream));
         ctx->thr_cache = thr;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_thr, ctx->thr_cache.data(), thr.size() * 4, hipMemcpyHostToDevice, stream));
     }
     if (lut != ctx->lut_cache) {
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_lut, lut.data(), lut.size() * 8, hipMemcpyHostToDevice, stream));
         ctx->lut_cache = lut;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_lut, ctx->lut_cache.data(), lut.size() * 8, hipMemcpyHostToDevice, stream));
     }
     KParams p{};
     p.uops = ctx->d_uops;
@@ -333,14 +336,14 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.max_len = ctx->max_len;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
     p.summary = out->summary;
-    p.ev_main = reinterpret_cast<uint4 *>(out->ev_main);
-    p.ev_amp = out->ev_amp;
+    p.events = reinterpret_cast<uint4 *>(out->events);
     p.trace = reinterpret_cast<uint4 *>(out->trace);
     p.meas = reinterpret_cast<uint2 *>(out->meas);
     p.regs_out = out->regs;
     p.hist = reinterpret_cast<unsigned long long *>(out->hist);
     p.shot_begin = shot_begin;
     p.n_lanes = (uint32_t)(n_shots * C);
+    p.n_shots = (uint32_t)n_shots;
     p.C = C;
     p.log2C = 0;
     while ((1u << p.log2C) < C) p.log2C++;
@@ -348,8 +351,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.grp_g0 = (uint32_t)((shot_begin / cfg->shots_per_group) % cfg->n_groups);
     p.grp_r0 = (uint32_t)(shot_begin % cfg->shots_per_group);
     p.max_cycles = cfg->max_cycles;
-    p.event_cap = out->ev_main || out->ev_amp ? cfg->event_cap : 0;
-    p.trace_cap = out->trace ? cfg->trace_cap : 0;
+    p.event_cap = cfg->event_cap;           // the overflow flags follow the caps whether or not a buffer is given
+    p.trace_cap = cfg->trace_cap;
     p.meas_cap = cfg->meas_cap;
     p.fproc_mode = cfg->fproc_mode; p.meas_elem = cfg->meas_elem;
     p.meas_latency = cfg->meas_latency; p.sync_latency = cfg->sync_latency;
@@ -362,18 +365,10 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.lut_mask = cfg->lut_mask;
     const uint64_t guard = (uint64_t)C * (cfg->max_cycles / 3u + 4u) + 1024u;
     p.iter_guard = guard > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)guard;
-    // thread order and LDS program staging: a workgroup of S = BLOCK / C shots spans at
-    // most w consecutive program groups; stage their programs if they fit
+    // LDS program staging: a workgroup of S = BLOCK / C shots spans at most w
+    // consecutive program groups; stage their programs if they fit
     const uint32_t S = BLOCK / C, ng = cfg->n_groups;
-    p.shot_order = 0; p.rows = 0;
-    uint64_t w;
-    if ((cfg->exec_flags & DPEMU_X_GROUP_MAJOR) && cfg->shots_per_group == 1 && ng > 1 && n_shots % ng == 0) {
-        p.shot_order = 1;
-        p.rows = (uint32_t)(n_shots / ng);
-        w = (S - 1) / p.rows + 2;
-    } else {
-        w = (ng == 1) ? 1 : (S - 1) / cfg->shots_per_group + 2;
-    }
+    const uint64_t w = (ng == 1) ? 1 : (S - 1) / cfg->shots_per_group + 2;
     uint64_t footprint = ~0ull;
     if (w * C <= BLOCK) {
         const std::vector<uint64_t> &gl = ctx->group_len;
@@ -395,37 +390,26 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     }
     p.prog_lds_words = 0;
     int feat = 0;
-    // Branch-free programs run on the wave-uniform-ip kernel (straight.hip)
-    // unless ip could wrap (a 2^16-command program) or the general interpreter
-    // is forced: pulse-only programs always, programs with reg_alu / inc_qclk
-    // on grids of <= 4 workgroups per CU, where latency (not VALU throughput)
-    // bounds the general interpreter -- at full occupancy its per-opcode
-    // switch retires a mixed wave's commands with fewer instructions.  Those
-    // small grids also fetch commands in batches of 4.  The kernel stages the
-    // workgroup's programs in LDS when they fit the share of a CU's LDS that
-    // the grid's co-resident workgroups leave and the programs are long (a
-    // dependent global fetch per command is then the bottleneck) or staging is
-    // asked for; else it fetches the command-major image.  The general
-    // interpreter stages only on request, within 16 KiB.
-    // A/B knobs: DPEMU_LINEAR = 0 / 1 never / always runs ALU programs on
-    // straight.hip; DPEMU_FETCH_BATCH = 1 / 4 forces the batch.
+    // Pulse-only programs run on the wave-uniform-ip kernel (straight.hip)
+    // unless ip could wrap (a 2^16-command program) or the general
+    // interpreter is asked for (DPEMU_X_GENERAL).  Small grids (latency-bound)
+    // fetch commands in batches of 4.  The kernel stages the workgroup's
+    // programs in LDS when they fit the share of a CU's LDS that the grid's
+    // co-resident workgroups leave and the programs are long (a dependent
+    // global fetch per command is then the bottleneck); else it fetches the
+    // command-major image.  The general interpreter stages only on request
+    // (DPEMU_X_PROG_LDS), within 16 KiB.
     const uint64_t blocks = ((uint64_t)p.n_lanes + BLOCK - 1) / BLOCK;
     const bool small = blocks <= 4 * 256;
-    const char *lin_env = getenv("DPEMU_LINEAR"), *fb_env = getenv("DPEMU_FETCH_BATCH");
-    const bool linear_ok = lin_env ? atoi(lin_env) != 0 : small;
-    const int fetch_batch = fb_env ? (atoi(fb_env) == 1 ? 1 : 4) : (small ? 4 : 1);
-    const bool uniform = (ctx->straight || (ctx->linear && linear_ok)) && ctx->max_len < 65536u &&
-                         !(cfg->exec_flags & DPEMU_X_GENERAL);
-    const bool regs = !ctx->straight;
+    const int fetch_batch = small ? 4 : 1;
+    const bool uniform = ctx->straight && ctx->max_len < 65536u && !(cfg->exec_flags & DPEMU_X_GENERAL);
     int src = cmd_major ? STRAIGHT_ROWS : STRAIGHT_PROG;
     if (uniform) {
         const uint64_t per_cu = std::min<uint64_t>(8, std::max<uint64_t>(1, (blocks + 255) / 256));
-        const uint64_t budget = std::min<uint64_t>(STRAIGHT_LDS_MAX, ((regs ? 134ull : 150ull) * 1024 / per_cu) / 16);
-        const bool want = (cfg->exec_flags & DPEMU_X_PROG_LDS) || ctx->max_len >= 64;
-        if (footprint <= budget && want) {
+        const uint64_t budget = std::min<uint64_t>(STRAIGHT_LDS_MAX, (150ull * 1024 / per_cu) / 16);
+        if (footprint <= budget && ctx->max_len >= 64) {
             src = STRAIGHT_LDS;
             p.prog_lds_words = (uint32_t)std::max<uint64_t>(16, (footprint + 15) & ~15ull);
-            feat |= FEAT_PROG_LDS;
         }
     } else if (footprint <= PROG_LDS_MAX && (cfg->exec_flags & DPEMU_X_PROG_LDS)) {
         feat |= FEAT_PROG_LDS;
@@ -454,10 +438,10 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
         p.hist_lds = 0;
         if (repl) {
             const uint64_t stride = (bins + 31) & ~31ull;        // replicas on separate 128-B lines
-            const uint64_t blocks = (p.n_lanes + BLOCK - 1) / BLOCK;
             R = (uint32_t)std::min<uint64_t>({64, blocks, std::max<uint64_t>(1, (2ull << 20) / (stride * 4))});
             const uint64_t need = (uint64_t)R * stride * 4;
             if (need > ctx->hist_rep_bytes) {
+                HIPCHK(ctx, hipStreamSynchronize(stream));    // earlier work may still use the old replicas
                 (void)hipFree(ctx->d_hist_rep);
                 ctx->d_hist_rep = nullptr; ctx->hist_rep_bytes = 0;
                 HIPCHK(ctx, hipMalloc(&ctx->d_hist_rep, need));
@@ -474,15 +458,14 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     }
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
-    if (uniform) HIPCHK(ctx, launch_straight(p, src, regs, fetch_batch, stream));
+    if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, stream));
     {
         char name[96];
         if (uniform)
-            snprintf(name, sizeof name, "straight_kernel<%s,%s,fb%d>",
-                     src == STRAIGHT_ROWS ? "rows" : src == STRAIGHT_PROG ? "prog" : "lds",
-                     regs ? "regs" : "pulse", fetch_batch);
+            snprintf(name, sizeof name, "straight_kernel<%s,fb%d>",
+                     src == STRAIGHT_ROWS ? "rows" : src == STRAIGHT_PROG ? "prog" : "lds", fetch_batch);
         else
             snprintf(name, sizeof name, "interp_kernel<feat=0x%x>", feat);
         ctx->last_kernel = name;
@@ -490,7 +473,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     if (out->hist && p.hist_rep)
         HIPCHK(ctx, launch_hist_reduce(ctx->d_hist_rep, R, hist_stride, bins,
                                        reinterpret_cast<unsigned long long *>(out->hist), stream));
-    ctx->last_feat = uniform ? (feat | FEAT_UNIFORM) : feat;
+    HIPCHK(ctx, order_end(ctx, stream));
     return DPEMU_OK;
 }
 
@@ -516,10 +499,9 @@ int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
     HIPCHK(ctx, hipSetDevice(ctx->device));
     const uint64_t nl = n_shots * cfg->cores_per_shot;
     struct Buf { void *host; void *dev; size_t bytes; bool in; };
-    Buf bufs[7] = {
+    Buf bufs[6] = {
         {host_out->summary, nullptr, nl * 32, false},
-        {host_out->ev_main, nullptr, (size_t)cfg->event_cap * nl * 16, false},
-        {host_out->ev_amp, nullptr, (size_t)cfg->event_cap * nl * 2, false},
+        {host_out->events, nullptr, (size_t)cfg->event_cap * nl * 16, false},
         {host_out->trace, nullptr, (size_t)cfg->trace_cap * nl * 16, false},
         {host_out->meas, nullptr, (size_t)cfg->meas_cap * nl * 8, false},
         {host_out->regs, nullptr, nl * 64, false},
@@ -534,10 +516,9 @@ int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
     }
     if (result == DPEMU_OK) {
         dpemu_outputs d{};
-        d.summary = (uint32_t *)bufs[0].dev; d.ev_main = (uint32_t *)bufs[1].dev;
-        d.ev_amp = (uint16_t *)bufs[2].dev; d.trace = (uint32_t *)bufs[3].dev;
-        d.meas = (uint32_t *)bufs[4].dev; d.regs = (uint32_t *)bufs[5].dev;
-        d.hist = (uint64_t *)bufs[6].dev;
+        d.summary = (uint32_t *)bufs[0].dev; d.events = (uint32_t *)bufs[1].dev;
+        d.trace = (uint32_t *)bufs[2].dev; d.meas = (uint32_t *)bufs[3].dev;
+        d.regs = (uint32_t *)bufs[4].dev; d.hist = (uint64_t *)bufs[5].dev;
         result = run_impl(ctx, cfg, shot_begin, n_shots, &d, nullptr);
         if (result == DPEMU_OK) {
             hipError_t e = hipDeviceSynchronize();
@@ -548,6 +529,7 @@ int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
                 hipMemcpy(b.host, b.dev, b.bytes, hipMemcpyDeviceToHost) != hipSuccess)
                 result = fail(ctx, DPEMU_E_DEVICE, "copy back failed");
     }
+    (void)hipDeviceSynchronize();
     for (auto &b : bufs) if (b.dev) (void)hipFree(b.dev);
     return result;
 }
@@ -571,11 +553,11 @@ int dpemu_dds_sin_lut(int16_t *out)
 }  // extern "C"
 
 extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uint32_t *summary,
-                         const uint32_t *ev_main, const uint16_t *ev_amp, const uint32_t *env_tables,
-                         const uint32_t *freq_tables, int16_t *iq_out, void *stream)
+                         const uint32_t *events, const uint32_t *env_tables, const uint32_t *freq_tables,
+                         int16_t *iq_out, void *stream)
 {
     if (!ctx) return DPEMU_E_INVALID;
-    if (!ch || !summary || !ev_main || !ev_amp || !env_tables || !freq_tables || !iq_out)
+    if (!ch || !summary || !events || !env_tables || !freq_tables || !iq_out)
         return fail(ctx, DPEMU_E_INVALID, "dpemu_dds: null argument");
     if (ch->n_samples % 4) return fail(ctx, DPEMU_E_INVALID, "n_samples must be a multiple of 4");
     if (ch->event_cap > DDS_MAX_EVENTS) return fail(ctx, DPEMU_E_INVALID, "event_cap > %u", DDS_MAX_EVENTS);
@@ -583,10 +565,6 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     if (ch->n_channels > 65535) return fail(ctx, DPEMU_E_INVALID, "n_channels > 65535");
     std::vector<uint32_t> desc((size_t)ch->n_channels * DDS_CH_WORDS);
     uint32_t env_max = 0, freq_max = 0;         // LDS staging sizes: largest tables that fit
-    uint32_t seg_env = 0, seg_freq = 0;         // the same for the segment kernel (pairs counted)
-    bool any_seg = false, any_chunk = false;
-    std::vector<uint32_t> seg_list;             // appended to the descriptors on the device
-    const bool seg_ok = ctx->dds_seg && (ctx->dds_probe == 0 || ctx->dds_probe >= 5);
     for (uint32_t i = 0; i < ch->n_channels; i++) {
         uint32_t *d = &desc[(size_t)i * DDS_CH_WORDS];
         d[0] = ch->ch_lane[i]; d[1] = ch->ch_elem[i] & 3u; d[2] = ch->spc[i]; d[3] = ch->interp[i];
@@ -594,42 +572,28 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
         if (d[0] >= ch->n_lanes) return fail(ctx, DPEMU_E_INVALID, "channel %u: lane %u >= n_lanes", i, d[0]);
         if (d[2] < 1 || d[2] > 16) return fail(ctx, DPEMU_E_INVALID, "channel %u: spc %u not in [1, 16]", i, d[2]);
         if (d[3] < 1) return fail(ctx, DPEMU_E_INVALID, "channel %u: interp must be >= 1", i);
-        const uint32_t interp = d[3], env_w = interp == 1 ? 2 * d[5] : d[5];
-        const bool seg = seg_ok && (d[2] == 8 || d[2] == 16) && (interp & (interp - 1)) == 0 &&
-                         env_w <= DDS_SEG_ENV_MAX && d[7] <= DDS_FREQ_LDS_MAX;
-        if (seg) {
-            d[1] |= DDS_SEG_FLAG;
-            seg_list.push_back(i);
-            any_seg = true;
-            seg_env = std::max(seg_env, env_w);
-            seg_freq = std::max(seg_freq, 2 * d[7]);
-        } else {
-            any_chunk = true;
-            // staged words: (E, E') pairs for interp 1 and (R, R') pairs in Y form
-            const uint32_t ew = ctx->dds_yform ? env_w : d[5], fw = ctx->dds_yform ? 2 * d[7] : d[7];
-            if (ew <= DDS_ENV_LDS_MAX) env_max = std::max(env_max, ew);
-            if (fw <= DDS_FREQ_LDS_MAX) freq_max = std::max(freq_max, fw);
-        }
+        // staged words: (E, E') pairs for interp 1, (R, R') pairs of the freq entries
+        const uint32_t ew = d[3] == 1 ? 2 * d[5] : d[5], fw = 2 * d[7];
+        if (ew <= DDS_ENV_LDS_MAX) env_max = std::max(env_max, ew);
+        if (fw <= DDS_FREQ_LDS_MAX) freq_max = std::max(freq_max, fw);
     }
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
-    const size_t n_desc = desc.size();
-    desc.insert(desc.end(), seg_list.begin(), seg_list.end());
+    HIPCHK(ctx, order_begin(ctx, s));
     if (desc != ctx->ch_cache) {            // descriptors change rarely: upload only then
+        HIPCHK(ctx, hipStreamSynchronize(s));   // an earlier launch may still read d_ch
         if (desc.size() > ctx->ch_cap) {
             (void)hipFree(ctx->d_ch);
             ctx->d_ch = nullptr; ctx->ch_cap = 0;
             HIPCHK(ctx, hipMalloc(&ctx->d_ch, desc.size() * 4));
             ctx->ch_cap = desc.size();
         }
-        HIPCHK(ctx, hipStreamSynchronize(s));   // the previous launch may still read d_ch
         HIPCHK(ctx, hipMemcpy(ctx->d_ch, desc.data(), desc.size() * 4, hipMemcpyHostToDevice));
         ctx->ch_cache = desc;
     }
     DDSParams p{};
     p.summary = summary;
-    p.ev_main = reinterpret_cast<const uint4 *>(ev_main);
-    p.ev_amp = ev_amp;
+    p.events = reinterpret_cast<const uint4 *>(events);
     p.env = env_tables; p.freq = freq_tables;
     p.sin_lut = ctx->d_sin;
     p.ch = ctx->d_ch;
@@ -639,39 +603,25 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.ev_lds = std::max<uint32_t>(8, (ch->event_cap + 7) & ~7u);
     p.env_lds = (env_max + 3) & ~3u;
     p.freq_lds = (freq_max + 3) & ~3u;
-    p.chunk = ctx->dds_chunk;
-    p.rows = ctx->dds_rows;
-    p.probe = ctx->dds_probe;
-    p.lds_pad = ctx->dds_lds_pad;
-    p.yform = ctx->dds_yform;
-    p.spt = ctx->dds_spt;
-    p.cyc = ctx->dds_cyc;
-    if (ctx->dds_index && (any_chunk || any_seg) && ctx->dds_probe != 5 && ctx->dds_probe != 12) {      // event index of the chunk path (grown, never shrunk)
-        const uint32_t chunks = (p.n_samples + p.chunk - 1) / p.chunk;
-        const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds, chunks);
-        if (need > ctx->dds_index_cap) {
-            HIPCHK(ctx, hipStreamSynchronize(s));   // the previous launch may still use it
-            (void)hipFree(ctx->d_dds_index);
-            ctx->d_dds_index = nullptr; ctx->dds_index_cap = 0;
-            HIPCHK(ctx, hipMalloc(&ctx->d_dds_index, need));
-            ctx->dds_index_cap = need;
-        }
-        uint8_t *b = static_cast<uint8_t *>(ctx->d_dds_index);
-        p.xs = reinterpret_cast<uint4 *>(b);
-        p.win = reinterpret_cast<uint4 *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
-        p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16 + (uint64_t)p.n_channels * chunks * 16);
+    p.tiles = (p.n_samples + DDS_TILE - 1) / DDS_TILE;
+    p.stripes = std::max<uint32_t>(1, std::min<uint32_t>(p.tiles, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE));
+    const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds, p.tiles);
+    if (need > ctx->dds_index_cap) {         // the event index (grown, never shrunk)
+        HIPCHK(ctx, hipStreamSynchronize(s));   // an earlier launch may still use it
+        (void)hipFree(ctx->d_dds_index);
+        ctx->d_dds_index = nullptr; ctx->dds_index_cap = 0;
+        HIPCHK(ctx, hipMalloc(&ctx->d_dds_index, need));
+        ctx->dds_index_cap = need;
     }
-    DDSParams ps = p;
-    ps.env_lds = (seg_env + 3) & ~3u;
-    ps.freq_lds = (seg_freq + 3) & ~3u;
-    ps.chunk = p.xs ? p.chunk : ctx->dds_seg_chunk;   // one window per chunk of the index
-    ps.seg_list = ctx->d_ch + n_desc;
-    ps.n_seg = (uint32_t)seg_list.size();
-    ps.grid_per_cu = ctx->dds_seg_per_cu;
+    uint8_t *b = static_cast<uint8_t *>(ctx->d_dds_index);
+    p.xs = reinterpret_cast<uint4 *>(b);
+    p.win = reinterpret_cast<uint4 *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
+    p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16 + (uint64_t)p.n_channels * p.tiles * 16);
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, launch_dds_index(p, s));   // outside the timed bracket: it holds the synthesis kernel alone
     HIPCHK(ctx, timing_start(ctx, s, &ev_stop));
-    HIPCHK(ctx, launch_dds(p, ps, any_seg, any_chunk, s));
+    HIPCHK(ctx, launch_dds(p, s));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, s));
+    HIPCHK(ctx, order_end(ctx, s));
     return DPEMU_OK;
 }

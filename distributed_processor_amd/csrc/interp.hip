@@ -98,14 +98,14 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     const bool valid = pos < p.n_lanes;
     const uint32_t core = pos & (C - 1);
     const uint32_t spos = pos >> p.log2C;
-    const uint32_t lane = (shot_of_pos(p, spos) << p.log2C) | core;   // output lane index
-    const uint64_t shot = p.shot_begin + (lane >> p.log2C);
+    const uint32_t lane = out_lane(p, spos, core);   // output lane index (core-major)
+    const uint64_t shot = p.shot_begin + spos;
     const uint32_t wl = tid & 63;                    // lane within the wavefront
     const uint32_t leader_tid = tid & ~(C - 1);
 
     uint32_t base = 0, nprog = 0, grp = 0, prog = 0;
     if (valid) {
-        grp = lane_group(p, lane);
+        grp = shot_group(p, spos);
         prog = p.prog_table[(uint64_t)grp * C + core];
         base = p.offsets[prog];
         nprog = p.n_instr[prog];
@@ -154,12 +154,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 
     auto emit_event = [&](uint32_t te, uint32_t kind) {
         if (n_ev < p.event_cap) {
-            const uint64_t idx = (uint64_t)n_ev * n_lanes + lane;
-            if (p.ev_main) {
-                const uint32_t q = (te < qa_t) ? 0u : qa_q + (te - qa_t);
-                p.ev_main[idx] = make_uint4(te, q, event_word(pe, kind), pp);
-            }
-            if (p.ev_amp) p.ev_amp[idx] = (uint16_t)pa;
+            if (p.events) p.events[(uint64_t)n_ev * n_lanes + lane] = event_record(te, pe, pp, pa, kind);
         } else flags |= F_EVENT_OVF;
         n_ev++;
         if (kind == 0 && p.meas_elem != 0xFFu && ((pe >> 24) & 3u) == p.meas_elem) {

@@ -42,7 +42,6 @@ constexpr int FEAT_SYNC = 2;    // SYNC barriers
 constexpr int FEAT_LUT = 4;     // fproc_lut back end
 constexpr int FEAT_PROG_LDS = 8; // the workgroup's programs staged in LDS (fits PROG_LDS_MAX)
 constexpr int FEAT_STRAIGHT = 16; // only pulse / idle / done / hang opcodes: no register file
-constexpr int FEAT_UNIFORM = 32;  // (reporting) FEAT_STRAIGHT run by straight_kernel: wave-uniform ip
 constexpr uint32_t PROG_LDS_MAX = 1024;   // commands (16 KiB) of dynamic LDS per workgroup
 
 constexpr uint32_t ST_DONE = DPEMU_ST_DONE, ST_MAX_CYCLES = DPEMU_ST_MAX_CYCLES;
@@ -107,17 +106,16 @@ struct KParams {
     uint32_t max_len;             // longest program; the command-major image's guard row
     const uint32_t *p1_thr;
     const uint64_t *lut_table;
-    // outputs (device, nullable)
+    // outputs (device, nullable); lane L = core * n_shots + shot (core-major)
     uint32_t *summary;
-    uint4 *ev_main;
-    uint16_t *ev_amp;
+    uint4 *events;                // {t, env | cfg << 24 | kind << 28, phase | freq << 17, amp}
     uint4 *trace;
     uint2 *meas;
     uint32_t *regs_out;
     unsigned long long *hist;
     // run
     uint64_t shot_begin;
-    uint32_t n_lanes, C, log2C, n_groups, shots_per_group;
+    uint32_t n_lanes, n_shots, C, log2C, n_groups, shots_per_group;
     uint32_t grp_g0, grp_r0;      // (shot_begin / spg) % n_groups, shot_begin % spg
     uint32_t max_cycles, event_cap, trace_cap, meas_cap;
     uint32_t fproc_mode, meas_elem, meas_latency, sync_latency;
@@ -127,7 +125,6 @@ struct KParams {
     int32_t ro_sep, ro_thr;
     uint32_t ro_sigma, ro_win, ro_wrecip;   // ro_wrecip = floor(2^24 / ro_win)
     uint32_t iter_guard;
-    uint32_t shot_order, rows;    // 1: group-major thread order (shots_per_group 1, n = rows * n_groups)
     uint32_t prog_lds_words;      // dynamic LDS commands (FEAT_PROG_LDS)
     uint32_t *hist_rep;           // [hist_reps][hist_stride] u32 replicas (128-B aligned rows)
     uint32_t hist_reps, hist_lds; // hist_lds: n_groups << C <= HIST_LDS_MAX, aggregate in LDS
@@ -139,73 +136,60 @@ hipError_t launch_hist_reduce(const uint32_t *rep, uint32_t R, uint64_t stride, 
                               unsigned long long *hist, hipStream_t stream);
 
 hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
-// branch-free programs (straight.hip); src: where commands are fetched from;
-// regs: programs with reg_alu / inc_qclk (register file in LDS); fb: commands
-// fetched per batch (1 or 4)
+// pulse-only programs (straight.hip); src: where commands are fetched from;
+// fb: commands fetched per batch (1 or 4)
 enum { STRAIGHT_ROWS = 0, STRAIGHT_PROG = 1, STRAIGHT_LDS = 2 };
 constexpr uint32_t STRAIGHT_LDS_MAX = 9216;   // commands (144 KiB) of dynamic LDS per workgroup
-hipError_t launch_straight(const KParams &p, int src, bool regs, int fb, hipStream_t stream);
+hipError_t launch_straight(const KParams &p, int src, int fb, hipStream_t stream);
 
 // ---- DDS ------------------------------------------------------------------
+// Two launches per synthesis (dds.hip): dds_index_kernel compacts each
+// channel's strobes and pulse resets once and writes every sample tile's
+// window of them; dds_tile_kernel, grid (DDS stripes, channels), sweeps the
+// tiles of a channel round-robin over its stripe workgroups, so the
+// workgroups of a channel write adjacent tiles at the same time.
 struct DDSParams {
     const uint32_t *summary;
-    const uint4 *ev_main;
-    const uint16_t *ev_amp;
+    const uint4 *events;           // dpemu_run event records, slot-major
     const uint32_t *env, *freq;
     const int16_t *sin_lut;        // Q15 sine table [4096]
     const uint32_t *ch;            // per-channel descriptors, DDS_CH_WORDS u32 each
     uint32_t *iq;                  // [n_channels][n_samples] packed {I16 low, Q16 high}
     uint32_t n_channels, n_lanes, n_samples, event_cap;
-    uint32_t ev_lds;               // compacted-event slots in LDS (>= event_cap, multiple of 8)
-    uint32_t env_lds, freq_lds;    // LDS staging capacity for a channel's env / freq table (words)
-    uint32_t chunk;                // samples per workgroup (multiple of 8 * BLOCK)
-    uint32_t rows;                 // quad rows per thread per tile (1, 2, 4); 0 = 8 contiguous samples
-    uint32_t probe;                // measurement probes (DPEMU_DDS_PROBE): 3 / 4 = bare stores,
-                                   // thread-contiguous / rows layout; 0 = normal
-    uint32_t cyc;                  // lean chunk kernel: per-chunk cycle table (0 = walk the strobes)
-    uint32_t spt;                  // lean chunk kernel: samples per thread per tile (4 or 8)
-    uint32_t yform;                // chunk kernel: Y-form quad sweep (pair-staged tables; 0 = X/Y form)
-    uint32_t lds_pad;              // extra dynamic LDS per workgroup (DPEMU_DDS_LDSPAD, occupancy A/B)
-    const uint32_t *seg_list;      // segment kernel: its channels (indices into ch)
-    uint32_t n_seg;
-    uint32_t grid_per_cu;          // segment kernel: workgroups per CU (0 = occupancy)
-    // chunk path event index (dds_index_kernel -> dds_chunk_kernel; null = each
-    // workgroup compacts its lane's events itself)
-    uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env, phase | freq, amp}
+    uint32_t ev_lds;               // compacted-event slots per channel (>= event_cap, multiple of 8)
+    uint32_t env_lds, freq_lds;    // LDS staging capacity for a channel's env / freq table (words, as staged)
+    uint32_t tiles;                // sample tiles per channel (DDS_TILE samples each)
+    uint32_t stripes;              // workgroups per channel (gridDim.x)
+    // event index (dds_index_kernel -> dds_tile_kernel)
+    uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
     uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
-    uint4 *win;                    // [n_channels][chunks] {strobe lo, count, reset lo, count}
+    uint4 *win;                    // [n_channels][tiles] {strobe lo, count, reset lo, count}
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
 constexpr uint32_t DDS_MAX_EVENTS = 1024;
-constexpr uint32_t DDS_CHUNK = 1u << 14;   // samples per workgroup (lean kernel A/B: 16 Ki beats 8 / 24 / 32 Ki)
-constexpr uint32_t DDS_ENV_LDS_MAX = 8192;   // words: tables up to 32 KiB are staged in LDS
-constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;  // words: 128 freq entries
+constexpr uint32_t DDS_TILE = 4 * BLOCK;      // samples per tile: 4 per thread, one 16-B store each
+#ifndef DDS_TPS
+#define DDS_TPS 16
+#endif
+constexpr uint32_t DDS_TILES_PER_STRIPE = DDS_TPS;   // tiles per workgroup (build-time A/B: -DDDS_TPS=)
+constexpr uint32_t DDS_ENV_LDS_MAX = 8192;    // words: tables up to 32 KiB are staged in LDS
+constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;   // words: 64 freq entries as (R, R') pairs
 
-// dynamic LDS bytes of dds_chunk_kernel
-__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_lds)
+// dynamic LDS bytes of dds_tile_kernel: half sine table | strobe records
+// (16 B) | strobe times | reset times | tile windows | env | freq
+__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t tiles_per_stripe, uint32_t env_lds,
+                                                  uint32_t freq_lds)
 {
-    return 4096 * 2 + ev_lds * 18 + (env_lds + freq_lds) * 4;
+    return 4096 + ev_lds * 24 + tiles_per_stripe * 16 + (env_lds + freq_lds) * 4;
 }
 
-// bytes of the chunk path's event index (xs, xr, win)
-inline uint64_t dds_index_bytes(uint32_t n_channels, uint32_t ev_lds, uint32_t chunks)
+// bytes of the event index (xs, xr, win)
+inline uint64_t dds_index_bytes(uint32_t n_channels, uint32_t ev_lds, uint32_t tiles)
 {
-    return (uint64_t)n_channels * ev_lds * 20 + (uint64_t)n_channels * chunks * 16;
+    return (uint64_t)n_channels * ev_lds * 20 + (uint64_t)n_channels * tiles * 16;
 }
 
-// dynamic LDS bytes of dds_seg_kernel; env_lds counts words as staged
-// (pairs for interp 1), freq_lds the (R, R') pair words
-inline uint32_t dds_seg_lds_bytes(uint32_t ev_lds, uint32_t env_lds, uint32_t freq_lds, uint32_t chunk)
-{
-    return 4096 * 2 + ev_lds * 40 + chunk / 2 + (env_lds + freq_lds) * 4;
-}
-constexpr uint32_t DDS_SEG_FLAG = 0x100;        // descriptor word 1: channel runs on dds_seg_kernel
-constexpr uint32_t DDS_SEG_CHUNK = 1u << 15;    // samples per sub-chunk (group table) on the segment path
-constexpr uint32_t DDS_SEG_ENV_MAX = 4096;      // staged env words (pairs counted) on the segment path
-
-// the event index (p.xs; the synthesis kernels of launch_dds read it)
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream);
-// p: chunk-kernel parameters; ps: segment-kernel parameters (same buffers)
-hipError_t launch_dds(const DDSParams &p, const DDSParams &ps, bool any_seg, bool any_chunk, hipStream_t stream);
+hipError_t launch_dds(const DDSParams &p, hipStream_t stream);
 
 }  // namespace dpemu

@@ -68,8 +68,8 @@ __device__ __forceinline__ uint32_t meas_bit(const KParams &p, uint64_t shot, ui
     if (p.meas_model != DPEMU_MEAS_READOUT) return state;
     const int64_t z = (int64_t)((r.y & 0xFFFFu) + (r.y >> 16) + (r.z & 0xFFFFu) + (r.z >> 16)) - 131070;
     int64_t s = ((int64_t)p.ro_sep * (int64_t)(amp & 0xFFFFu)) >> 16;
-    if (p.ro_win) {     // no division on the device: floor(2^24 / ro_win) comes from the host
-        const uint32_t w = (env >> 12) & 0xFFFu;
+    const uint32_t w = (env >> 12) & 0xFFFu;
+    if (p.ro_win && w) {    // W = 0: a CW envelope, no window scaling; floor(2^24 / ro_win) from the host
         s = (s * (int64_t)((w < p.ro_win ? w : p.ro_win) * p.ro_wrecip)) >> 24;
     }
     const int64_t x = (state ? s : -s) + ((z * (int64_t)p.ro_sigma) >> 16);
@@ -83,34 +83,36 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot, uint32_t lane_in
     return (ballot >> base) & gm;
 }
 
-// shot index within the run of the block-linear shot position sp: natural order, or
-// group-major (shot_order 1: shots_per_group 1, n_shots = rows * n_groups) so that a
-// workgroup's shots share their programs
-__device__ __forceinline__ uint32_t shot_of_pos(const KParams &p, uint32_t sp)
-{
-    return p.shot_order ? (sp % p.rows) * p.n_groups + sp / p.rows : sp;
-}
-
-// program group of output lane `lane`: (shot / spg) % n_groups from the run's
+// program group of the run's shot sl: (shot / spg) % n_groups from the run's
 // first shot (g0, r0 from the host) in 32-bit arithmetic -- a u64 division
 // would cost ~150 VALU instructions per lane
-__device__ __forceinline__ uint32_t lane_group(const KParams &p, uint32_t lane)
+__device__ __forceinline__ uint32_t shot_group(const KParams &p, uint32_t sl)
 {
-    const uint32_t sl = lane >> p.log2C;                 // shot within the run (< 2^31)
     const uint64_t num = (uint64_t)p.grp_r0 + sl;
     const uint32_t q = (num >> 32) ? (uint32_t)(num / p.shots_per_group) : (uint32_t)num / p.shots_per_group;
     const uint32_t g = p.grp_g0 + q % p.n_groups;       // < 2 n_groups <= 2^32
     return g >= p.n_groups ? g - p.n_groups : g;
 }
 
-// index of the program-group "step" of shot position sp relative to position sp0
+// index of the program-group "step" of shot sp relative to shot sp0 of the run
 __device__ __forceinline__ uint32_t group_step(const KParams &p, uint32_t sp, uint32_t sp0)
 {
     if (p.n_groups == 1) return 0;
-    if (p.shot_order) return sp / p.rows - sp0 / p.rows;
-    const uint64_t a = (p.shot_begin + shot_of_pos(p, sp)) / p.shots_per_group;
-    const uint64_t b = (p.shot_begin + shot_of_pos(p, sp0)) / p.shots_per_group;
+    const uint64_t a = (p.shot_begin + sp) / p.shots_per_group;
+    const uint64_t b = (p.shot_begin + sp0) / p.shots_per_group;
     return (uint32_t)(a - b);
+}
+
+// output lane of (run shot sl, core): core-major (include/dpemu.h)
+__device__ __forceinline__ uint32_t out_lane(const KParams &p, uint32_t sl, uint32_t core)
+{
+    return core * p.n_shots + sl;
+}
+
+// the 16-B event record (include/dpemu.h): pulse_iface snapshot at cycle te
+__device__ __forceinline__ uint4 event_record(uint32_t te, uint32_t pe, uint32_t pp, uint32_t pa, uint32_t kind)
+{
+    return make_uint4(te, event_word(pe, kind), pp, pa & 0xFFFFu);
 }
 
 // Stage the programs of this workgroup's (group, core) slots in LDS -- the
@@ -127,7 +129,7 @@ __device__ __forceinline__ uint32_t stage_programs(const KParams &p, uint4 *s_pr
     const uint32_t n_shots = p.n_lanes >> p.log2C;
     const uint32_t sp0 = (blockIdx.x * BLOCK) >> p.log2C;
     const uint32_t spl = min(sp0 + (BLOCK >> p.log2C), n_shots) - 1u;
-    const uint32_t g0 = (uint32_t)(((p.shot_begin + shot_of_pos(p, sp0)) / p.shots_per_group) % p.n_groups);
+    const uint32_t g0 = (uint32_t)(((p.shot_begin + sp0) / p.shots_per_group) % p.n_groups);
     const uint32_t nslots = (group_step(p, spl, sp0) + 1u) * C;
     uint32_t len = 0;
     if (tid < nslots) {

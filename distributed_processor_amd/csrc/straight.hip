@@ -1,22 +1,15 @@
-// straight.hip -- the interpreter for branch-free programs on CDNA4 (gfx950).
+// straight.hip -- the interpreter for pulse-only programs on CDNA4 (gfx950).
 //
-// A program with no jump, fproc or sync command (op4 not in {2, 3, 4, 5, 7})
-// never moves its instruction pointer except by +1 (hdl/instr_ptr.v without
-// a jump).  So every lane still running in loop iteration k is executing
-// command k of its program: the command index is wave-uniform, the per-lane
-// ip / mode state of the general interpreter (interp.hip) disappears, and the
-// next commands' addresses are known before the current one executes, so
-// they are fetched in batches of FB (one memory latency per FB commands).
-//
-// Two specialisations:
-//   REGS = false  pulse-only programs (pulse write / trigger, idle, pulse
-//                 reset, done, hang): no register file, qclk never reloaded
-//                 (hdl/qclk.v), so qclk(D) = D - 1 after the two-cycle reset
-//                 hold;
-//   REGS = true   plus reg_alu (op4 1) and inc_qclk (op4 6): the 16 x 32-bit
-//                 reg_file in LDS as [reg][lane] (alu.v, reg_file.v),
-//                 register-sourced pulse fields, register / qclk traces and a
-//                 qclk anchor that inc_qclk reloads.
+// A program of pulse write / trigger, idle, pulse reset, done and hang
+// commands never moves its instruction pointer except by +1
+// (hdl/instr_ptr.v without a jump) and never writes a register, so qclk is
+// never reloaded (hdl/qclk.v): qclk(D) = D - 1 after the two-cycle reset hold.
+// Every lane still running in loop iteration k is executing command k of its
+// program: the command index is wave-uniform, the per-lane ip / mode state of
+// the general interpreter (interp.hip) disappears, and the next commands'
+// addresses are known before the current one executes, so they are fetched
+// in batches of FB (one memory latency per FB commands).  (Branch-free
+// programs with reg_alu / inc_qclk run on macro.hip.)
 // Timing is hdl/ctrl.v's closed form (oracle/fast_model.c); the first
 // command is peeled to model the reset hold (cmd_time 0 there strobes twice).
 // Outputs and their layout are identical to interp_kernel's.
@@ -45,43 +38,27 @@
 namespace dpemu {
 
 
-// alu.v:20-50; le = sub[31] ^ overflow == signed a < b
-__device__ __forceinline__ uint32_t alu_eval(uint32_t op, uint32_t a, uint32_t b)
-{
-    const uint32_t sub = a - b;
-    const uint32_t lt = (int32_t)a < (int32_t)b;
-    uint32_t r = a;                 // 0: id0
-    r = (op == 1) ? a + b : r;
-    r = (op == 2) ? sub : r;
-    r = (op == 3) ? (uint32_t)(sub == 0) : r;
-    r = (op == 4) ? lt : r;
-    r = (op == 5) ? (lt ^ 1u) : r;
-    r = (op == 6) ? b : r;
-    r = (op == 7) ? 0u : r;
-    return r;
-}
-
-template <int SRC, bool REGS, int FB>
+template <int SRC, int FB>
 __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
 {
     constexpr bool ROWS = SRC == STRAIGHT_ROWS, LDS = SRC == STRAIGHT_LDS;
     __shared__ uint32_t s_hist[HIST_LDS_MAX];
     __shared__ uint32_t s_pref[LDS ? BLOCK + 1 : 1];
     __shared__ uint32_t s_scan[BLOCK / 64];
-    __shared__ uint32_t s_regs[REGS ? 16 : 1][REGS ? BLOCK : 1];
     extern __shared__ uint4 s_prog[];
     const uint32_t tid = threadIdx.x;
     const uint32_t C = p.C;
     const uint32_t pos = blockIdx.x * BLOCK + tid;
     const bool valid = pos < p.n_lanes;
     const uint32_t core = pos & (C - 1);
-    const uint32_t lane = (shot_of_pos(p, pos >> p.log2C) << p.log2C) | core;   // output lane index
-    const uint64_t shot = p.shot_begin + (lane >> p.log2C);
+    const uint32_t sl = pos >> p.log2C;              // shot within the run
+    const uint32_t lane = out_lane(p, sl, core);      // output lane index (core-major)
+    const uint64_t shot = p.shot_begin + sl;
     const uint32_t n_lanes = p.n_lanes;
 
     uint32_t grp = 0, prog = 0, base = 0, nprog = 0;
     if (valid) {
-        grp = lane_group(p, lane);
+        grp = shot_group(p, sl);
         prog = p.prog_table[(uint64_t)grp * C + core];
         nprog = p.n_instr[prog];
         if (!ROWS) base = p.offsets[prog];
@@ -91,32 +68,24 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
         __syncthreads();
     }
-    if constexpr (LDS) base = stage_programs(p, s_prog, s_pref, s_scan, pos >> p.log2C);
-    if constexpr (REGS) {
-#pragma unroll
-        for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
-    }
+    if constexpr (LDS) base = stage_programs(p, s_prog, s_pref, s_scan, sl);
 
     const uint32_t max_cycles = p.max_cycles;
     uint32_t t = 0, pe = 0, pp = 0, pa = 0;            // next DECODE cycle; pulse register image
-    uint32_t qa_t = 1, qa_q = 0;                       // qclk(t) = qa_q + t - qa_t for t >= qa_t
-    uint32_t flags = 0, n_ev = 0, n_meas = 0, meas_bits = 0, last_bit = 0, n_tr = 0;
+    uint32_t flags = 0, n_ev = 0, n_meas = 0, meas_bits = 0, last_bit = 0;
     // st: 0 while running, else the finish status (| ST_TOP: stopped by the
     // max_cycles check before a fetch, so that command did not retire); k_end:
     // the command index at the finish.  A finish leaves t alone: t_end = t
     constexpr uint32_t ST_TOP = 0x100u;
     uint32_t st = valid ? 0u : ST_DONE, k_end = 0;
 
-    // pulse_iface strobe at cycle te, qclk q (kind 0: trigger, 1: phase reset)
-    // with the current pulse registers, for lanes with `ok`; readout-element
+    // pulse_iface strobe at cycle te (kind 0: trigger, 1: phase reset) with
+    // the current pulse registers, for lanes with `ok`; readout-element
     // triggers draw the measurement.  Overflow flags are derived from the
     // final counts (a record is dropped iff its count exceeds the cap)
-    auto emit = [&](bool ok, uint32_t te, uint32_t q, uint32_t kind) {
-        if (ok && n_ev < p.event_cap) {
-            const uint64_t slot = (uint64_t)n_ev * n_lanes + lane;
-            if (p.ev_main) p.ev_main[slot] = make_uint4(te, q, event_word(pe, kind), pp);
-            if (p.ev_amp) p.ev_amp[slot] = (uint16_t)pa;
-        }
+    auto emit = [&](bool ok, uint32_t te, uint32_t kind) {
+        if (ok && n_ev < p.event_cap && p.events)
+            p.events[(uint64_t)n_ev * n_lanes + lane] = event_record(te, pe, pp, pa, kind);
         n_ev += ok ? 1u : 0u;
         const bool is_meas = ok && kind == 0u && ((pe >> 24) & 3u) == p.meas_elem;   // meas_elem 0xFF: none
         uint32_t bit = 0;
@@ -130,13 +99,6 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         n_meas += is_meas ? 1u : 0u;
     };
 
-    // register write / qclk load record (trace_cap 0: trace output off)
-    auto trace = [&](bool ok, uint32_t tt, uint32_t addr, uint32_t val) {
-        if (ok && n_tr < p.trace_cap && p.trace)
-            p.trace[(uint64_t)n_tr * n_lanes + lane] = make_uint4(tt, addr, val, 0u);
-        n_tr += ok ? 1u : 0u;
-    };
-
     // command k of this lane's program, zero (DONE) past its end; in bounds for any k
     auto fetch = [&](uint32_t k) -> uint4 {
         if constexpr (ROWS) {
@@ -147,31 +109,16 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         }
     };
 
-    // register-sourced pulse fields: reg[rs0] ORed into the cleared fields
-    auto pulse_regs = [&](const uint4 u, uint32_t reg0) {
-        pe |= (u.w & UOP_RS_ENV) ? (reg0 & 0xFFFFFFu) : 0u;
-        pp |= (u.w & UOP_RS_PH) ? (reg0 & 0x1FFFFu) : 0u;
-        pp |= (u.w & UOP_RS_FR) ? ((reg0 & 0x1FFu) << 17) : 0u;
-        pa = (u.w & UOP_RS_AMP) ? (reg0 & 0xFFFFu) : pa;
-    };
-
     // retire command u = k for the lanes in `live` (running): any opcode, any state
     auto retire = [&](const uint4 u, uint32_t k, bool first, bool live) {
         const uint32_t D = t;
         const uint32_t op4 = u.y >> 28;
         // opcode classes as bit tables: cmd_time wait 9/C, pulse class 8/9/B/C,
-        // strobe 9/B, ALU class 1/6.  Pulse writes need no class: decode_cmd
-        // leaves the write enables and register-source bits of every other
-        // opcode zero, so pulse_write / pulse_regs are no-ops there
+        // strobe 9/B.  Pulse writes need no class: decode_cmd leaves the write
+        // enables of every other opcode zero, so pulse_write is a no-op there
         const bool waits = (0x1200u >> op4) & 1u;
         const bool pulse_cls = (0x1B00u >> op4) & 1u;
         const bool strobe = (0x0A00u >> op4) & 1u;
-        const bool alu_cls = REGS && ((0x0042u >> op4) & 1u);
-        uint32_t reg0 = 0, reg1 = 0;
-        if constexpr (REGS) {
-            reg0 = s_regs[(u.w >> 20) & 15u][tid];
-            reg1 = s_regs[(u.y >> 4) & 15u][tid];
-        }
         const uint32_t T = u.x;
         uint32_t wait;
         bool big = false, dbl = false;
@@ -181,42 +128,26 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
             wait = dbl ? 0u : T + 1u;
             big = T == INF32;
         } else {
-            wait = T - (qa_q + (D - qa_t));                 // D > qa_t after the first command
+            wait = T - (D - 1u);                            // qclk(D) = D - 1 after the hold
         }
         const bool top = D > max_cycles;
         const bool over = waits && (big || wait > max_cycles - D);
         flags |= (live && !top && waits && (big || wait >= 0x80000000u)) ? F_LATE : 0u;
         const uint32_t fin = top ? (ST_MAX_CYCLES | ST_TOP) : over ? ST_MAX_CYCLES
-                           : (pulse_cls || alu_cls) ? 0u : (op4 >= 0xDu ? ST_HUNG_OPCODE : ST_DONE);
+                           : pulse_cls ? 0u : (op4 >= 0xDu ? ST_HUNG_OPCODE : ST_DONE);
         st = live ? fin : st;
         k_end = live ? k : k_end;
         const bool ok = live && fin == 0u;
         const uint32_t tT = D + (waits ? wait : 0u);
-        pulse_write(u, pe, pp, pa);                     // pulse_reg.sv:59-97
-        if constexpr (REGS) pulse_regs(u, reg0);
+        pulse_write(u, pe, pp, pa);                     // pulse_reg.sv:59-97 (reg_in reads 0)
         const bool rst = op4 == 0xBu;
-        // qclk of the strobe: first command (qa = (1, 0)) 0 at cycle 0
-        const uint32_t te = rst ? D : tT + 2u;
-        emit(ok && strobe, te, first ? (te ? te - 1u : 0u) : qa_q + (te - qa_t), rst ? 1u : 0u);
+        emit(ok && strobe, rst ? D : tT + 2u, rst ? 1u : 0u);
         if (first) {
             const bool two = ok && dbl && op4 == 0x9u;
-            emit(two, tT + 3u, tT + 2u, 0u);
+            emit(two, tT + 3u, 0u);
             flags |= two ? F_DOUBLE_STROBE : 0u;
         }
-        if constexpr (REGS) {
-            // reg_alu: reg[rd] = alu(in0, reg[rs1]); inc_qclk: qclk = alu(in0, qclk(D)) + 3 at D + 3
-            const uint32_t in0 = (u.y & 8u) ? reg0 : u.x;
-            const uint32_t qD = first ? 0u : qa_q + (D - qa_t);
-            const bool is_q = op4 == 0x6u;
-            const uint32_t out = alu_eval(u.y & 7u, in0, is_q ? qD : reg1);
-            const uint32_t rd = (u.y >> 8) & 15u;
-            if (ok && op4 == 0x1u) s_regs[rd][tid] = out;
-            trace(ok && alu_cls, D + 3u, is_q ? TRACE_QCLK_LOAD : rd, is_q ? out + 3u : out);
-            const bool load = ok && is_q;
-            qa_t = load ? D + 3u : qa_t;
-            qa_q = load ? out + 3u : qa_q;
-        }
-        t = ok ? (alu_cls ? D + 4u : tT + 3u) : t;
+        t = ok ? tT + 3u : t;
     };
 
     // the cmd_time wait of a pulse / idle command after the first: past the
@@ -226,7 +157,7 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
     auto timed = [&](const uint4 u, uint32_t k, uint32_t &tT) -> bool {
         const bool live = st == 0u;
         const uint32_t D = t;
-        const uint32_t wait = u.x - (qa_q + (D - qa_t));
+        const uint32_t wait = u.x - (D - 1u);
         const bool stop = live && wait > max_cycles - D;
         flags |= (stop && wait >= 0x80000000u) ? F_LATE : 0u;
         st = stop ? ST_MAX_CYCLES : st;
@@ -249,8 +180,7 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         case 0x9: {                                         // pulse write + trigger at cmd_time
             const bool ok = timed(u, k, tT);
             pulse_write(u, pe, pp, pa);
-            if constexpr (REGS) pulse_regs(u, s_regs[(u.w >> 20) & 15u][tid]);
-            emit(ok, tT + 2u, qa_q + (tT + 2u - qa_t), 0u);
+            emit(ok, tT + 2u, 0u);
             t = ok ? tT + 3u : t;
             break;
         }
@@ -261,18 +191,17 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         }
         case 0x8:                                           // pulse write, no trigger
             pulse_write(u, pe, pp, pa);
-            if constexpr (REGS) pulse_regs(u, s_regs[(u.w >> 20) & 15u][tid]);
             t = live ? t + 3u : t;
             break;
         case 0xB:                                           // phase reset strobe at decode
-            emit(live, t, qa_q + (t - qa_t), 1u);
+            emit(live, t, 1u);
             t = live ? t + 3u : t;
             break;
         case 0x0: case 0xA:                                 // done
             st = live ? ST_DONE : st;
             k_end = live ? k : k_end;
             break;
-        default:                                            // ALU / qclk, mixed opcodes, hung, past max_cycles
+        default:                                            // mixed opcodes, hung, past max_cycles
             retire(u, k, false, live);
         }
     };
@@ -288,47 +217,42 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
             step(u[j], k + j);
         }
     }
-    flags |= (n_ev > p.event_cap ? F_EVENT_OVF : 0u) |
-             (n_meas > min(p.meas_cap, MEAS_LOOKUP) ? F_MEAS_OVF : 0u) |
-             (p.trace_cap && n_tr > p.trace_cap ? F_TRACE_OVF : 0u);
+    flags |= (n_ev > p.event_cap ? F_EVENT_OVF : 0u) | (n_meas > min(p.meas_cap, MEAS_LOOKUP) ? F_MEAS_OVF : 0u);
 
     if (valid && p.summary)
         write_summary(p, lane, t, k_end, st & 0xFFu, flags, n_ev, k_end + ((st & ST_TOP) ? 0u : 1u),
-                      t < qa_t ? 0u : qa_q + (t - qa_t), n_meas, meas_bits, n_tr);
+                      t < 1u ? 0u : t - 1u, n_meas, meas_bits, 0u);
     if (valid && p.regs_out) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = REGS ? s_regs[r][tid] : 0u;
+        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = 0u;
     }
     count_outcome(p, s_hist, valid, core, grp, last_bit);
 }
 
-template <int SRC, bool REGS, int FB>
+template <int SRC, int FB>
 static hipError_t launch_src(const KParams &p, uint32_t blocks, size_t shmem, hipStream_t stream)
 {
     if (shmem > 64 * 1024) {
         // programs staged in dynamic LDS beyond the default 64 KiB need the opt-in
         static size_t granted = 0;
         if (shmem > granted) {
-            hipError_t e = hipFuncSetAttribute((const void *)straight_kernel<SRC, REGS, FB>,
+            hipError_t e = hipFuncSetAttribute((const void *)straight_kernel<SRC, FB>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
             if (e != hipSuccess) return e;
             granted = shmem;
         }
     }
-    hipLaunchKernelGGL((straight_kernel<SRC, REGS, FB>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    hipLaunchKernelGGL((straight_kernel<SRC, FB>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
     return hipGetLastError();
 }
 
-hipError_t launch_straight(const KParams &p, int src, bool regs, int fb, hipStream_t stream)
+hipError_t launch_straight(const KParams &p, int src, int fb, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
     if (blocks == 0) return hipSuccess;
     const size_t shmem = src == STRAIGHT_LDS ? (size_t)p.prog_lds_words * sizeof(uint4) : 0;
 #define SRC_CASE(S)                                                                                    \
-    case S: return regs ? (fb == 1 ? launch_src<S, true, 1>(p, blocks, shmem, stream)                 \
-                                   : launch_src<S, true, 4>(p, blocks, shmem, stream))                \
-                        : (fb == 1 ? launch_src<S, false, 1>(p, blocks, shmem, stream)                \
-                                   : launch_src<S, false, 4>(p, blocks, shmem, stream));
+    case S: return fb == 1 ? launch_src<S, 1>(p, blocks, shmem, stream) : launch_src<S, 4>(p, blocks, shmem, stream);
     switch (src) {
     SRC_CASE(STRAIGHT_ROWS) SRC_CASE(STRAIGHT_PROG) SRC_CASE(STRAIGHT_LDS)
     }

@@ -94,6 +94,38 @@ class ProgramSet:
         self.words = np.ascontiguousarray(self.words)
         self.table = table
 
+    @classmethod
+    def from_arrays(cls, words, offsets, n_instr, table, n_groups, cores_per_shot, buffers=None):
+        """A ProgramSet from packed arrays (the dpemu_load_programs layout):
+        words (n, 4) u32, program p = words[offsets[p]:offsets[p] + n_instr[p]],
+        table[g * C + c] = program of core c in group g.  For program tables
+        too large to pass through assembler dicts (config 4: 2 * 10^5
+        programs, workloads.config4_rb_set)."""
+        self = cls.__new__(cls)
+        C_ = int(cores_per_shot)
+        if C_ < 1 or C_ & (C_ - 1) or C_ > _abi.MAX_CORES:
+            raise ValueError('cores_per_shot must be a power of two in [1, 64]')
+        self.words = np.ascontiguousarray(np.asarray(words, np.uint32).reshape(-1, 4))
+        self.offsets = np.ascontiguousarray(offsets, np.uint32)
+        self.n_instr = np.ascontiguousarray(n_instr, np.uint32)
+        self.table = np.ascontiguousarray(table, np.uint32).reshape(-1)
+        if len(self.offsets) != len(self.n_instr) or len(self.table) != int(n_groups) * C_:
+            raise ValueError('offsets / n_instr / table sizes disagree')
+        if len(self.n_instr) and (self.offsets.astype(np.uint64) + self.n_instr).max() > len(self.words):
+            raise ValueError('a program runs past the end of words')
+        if len(self.table) and self.table.max() >= len(self.n_instr):
+            raise ValueError('table names a program that does not exist')
+        self.cores_per_shot = C_
+        self.n_groups = int(n_groups)
+        self.buffers = buffers if buffers is not None else {}
+        return self
+
+    def program(self, group: int, core: int) -> np.ndarray:
+        """(n, 4) u32 machine code of core ``core`` in group ``group``"""
+        p = int(self.table[group * self.cores_per_shot + core])
+        o = int(self.offsets[p])
+        return self.words[o:o + int(self.n_instr[p])]
+
     @property
     def n_programs(self):
         return len(self.n_instr)
@@ -114,24 +146,14 @@ class EmulationResult:
         return self.n_shots * self.cfg.cores_per_shot
 
     def lane(self, shot, core):
-        return (shot - self.shot_begin) * self.cfg.cores_per_shot + core
+        """output lane of (absolute shot, core): core-major (include/dpemu.h)"""
+        return int(_abi.lane_index(shot - self.shot_begin, core, self.n_shots))
 
     def events(self, shot, core) -> np.ndarray:
-        """structured events of one lane: t, qclk, env_word, cfg, kind, phase, freq, amp"""
+        """structured events of one lane: t, env_word, cfg, kind, phase, freq, amp"""
         L = self.lane(shot, core)
         n = min(int(self.summary['n_events'][L]), self.cfg.event_cap)
-        ev = self.arrays['ev_main'][:n, L]
-        amp = self.arrays['ev_amp'][:n, L] if 'ev_amp' in self.arrays else np.zeros(n, np.uint16)
-        out = np.zeros(n, dtype=[('t', 'u4'), ('qclk', 'u4'), ('env_word', 'u4'), ('cfg', 'u1'),
-                                 ('kind', 'u1'), ('phase', 'u4'), ('freq', 'u2'), ('amp', 'u2')])
-        out['t'], out['qclk'] = ev[:, 0], ev[:, 1]
-        out['env_word'] = ev[:, 2] & 0xFFFFFF
-        out['cfg'] = (ev[:, 2] >> 24) & 0xF
-        out['kind'] = ev[:, 2] >> 28
-        out['phase'] = ev[:, 3] & 0x1FFFF
-        out['freq'] = ev[:, 3] >> 17
-        out['amp'] = amp
-        return out
+        return decode_events(self.arrays['events'][:n, L])
 
     def status_counts(self):
         st, n = np.unique(self.summary['status'], return_counts=True)
@@ -140,6 +162,22 @@ class EmulationResult:
     @property
     def histogram(self):
         return self.arrays.get('hist')
+
+
+def decode_events(ev) -> np.ndarray:
+    """structured view of event records (..., 4) u32: t, env_word, cfg, kind,
+    phase, freq, amp (the pulse_iface fields, hdl/pulse_iface.sv:2-6)"""
+    ev = np.asarray(ev).view(np.uint32)
+    out = np.zeros(ev.shape[:-1], dtype=[('t', 'u4'), ('env_word', 'u4'), ('cfg', 'u1'), ('kind', 'u1'),
+                                         ('phase', 'u4'), ('freq', 'u2'), ('amp', 'u2')])
+    out['t'] = ev[..., 0]
+    out['env_word'] = ev[..., 1] & 0xFFFFFF
+    out['cfg'] = (ev[..., 1] >> 24) & 0xF
+    out['kind'] = ev[..., 1] >> 28
+    out['phase'] = ev[..., 2] & 0x1FFFF
+    out['freq'] = ev[..., 2] >> 17
+    out['amp'] = ev[..., 3] & 0xFFFF
+    return out
 
 
 class Emulator:
@@ -193,7 +231,8 @@ class Emulator:
     # -------------------------------------------------------------- programs
     def load(self, programs, cores_per_shot: Optional[int] = None) -> ProgramSet:
         ps = programs if isinstance(programs, ProgramSet) else ProgramSet(programs, cores_per_shot)
-        rc = self._L.dpemu_load_programs(self._h, ps.words.ctypes.data, ps.offsets.ctypes.data,
+        rc = self._L.dpemu_load_programs(self._h, ps.words.ctypes.data, int(ps.words.shape[0]),
+                                         ps.offsets.ctypes.data,
                                          ps.n_instr.ctypes.data, ps.n_programs, ps.table.ctypes.data,
                                          ps.n_groups, ps.cores_per_shot)
         check(self._h, rc, 'dpemu_load_programs', self._L)
@@ -208,7 +247,7 @@ class Emulator:
 
     # -------------------------------------------------------------- running
     def run(self, n_shots: int, shot_begin: int = 0, cfg: Optional[_abi.Config] = None,
-            outputs: Iterable[str] = ('summary', 'ev_main', 'ev_amp', 'meas', 'hist'),
+            outputs: Iterable[str] = ('summary', 'events', 'meas', 'hist'),
             **cfg_kw) -> EmulationResult:
         """Emulate shots [shot_begin, shot_begin + n_shots); results copied to host."""
         cfg = cfg or self.config(**cfg_kw)
@@ -221,12 +260,19 @@ class Emulator:
 
     def run_device(self, cfg: _abi.Config, n_shots: int, shot_begin: int, outputs: dict,
                    stream=None):
-        """Asynchronous run into caller-owned device buffers (e.g. torch tensors:
-        pass {name: tensor}); stream: torch.cuda.Stream / raw handle / None."""
+        """Asynchronous run into caller-owned device buffers: torch tensors
+        {name: tensor} shaped as alloc_device_outputs makes them (checked: the
+        C ABI takes bare pointers); stream: torch.cuda.Stream / raw handle / None."""
+        unknown = set(outputs) - set(_abi.OUTPUT_NAMES)
+        if unknown:
+            raise DpemuError('unknown outputs {}'.format(sorted(unknown)))
+        want = device_output_specs(cfg, n_shots)
         o = _abi.Outputs()
         for name, _ in _abi.Outputs._fields_:
             t = outputs.get(name)
-            setattr(o, name, None if t is None else (t.data_ptr() if hasattr(t, 'data_ptr') else int(t)))
+            if t is not None:
+                _check_tensor(name, t, want[name], self.device)
+            setattr(o, name, None if t is None else t.data_ptr())
         s = getattr(stream, 'cuda_stream', stream)
         rc = self._L.dpemu_run(self._h, C.addressof(cfg), int(shot_begin), int(n_shots), C.addressof(o),
                                C.c_void_p(s) if s else None)
@@ -238,11 +284,15 @@ class Emulator:
         Returns (or fills) an int32 device tensor [n_channels, n_samples]
         whose words hold I in the low and Q in the high 16 bits."""
         import torch
-        for k in ('summary', 'ev_main', 'ev_amp'):
+        for k in ('summary', 'events'):
             if k not in outputs:
                 raise DpemuError('synthesize needs the run\'s {} output'.format(k))
-        if outputs['ev_main'].shape[:2] != (plan.event_cap, plan.n_lanes):
-            raise DpemuError('event arrays do not match the plan (event_cap, n_lanes)')
+        if tuple(outputs['events'].shape) != (plan.event_cap, plan.n_lanes, 4) or \
+                tuple(outputs['summary'].shape) != (plan.n_lanes, 8):
+            raise DpemuError('event / summary arrays do not match the plan (event_cap, n_lanes)')
+        for k in ('summary', 'events'):
+            if not outputs[k].is_contiguous() or outputs[k].device.type != 'cuda':
+                raise DpemuError('{} must be a contiguous device tensor'.format(k))
         dev = outputs['summary'].device
         if iq is None:
             iq = torch.empty((plan.n_channels, int(n_samples)), dtype=torch.int32, device=dev)
@@ -252,23 +302,47 @@ class Emulator:
         ch = plan.struct(n_samples)
         s = getattr(stream, 'cuda_stream', stream)
         rc = self._L.dpemu_dds(self._h, C.addressof(ch), outputs['summary'].data_ptr(),
-                               outputs['ev_main'].data_ptr(), outputs['ev_amp'].data_ptr(),
-                               env.data_ptr(), freq.data_ptr(), iq.data_ptr(),
+                               outputs['events'].data_ptr(), env.data_ptr(), freq.data_ptr(), iq.data_ptr(),
                                C.c_void_p(s) if s else None)
         check(self._h, rc, 'dpemu_dds', self._L)
         return iq
 
 
-def alloc_device_outputs(cfg: _abi.Config, n_shots: int, want=('summary', 'ev_main', 'ev_amp', 'meas', 'hist'),
+def device_output_specs(cfg: _abi.Config, n_shots: int):
+    """{name: (shape, torch dtype)} of the dpemu_outputs arrays of a run"""
+    import torch
+    n_lanes = int(n_shots) * cfg.cores_per_shot
+    return {'summary': ((n_lanes, 8), torch.int32), 'events': ((cfg.event_cap, n_lanes, 4), torch.int32),
+            'trace': ((cfg.trace_cap, n_lanes, 4), torch.int32),
+            'meas': ((cfg.meas_cap, n_lanes, 2), torch.int32), 'regs': ((16, n_lanes), torch.int32),
+            'hist': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64)}
+
+
+def _check_tensor(name, t, spec, device):
+    """a caller tensor must match what the kernel writes: size, dtype,
+    contiguity and device (the C ABI has no size arguments)"""
+    import torch
+    shape, dtype = spec
+    if not isinstance(t, torch.Tensor):
+        raise DpemuError('{}: expected a torch tensor'.format(name))
+    if name == 'hist' and len(shape) == 2 and shape[1] > 4096:
+        raise DpemuError('hist needs cores_per_shot <= 12')
+    if t.device.type != 'cuda' or (t.device.index if t.device.index is not None else 0) != device:
+        raise DpemuError('{}: tensor on {} but the emulator runs on cuda:{}'.format(name, t.device, device))
+    if t.element_size() != torch.empty((), dtype=dtype).element_size() or t.is_floating_point():
+        raise DpemuError('{}: dtype {} (want {})'.format(name, t.dtype, dtype))
+    if not t.is_contiguous():
+        raise DpemuError('{}: tensor must be contiguous'.format(name))
+    if t.numel() != int(np.prod(shape)):
+        raise DpemuError('{}: {} elements, the run writes {} ({})'.format(name, t.numel(), int(np.prod(shape)),
+                                                                        tuple(shape)))
+
+
+def alloc_device_outputs(cfg: _abi.Config, n_shots: int, want=('summary', 'events', 'meas', 'hist'),
                          device='cuda'):
     """torch device tensors laid out as dpemu_outputs."""
     import torch
-    n_lanes = int(n_shots) * cfg.cores_per_shot
-    shapes = {'summary': ((n_lanes, 8), torch.int32), 'ev_main': ((cfg.event_cap, n_lanes, 4), torch.int32),
-              'ev_amp': ((cfg.event_cap, n_lanes), torch.int16),
-              'trace': ((cfg.trace_cap, n_lanes, 4), torch.int32),
-              'meas': ((cfg.meas_cap, n_lanes, 2), torch.int32), 'regs': ((16, n_lanes), torch.int32),
-              'hist': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64)}
+    shapes = device_output_specs(cfg, n_shots)
     out = {}
     for k in want:
         shp, dt = shapes[k]

@@ -97,10 +97,11 @@ def max_over_ranks(value: float, device=None, group=None) -> float:
 
 def sample_lanes(n_shots: int, cores_per_shot: int, n_sample: int) -> np.ndarray:
     """Local lane indices of ``n_sample`` whole shots spread evenly over a
-    shard of ``n_shots`` (every core of each chosen shot).  The same count on
-    every rank keeps gather_sample's tensors equal-shaped."""
+    shard of ``n_shots`` (every core of each chosen shot; lanes are core-major,
+    L = core * n_shots + shot), ordered shot by shot.  The same count on every
+    rank keeps gather_sample's tensors equal-shaped."""
     if n_shots <= 0 or n_sample <= 0:
         return np.zeros(0, np.int64)
     k = min(int(n_sample), int(n_shots))
     shots = (np.arange(k, dtype=np.int64) * n_shots) // k
-    return (shots[:, None] * cores_per_shot + np.arange(cores_per_shot)[None, :]).reshape(-1)
+    return (np.arange(cores_per_shot, dtype=np.int64)[None, :] * int(n_shots) + shots[:, None]).reshape(-1)

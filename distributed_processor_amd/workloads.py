@@ -20,6 +20,7 @@ qdrv (16 samples/clk), element 1 rdrv (16/clk, interp 16), element 2 rdlo
 
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 from typing import Dict, List, Sequence
 
@@ -186,39 +187,192 @@ def _clifford_table():
 
 
 CLIFFORDS = _clifford_table()    # 24 entries
+RB_QUARTER = 2 ** 15               # pi/2 in 17-bit phase words
+RB_LAYER_CLKS = 3 * X90_CLKS + 16  # fixed layer length: the cores stay aligned
+RB_T0 = 10                         # first layer's cmd_time
+RB_PREG, RB_TREG = 1, 2            # virtual-Z phase register, per-pulse phase register
 
 
-def config4_rb(n_seq=1000, depth=200, seed=0x5EED, n_cores=2):
+def _mix64(x):
+    """splitmix64 finaliser on uint64 arrays (wrapping arithmetic)"""
+    with np.errstate(over='ignore'):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def rb_draws(seqs, depth, n_cores, seed=0x5EED):
+    """The random content of RB sequences ``seqs`` (global indices): Clifford
+    indices [len(seqs), depth, n_cores] in [0, 24) and cross-resonance bits
+    [len(seqs), depth].  Counter-based -- a hash of (seed, sequence, layer,
+    slot) -- so sequence s is the same whatever the table size or shard, and
+    the whole table is generated vectorised."""
+    if depth >= 1 << 16 or n_cores >= 255:
+        raise ValueError('depth < 65536 and n_cores < 255')
+    s = np.asarray(seqs, np.uint64).reshape(-1, 1, 1)
+    d = np.arange(depth, dtype=np.uint64).reshape(1, -1, 1)
+    j = np.arange(n_cores + 1, dtype=np.uint64).reshape(1, 1, -1)
+    with np.errstate(over='ignore'):
+        key = np.uint64((int(seed) * 0x9E3779B97F4A7C15) & (2 ** 64 - 1)) + ((s << np.uint64(24)) | (d << np.uint64(8)) | j)
+    h = _mix64(key)
+    cliffs = (h[:, :, :n_cores] % np.uint64(24)).astype(np.int64)
+    cr = ((h[:, :, n_cores] >> np.uint64(32)) & np.uint64(1)).astype(np.int64)
+    return cliffs, cr
+
+
+def _rb_builder(c):
+    """CoreBuilder with core c's RB tables registered in a fixed order, so every
+    sequence of a core shares one env / freq buffer set"""
+    b = CoreBuilder()
+    b.env_word(QDRV, X90_ENV)
+    b.freq_addr(QDRV, qubit_params(c)['fq'])
+    if c == 0:
+        b.freq_addr(QDRV, qubit_params(1)['fq'])   # cross-resonance drive
+    return b
+
+
+def config4_rb(n_seq=1000, depth=200, seed=0x5EED, n_cores=2, first=0):
     """2-qubit RB-like sequences: per layer each qubit plays a random Clifford
-    (<= 2 pulses, virtual Z by reg_alu on its phase register), and with
-    probability 1/2 a cross-resonance pulse on core 0.  Slots are fixed-length
-    so the cores stay aligned.  Returns n_seq assembled-program dicts."""
-    rng = np.random.default_rng(seed)
-    quarter = 2 ** 15        # pi/2 in 17-bit phase words
+    (<= 2 X90 pulses on X or Y, virtual Z by reg_alu on its phase register), and
+    with probability 1/2 a cross-resonance pulse on core 0.  Layers are
+    fixed-length so the cores stay aligned.  Returns n_seq assembled-program
+    dicts for global sequences [first, first + n_seq) -- the per-command
+    reference for :func:`config4_rb_set`, which builds the same machine code
+    vectorised."""
+    cliffs, cr = rb_draws(np.arange(first, first + n_seq), depth, n_cores, seed)
     groups = []
     for s in range(n_seq):
-        cliffs = rng.integers(0, 24, size=(depth, n_cores))
-        cr = rng.integers(0, 2, size=depth)
         prog = {}
         for c in range(n_cores):
             q = qubit_params(c)
-            b = CoreBuilder()
-            preg = 1
+            b = _rb_builder(c)
             b.emit(isa.pulse_reset())
-            b.emit(isa.alu_cmd('reg_alu', 'i', 0, 'id0', 0, preg))         # phase reg = 0
-            t = 10
+            b.emit(isa.alu_cmd('reg_alu', 'i', 0, 'id0', 0, RB_PREG))         # phase reg = 0
+            t = RB_T0
             for d in range(depth):
-                pre, z = CLIFFORDS[cliffs[d, c]]
+                pre, z = CLIFFORDS[cliffs[s, d, c]]
                 for i, ax in enumerate(pre):
-                    b.emit(isa.alu_cmd('reg_alu', 'i', quarter if ax == 'y' else 0, 'add', preg, 2))
-                    b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t + X90_CLKS * i, phase_reg=2)
+                    b.emit(isa.alu_cmd('reg_alu', 'i', RB_QUARTER if ax == 'y' else 0, 'add', RB_PREG, RB_TREG))
+                    b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t + X90_CLKS * i, phase_reg=RB_TREG)
                 if z:
-                    b.emit(isa.alu_cmd('reg_alu', 'i', z * quarter, 'add', preg, preg))
-                if c == 0 and cr[d]:
+                    b.emit(isa.alu_cmd('reg_alu', 'i', z * RB_QUARTER, 'add', RB_PREG, RB_PREG))
+                if c == 0 and cr[s, d]:
                     b.pulse(QDRV, qubit_params(1)['fq'], 0.0, 0.3, X90_ENV, t + 2 * X90_CLKS)
-                t += 3 * X90_CLKS + 16
+                t += RB_LAYER_CLKS
             readout(b, q, t)
             b.emit(isa.done_cmd())
             prog[str(c)] = b.assembled()
         groups.append(prog)
     return groups
+
+
+# per-layer command slots of config4_rb: (pre-rotation ALU, X90) x 2, virtual Z, CR
+_RB_PRE_AX = np.array([[-1, -1], [0, -1], [1, -1], [0, 0], [0, 1], [1, 0]])   # CLIFFORDS pre lists, 0 = x, 1 = y
+(_T_RESET, _T_INIT, _T_ALU_X, _T_ALU_Y, _T_PULSE, _T_Z1, _T_Z2, _T_Z3, _T_CR, _T_RDRV, _T_RDLO,
+ _T_DONE) = range(12)
+
+
+def _rb_templates(c):
+    """core c's command templates (cmd_time 0) and its env / freq buffers"""
+    q = qubit_params(c)
+    b = _rb_builder(c)
+    b.emit(isa.pulse_reset())
+    b.emit(isa.alu_cmd('reg_alu', 'i', 0, 'id0', 0, RB_PREG))
+    b.emit(isa.alu_cmd('reg_alu', 'i', 0, 'add', RB_PREG, RB_TREG))
+    b.emit(isa.alu_cmd('reg_alu', 'i', RB_QUARTER, 'add', RB_PREG, RB_TREG))
+    b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, 0, phase_reg=RB_TREG)
+    for z in (1, 2, 3):
+        b.emit(isa.alu_cmd('reg_alu', 'i', z * RB_QUARTER, 'add', RB_PREG, RB_PREG))
+    if c == 0:
+        b.pulse(QDRV, qubit_params(1)['fq'], 0.0, 0.3, X90_ENV, 0)
+    else:
+        b.emit(isa.done_cmd())                          # (no CR on other cores: never used)
+    b.pulse(RDRV, q['fr'], 0.0, q['ar'], RDRV_ENV, 0)
+    b.pulse(RDLO, q['fr'], q['rdlo_phase'], 1.0, RDLO_ENV, 0)
+    b.emit(isa.done_cmd())
+    return isa.words_to_u32(b.words), b.buffers()
+
+
+def rb_core_words(cliffs_c, cr, c, depth):
+    """Machine code of core c for a batch of sequences, vectorised: (words
+    (n, 4) u32 of all programs back to back, n_instr per sequence).
+    cliffs_c: [n_seq, depth] Clifford indices, cr: [n_seq, depth] CR bits."""
+    tmpl, _ = _rb_templates(c)
+    n = cliffs_c.shape[0]
+    pre = _RB_PRE_AX[cliffs_c // 4]                     # [n, depth, 2]
+    z = cliffs_c % 4
+    t = (RB_T0 + RB_LAYER_CLKS * np.arange(depth, dtype=np.int64))[None, :]
+    tid = np.full((n, depth, 6), -1, np.int8)
+    tt = np.zeros((n, depth, 6), np.uint32)
+    for i in (0, 1):
+        has = pre[:, :, i] >= 0
+        tid[:, :, 2 * i] = np.where(has, np.where(pre[:, :, i] == 1, _T_ALU_Y, _T_ALU_X), -1)
+        tid[:, :, 2 * i + 1] = np.where(has, _T_PULSE, -1)
+        tt[:, :, 2 * i + 1] = t + X90_CLKS * i
+    tid[:, :, 4] = np.where(z > 0, _T_Z1 + z - 1, -1)
+    if c == 0:
+        tid[:, :, 5] = np.where(cr > 0, _T_CR, -1)
+        tt[:, :, 5] = t + 2 * X90_CLKS
+    t_ro = RB_T0 + RB_LAYER_CLKS * depth
+    head = np.broadcast_to(np.array([_T_RESET, _T_INIT], np.int8), (n, 2))
+    tail = np.broadcast_to(np.array([_T_RDRV, _T_RDLO, _T_DONE], np.int8), (n, 3))
+    tid = np.concatenate([head, tid.reshape(n, -1), tail], axis=1)
+    tt = np.concatenate([np.zeros((n, 2), np.uint32), tt.reshape(n, -1),
+                         np.broadcast_to(np.array([t_ro, t_ro + RDLO_DELAY, 0], np.uint32), (n, 3))], axis=1)
+    keep = tid >= 0
+    n_instr = keep.sum(axis=1).astype(np.uint32)
+    words = tmpl[tid[keep].astype(np.int64)]            # program after program (row-major)
+    ts = tt[keep]
+    words[:, 0] |= ts << np.uint32(5)                   # cmd_time = cmd[36:5] (template field 0)
+    words[:, 1] |= ts >> np.uint32(27)
+    return words, n_instr
+
+
+class _SharedBuffers:
+    """ProgramSet.buffers for tables shared by every group: (g, c) -> core c's"""
+
+    def __init__(self, per_core):
+        self._per_core = per_core
+
+    def get(self, key, default=None):
+        return self._per_core.get(key[1], default)
+
+    def __getitem__(self, key):
+        return self._per_core[key[1]]
+
+
+def config4_rb_set(n_seq=100000, depth=200, seed=0x5EED, n_cores=2, chunk=8192):
+    """Config 4 at its stated size as a ProgramSet, generated vectorised:
+    group g = RB sequence g, program of (g, c) = c * n_seq + g (core-major
+    blocks).  Machine code identical to ``config4_rb`` (tests/test_workloads.py)."""
+    from .emulator import ProgramSet
+    C_ = 1
+    while C_ < n_cores:
+        C_ <<= 1
+    from concurrent.futures import ThreadPoolExecutor
+    starts = list(range(0, n_seq, chunk))
+
+    def one(s0):                                        # numpy releases the GIL in the bulk ops
+        cl, cr = rb_draws(np.arange(s0, min(s0 + chunk, n_seq)), depth, n_cores, seed)
+        return [rb_core_words(cl[:, :, c], cr, c, depth) for c in range(n_cores)]
+    with ThreadPoolExecutor(max(1, min(8, len(starts), os.cpu_count() or 1))) as pool:
+        parts = list(pool.map(one, starts))
+    # core-major: every sequence of core 0, then of core 1, ...
+    blocks = [parts[i][c] for c in range(n_cores) for i in range(len(starts))]
+    n_instr = np.concatenate([b[1] for b in blocks])
+    words = np.concatenate([b[0] for b in blocks]) if blocks else np.zeros((1, 4), np.uint32)
+    del parts, blocks
+    offsets = np.zeros(len(n_instr), np.uint64)
+    np.cumsum(n_instr[:-1], out=offsets[1:])
+    if offsets[-1] + n_instr[-1] >= 2 ** 32:
+        raise ValueError('program set exceeds 2^32 commands')
+    table = np.zeros((n_seq, C_), np.uint32)
+    empty = len(n_instr)
+    for c in range(C_):
+        table[:, c] = c * n_seq + np.arange(n_seq) if c < n_cores else empty
+    if C_ > n_cores:                                    # unused cores: one empty program
+        n_instr = np.append(n_instr, np.uint32(0))
+        offsets = np.append(offsets, np.uint64(len(words)))
+    bufs = {c: _rb_templates(c)[1] for c in range(n_cores)}
+    return ProgramSet.from_arrays(words, offsets.astype(np.uint32), n_instr, table.reshape(-1), n_seq, C_,
+                                  buffers=_SharedBuffers(bufs))

@@ -23,7 +23,11 @@
  * exceptions cross the ABI; dpemu_last_error() has the message).  Caller
  * owns every pointer it passes.  Device-pointer outputs must be device
  * memory of the context's device; NULL skips that output.  A context is not
- * re-entrant; use one per device (one process per GPU).
+ * re-entrant (one host thread at a time); use one per device (one process
+ * per GPU).  Work a context enqueues runs in call order even across streams:
+ * a call on a stream other than the previous call's first makes that stream
+ * wait for the previous call's work (the context's scratch buffers and
+ * uploaded constants are shared by its calls).
  */
 #ifndef DPEMU_H
 #define DPEMU_H
@@ -35,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DPEMU_ABI_VERSION 3
+#define DPEMU_ABI_VERSION 4
 
 /* ---- error codes ---------------------------------------------------- */
 #define DPEMU_OK            0
@@ -71,12 +75,13 @@ extern "C" {
 #define DPEMU_TRACE_QCLK_LOAD 16  /* INC_QCLK loaded qclk (value = qclk at t)             */
 #define DPEMU_TRACE_QCLK_RST  17  /* SYNC reset qclk (value 0 at t)                       */
 
-#define DPEMU_X_PROG_LDS    0x1   /* stage each workgroup's programs in LDS when they fit    */
-#define DPEMU_X_GROUP_MAJOR 0x2   /* group-major thread order (shots_per_group 1, n % n_groups == 0) */
+/* execution knobs (dpemu_config.exec_flags): results never depend on them; the
+ * parity tests run every variant against the oracle */
+#define DPEMU_X_PROG_LDS    0x1   /* general interpreter: stage each workgroup's programs in LDS when they fit */
 #define DPEMU_X_HIST_DIRECT 0x4   /* outcome histogram: atomics straight into out->hist       */
 #define DPEMU_X_HIST_REPL   0x8   /* outcome histogram: privatised replicas + reduce          */
 #define DPEMU_X_PROG_MAJOR  0x10  /* fetch from the program-major image, not the command-major copy */
-#define DPEMU_X_GENERAL     0x20  /* run pulse-only programs on the general interpreter, not straight.hip */
+#define DPEMU_X_GENERAL     0x20  /* run branch-free programs on the general interpreter too */
 
 #define DPEMU_MAX_CORES 64
 #define DPEMU_MEAS_LOOKUP 16      /* a core's first 16 measurements are visible to fproc;
@@ -93,8 +98,8 @@ typedef struct dpemu_config {
     uint32_t n_groups;         /* program groups; group(s) = (s/shots_per_group)%n_groups */
     uint32_t shots_per_group;  /* >= 1                                                  */
     uint32_t max_cycles;       /* <= 2^31 - 64                                          */
-    uint32_t event_cap;        /* event slots per lane                                   */
-    uint32_t trace_cap;        /* register-trace slots per lane (0 = no trace)           */
+    uint32_t event_cap;        /* event slots per lane (<= DPEMU_MAX_EVENT_CAP)           */
+    uint32_t trace_cap;        /* register-trace slots per lane (0 = no trace; <= DPEMU_MAX_EVENT_CAP) */
     uint32_t meas_cap;         /* measurement slots per lane (<= 32)                     */
     uint32_t fproc_mode;       /* DPEMU_FPROC_*                                          */
     uint32_t meas_elem;        /* strobe with (cfg & 3) == meas_elem is a readout; 0xFF none */
@@ -114,18 +119,26 @@ typedef struct dpemu_config {
      *   outcome = x > ro_thr
      * with ro_win != 0 the separation also scales with the readout window:
      *   s = (s * (min(W, ro_win) * floor(2^24 / ro_win))) >> 24   (int64)
+     * unless W == 0: a CW envelope word (length field 0) plays until the next
+     * pulse, so it integrates the whole window and s is not scaled
      * W = the strobe's envelope-length field (env word bits 23:12, in env words)
      * -- a window shorter than ro_win integrates less signal                  */
     int32_t  ro_sep;           /* half the state separation at full readout amplitude    */
     uint32_t ro_sigma;         /* noise scale, Q16 (noise sigma = ro_sigma / 2^16 * 37837.6) */
     int32_t  ro_thr;           /* discriminator threshold                                */
-    uint32_t ro_win;           /* reference readout window (env words); 0 = amplitude only */
+    uint32_t ro_win;           /* reference readout window (env words, < 4096); 0 = amplitude only */
 } dpemu_config;
 
 #define DPEMU_MEAS_STATE   0
 #define DPEMU_MEAS_READOUT 1
 
+#define DPEMU_MAX_EVENT_CAP (1u << 20)   /* event / trace slots per lane (validate)  */
+
 /*
+ * Lanes: lane L = core * n_shots + (shot - shot_begin) -- core-major, so the
+ * lanes of one core's shots are adjacent (the lanes that run one program in
+ * lockstep write whole cache lines).
+ *
  * Per-lane summary, 8 x u32:
  *   w0 t_end      decode cycle of DONE (done_gate from t_end+1) or of the stop
  *   w1 ip[15:0] | status[23:16] | flags[31:24]
@@ -136,17 +149,18 @@ typedef struct dpemu_config {
  *   w6 meas_bits  outcome of measurement m in bit m (m < 32)
  *   w7 n_trace    register-trace records (may exceed trace_cap)
  *
- * Event (slot-major: slot k of lane L at index k*n_lanes + L):
- *   ev_main uint4 {t, qclk, env[23:0] | cfg<<24 | kind<<28, phase[16:0] | freq<<17}
- *   ev_amp  uint16 amp
+ * Event (slot-major: slot k of lane L at index k*n_lanes + L), one 16-B record
+ * per pulse_iface strobe (hdl/pulse_iface.sv:2-6) or pulse reset:
+ *   uint4 {t, env[23:0] | cfg<<24 | kind<<28, phase[16:0] | freq<<17, amp[15:0]}
+ * (qclk at an event follows from t and the lane's qclk loads / resets, which
+ * the register trace records)
  * Trace (slot-major): uint4 {t (first cycle the value is visible), addr, value, 0}
  * Meas  (slot-major): uint2 {valid cycle, bit}
  * Histogram: uint64 [n_groups][2^C] (C <= 12), key bit c = last outcome of core c.
  */
 typedef struct dpemu_outputs {
     uint32_t *summary;    /* [n_lanes][8]                      */
-    uint32_t *ev_main;    /* [event_cap][n_lanes][4]           */
-    uint16_t *ev_amp;     /* [event_cap][n_lanes]              */
+    uint32_t *events;     /* [event_cap][n_lanes][4]           */
     uint32_t *trace;      /* [trace_cap][n_lanes][4]           */
     uint32_t *meas;       /* [meas_cap][n_lanes][2]            */
     uint32_t *regs;       /* [16][n_lanes] final register file */
@@ -166,11 +180,12 @@ const char *dpemu_last_error(dpemu_ctx *ctx);
  * little-endian u128 commands as u32 quads (word i of the u128 = bits
  * [32i+31:32i], cmd_mem_iface.sv:19-21), program p starting at quad
  * offsets[p] with n_instr[p] commands (assembler cmd_buf bytes reinterpret
- * directly).  Fetch beyond n_instr reads 0 (= DONE), as the zero-initialised
- * 2^16-deep cmd_mem of toplevel_sim does.
- * prog_table[g*C + c] = program run by core c of shots in group g.
+ * directly); offsets[p] + n_instr[p] <= n_words for every p.  Fetch beyond
+ * n_instr reads 0 (= DONE), as the zero-initialised 2^16-deep cmd_mem of
+ * toplevel_sim does.  prog_table[g*C + c] = program run by core c of shots
+ * in group g.  Replaces load_commands (cocotb/proc/test_proc.py:29-38).
  */
-int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, const uint32_t *offsets,
+int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words, const uint32_t *offsets,
                         const uint32_t *n_instr, uint32_t n_programs,
                         const uint32_t *prog_table, uint32_t n_groups, uint32_t cores_per_shot);
 
@@ -195,8 +210,8 @@ int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
  * int16 {I, Q} pairs; sample j is at emulated cycle j / spc.
  *
  * The dpemu_dds_channels arrays are HOST memory (n_channels entries each);
- * summary / ev_main / ev_amp / env_tables / freq_tables / iq_out are device
- * pointers.  n_samples must be a multiple of 4; event_cap <= 1024.
+ * summary / events / env_tables / freq_tables / iq_out are device pointers.
+ * n_samples must be a multiple of 4; event_cap <= 1024.
  */
 typedef struct dpemu_dds_channels {
     uint32_t n_channels;
@@ -214,8 +229,8 @@ typedef struct dpemu_dds_channels {
 } dpemu_dds_channels;
 
 int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uint32_t *summary,
-              const uint32_t *ev_main, const uint16_t *ev_amp, const uint32_t *env_tables,
-              const uint32_t *freq_tables, int16_t *iq_out, void *stream);
+              const uint32_t *events, const uint32_t *env_tables, const uint32_t *freq_tables,
+              int16_t *iq_out, void *stream);
 
 /* The Q15 sine table both the DDS kernel and its CPU restatement use. */
 int dpemu_dds_sin_lut(int16_t *out4096);
@@ -227,7 +242,7 @@ int dpemu_dds_sin_lut(int16_t *out4096);
  * dpemu_kernel_times waits for the recorded pairs, writes up to max_n
  * elapsed times in ms (oldest first) to ms, *n_out = how many, and clears the
  * record.  dpemu_last_kernel names the interpreter variant the last dpemu_run
- * launched (e.g. "straight_kernel<rows,pulse,fb1>", "interp_kernel<feat=0x3>").
+ * launched (e.g. "straight_kernel<rows,fb1>", "macro_kernel", "interp_kernel<feat=0x3>").
  */
 int         dpemu_set_kernel_timing(dpemu_ctx *ctx, int enable);
 int         dpemu_kernel_times(dpemu_ctx *ctx, float *ms, int max_n, int *n_out);

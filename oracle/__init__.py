@@ -68,7 +68,7 @@ class LaneOut(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         'status', 'flags', 't_end', 'ip', 'qclk_end', 'n_instr', 'n_events', 'n_trace',
         'n_meas', 'meas_bits')] + [('regs', C.c_uint32 * 16),
-                                   ('ev', C.POINTER(C.c_uint32)), ('amp', C.POINTER(C.c_uint16)),
+                                   ('ev', C.POINTER(C.c_uint32)),
                                    ('tr', C.POINTER(C.c_uint32)), ('meas', C.POINTER(C.c_uint32))]
 
 
@@ -104,13 +104,15 @@ def _setup(L):
     if hasattr(L, 'fast_run'):
         L.fast_run.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
         L.fast_run.restype = C.c_int
+    L.rtl_run_batch.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_int]
+    L.rtl_run_batch.restype = C.c_int64
     L.oracle_dds_sin_lut.argtypes = [C.c_void_p]
     L.oracle_dds.argtypes = [C.c_void_p, C.c_int]
 
 
 class DDSArgs(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ('n_channels', 'n_lanes', 'n_samples', 'event_cap')] + [
-        (n, C.c_void_p) for n in ('ch', 'summary', 'ev_main', 'ev_amp', 'env', 'freq', 'iq')]
+        (n, C.c_void_p) for n in ('ch', 'summary', 'events', 'env', 'freq', 'iq')]
 
 
 def dds_sin_lut():
@@ -119,14 +121,13 @@ def dds_sin_lut():
     return out
 
 
-def dds(desc, summary, ev_main, ev_amp, env, freq, n_samples, event_cap, threads=0):
+def dds(desc, summary, events, env, freq, n_samples, event_cap, threads=0):
     """oracle_dds: desc (n_ch, 8) u32 [lane, elem, spc, interp, env_off, env_len,
-    freq_off, freq_len]; event arrays in dpemu_run layout (host); returns
+    freq_off, freq_len]; event array in dpemu_run layout (host); returns
     (n_ch, n_samples) u32 samples, I in the low half, Q in the high half."""
     desc = np.ascontiguousarray(desc, np.uint32).reshape(-1, 8)
     summary = np.ascontiguousarray(summary).view(np.uint32)
-    ev_main = np.ascontiguousarray(ev_main).view(np.uint32)
-    ev_amp = np.ascontiguousarray(ev_amp).view(np.uint16)
+    events = np.ascontiguousarray(events).view(np.uint32)
     env = np.ascontiguousarray(env, np.uint32)
     freq = np.ascontiguousarray(freq, np.uint32)
     if len(env) == 0:
@@ -134,10 +135,10 @@ def dds(desc, summary, ev_main, ev_amp, env, freq, n_samples, event_cap, threads
     if len(freq) == 0:
         freq = np.zeros(1, np.uint32)
     n_lanes = summary.shape[0]
-    assert ev_main.shape[:2] == (event_cap, n_lanes) and ev_amp.shape == (event_cap, n_lanes)
+    assert events.shape[:2] == (event_cap, n_lanes)
     iq = np.zeros((desc.shape[0], int(n_samples)), np.uint32)
     a = DDSArgs(desc.shape[0], n_lanes, int(n_samples), int(event_cap), desc.ctypes.data,
-                summary.ctypes.data, ev_main.ctypes.data, ev_amp.ctypes.data, env.ctypes.data,
+                summary.ctypes.data, events.ctypes.data, env.ctypes.data,
                 freq.ctypes.data, iq.ctypes.data)
     lib().oracle_dds(C.addressof(a), int(threads))
     return iq
@@ -262,7 +263,7 @@ class PulseRegTB:
 
 
 def fast_run(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots, threads=0,
-             want=('summary', 'ev_main', 'ev_amp', 'trace', 'meas', 'regs', 'hist')):
+             want=('summary', 'events', 'trace', 'meas', 'regs', 'hist')):
     """Event-driven model over shots [shot_begin, shot_begin + n_shots).
 
     cfg: distributed_processor_amd._abi.Config; words: (n, 4) uint32 of all
@@ -281,6 +282,24 @@ def fast_run(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots, thre
     if rc != 0:
         raise RuntimeError('fast_run failed: {}'.format(rc))
     return out
+
+
+def rtl_run_batch(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots, horizon, threads=0):
+    """oracle_rtl over shots [shot_begin, shot_begin + n_shots), OpenMP over
+    shots: the per-clock CPU baseline.  Returns (summary rows (n_lanes, 8) u32
+    in the dpemu layout (core-major lanes), number of shots whose every core
+    reached DONE)."""
+    words = np.ascontiguousarray(words, dtype=np.uint32)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+    n_instr = np.ascontiguousarray(n_instr, dtype=np.uint32)
+    prog_table = np.ascontiguousarray(prog_table, dtype=np.uint32)
+    summary = np.zeros((int(n_shots) * cfg.cores_per_shot, 8), np.uint32)
+    done = lib().rtl_run_batch(C.addressof(cfg), words.ctypes.data, offsets.ctypes.data, n_instr.ctypes.data,
+                               prog_table.ctypes.data, int(shot_begin), int(n_shots), int(horizon),
+                               summary.ctypes.data, int(threads))
+    if done < 0:
+        raise RuntimeError('rtl_run_batch failed')
+    return summary, int(done)
 
 
 def shot_cfg_from_config(cfg):
@@ -336,24 +355,22 @@ def rtl_run_shot(cfg, programs, shot, horizon, ev_cap=256, tr_cap=256, meas_cap=
     bufs = []
     for c in range(ncore):
         ev = np.zeros((ev_cap, 4), np.uint32)
-        amp = np.zeros(ev_cap, np.uint16)
         tr = np.zeros((max(tr_cap, 1), 4), np.uint32)
         ms = np.zeros((max(meas_cap, 1), 2), np.uint32)
-        bufs.append((ev, amp, tr, ms))
+        bufs.append((ev, tr, ms))
         outs[c].ev = ev.ctypes.data_as(C.POINTER(C.c_uint32))
-        outs[c].amp = amp.ctypes.data_as(C.POINTER(C.c_uint16))
         outs[c].tr = tr.ctypes.data_as(C.POINTER(C.c_uint32))
         outs[c].meas = ms.ctypes.data_as(C.POINTER(C.c_uint32))
     ok = L.rtl_run_shot(C.byref(cfg), pp, ni, shot, horizon, ev_cap, tr_cap, meas_cap, outs)
     res = []
     for c in range(ncore):
         o = outs[c]
-        ev, amp, tr, ms = bufs[c]
+        ev, tr, ms = bufs[c]
         ne, nt, nm = min(o.n_events, ev_cap), min(o.n_trace, tr_cap), min(o.n_meas, meas_cap)
         res.append({'status': o.status, 'flags': o.flags, 't_end': o.t_end, 'ip': o.ip,
                     'qclk_end': o.qclk_end, 'n_instr': o.n_instr, 'n_events': o.n_events,
                     'n_trace': o.n_trace, 'n_meas': o.n_meas, 'meas_bits': o.meas_bits,
                     'regs': np.array(o.regs[:], np.uint32),
-                    'events': ev[:ne].copy(), 'amp': amp[:ne].copy(), 'trace': tr[:nt].copy(),
+                    'events': ev[:ne].copy(), 'trace': tr[:nt].copy(),
                     'meas': ms[:nm].copy()})
     return bool(ok), res

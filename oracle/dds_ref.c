@@ -75,18 +75,21 @@ void oracle_dds(const oracle_dds_args *a, int n_threads)
         uint32_t n_ev = a->summary[8ull * lane + 2];
         if (n_ev > a->event_cap) n_ev = a->event_cap;
         uint32_t *out = a->iq + (uint64_t)ch * a->n_samples;
+        /* the latest strobe of the element and the latest pulse_reset at or
+         * before cycle n: a lane's events are in time order, so one cursor
+         * walks them as n grows (ties: the later event wins) */
+        uint32_t e = 0;
+        int have = 0;
+        uint32_t st_t = 0, env_w = 0, pf = 0, amp = 0, t_ref = 0;
         for (uint32_t j = 0; j < a->n_samples; j++) {
             const uint32_t n = j / spc, k = j % spc;
-            int have = 0;
-            uint32_t st_t = 0, env_w = 0, pf = 0, amp = 0, t_ref = 0;
-            for (uint32_t e = 0; e < n_ev; e++) {
-                const uint32_t *ev = a->ev_main + 4 * ((uint64_t)e * a->n_lanes + lane);
-                if (ev[0] > n) continue;
-                const uint32_t kind = ev[2] >> 28, cfg = (ev[2] >> 24) & 0xF;
+            for (; e < n_ev; e++) {
+                const uint32_t *ev = a->events + 4 * ((uint64_t)e * a->n_lanes + lane);
+                if (ev[0] > n) break;
+                const uint32_t kind = ev[1] >> 28, cfg = (ev[1] >> 24) & 0xF;
                 if (kind == DPEMU_EV_PULSE_RESET) t_ref = ev[0];
                 if (kind == DPEMU_EV_STROBE && (cfg & 3) == elem) {
-                    have = 1; st_t = ev[0]; env_w = ev[2] & 0xFFFFFF; pf = ev[3];
-                    amp = a->ev_amp[(uint64_t)e * a->n_lanes + lane];
+                    have = 1; st_t = ev[0]; env_w = ev[1] & 0xFFFFFF; pf = ev[2]; amp = ev[3] & 0xFFFF;
                 }
             }
             int32_t oi = 0, oq = 0;

@@ -46,7 +46,8 @@ typedef struct {
     uint32_t status, flags, n_instr_exec, n_events, n_trace, n_meas, meas_bits, last_bit;
     uint32_t t_end, ip_end, qclk_end;
     uint32_t mt[MEAS_LOOKUP]; uint8_t mb[MEAS_LOOKUP];   /* measurement (valid cycle, bit) */
-    uint32_t lane;                   /* output lane index */
+    uint32_t lane;                   /* output lane index (core-major) */
+    uint32_t core;
 } flane;
 
 typedef struct {
@@ -84,19 +85,19 @@ static void emit_event(fshot *s, flane *l, uint32_t t, uint32_t kind)
 {
     const dpemu_config *cfg = s->cfg;
     if (l->n_events < cfg->event_cap) {
-        if (s->out->ev_main) {
-            uint32_t *e = s->out->ev_main + 4 * ((uint64_t)l->n_events * s->n_lanes + l->lane);
-            e[0] = t; e[1] = qclk_at(l, t);
-            e[2] = (l->pr[0] & 0xFFFFFF) | ((l->pr[4] & 0xF) << 24) | (kind << 28);
-            e[3] = (l->pr[1] & 0x1FFFF) | ((l->pr[2] & 0x1FF) << 17);
+        if (s->out->events) {     /* pulse_iface snapshot (include/dpemu.h event record) */
+            uint32_t *e = s->out->events + 4 * ((uint64_t)l->n_events * s->n_lanes + l->lane);
+            e[0] = t;
+            e[1] = (l->pr[0] & 0xFFFFFF) | ((l->pr[4] & 0xF) << 24) | (kind << 28);
+            e[2] = (l->pr[1] & 0x1FFFF) | ((l->pr[2] & 0x1FF) << 17);
+            e[3] = l->pr[3] & 0xFFFF;
         }
-        if (s->out->ev_amp) s->out->ev_amp[(uint64_t)l->n_events * s->n_lanes + l->lane] = (uint16_t)l->pr[3];
     } else l->flags |= DPEMU_F_EVENT_OVF;
     l->n_events++;
 
     /* measurement model: readout strobe -> meas_valid meas_latency clocks later */
     if (kind == DPEMU_EV_STROBE && cfg->meas_elem != 0xFF && (l->pr[4] & 3) == cfg->meas_elem) {
-        uint32_t core = l->lane % s->C;
+        uint32_t core = l->core;
         uint32_t m = l->n_meas;
         uint32_t bit = oracle_meas_bit(cfg->seed, s->shot, core, m, cfg->p1_threshold[core], l->pr[3],
                                        cfg->meas_model, cfg->ro_sep, cfg->ro_sigma, cfg->ro_thr,
@@ -242,7 +243,7 @@ static uint32_t strobe_bound(const fshot *s, const flane *l)
     case M_RUN: return l->t + 2;
     case M_LUT: return l->wait_d + 7;
     case M_SYNC: {
-        if (!((s->part >> (l->lane % s->C)) & 1)) return INF32;   /* never released */
+        if (!((s->part >> l->core) & 1)) return INF32;   /* never released */
         uint64_t m = 0;
         for (uint32_t c = 0; c < s->C; c++) {
             if (!((s->part >> c) & 1)) continue;
@@ -456,7 +457,8 @@ int fast_run(const dpemu_config *cfg, const uint32_t *words, const uint32_t *off
             l->prog = words + 4 * (uint64_t)offsets[p];
             l->n_instr = n_instr[p];
             l->qa_t = 1; l->qa_q = 0;
-            l->lane = (uint32_t)((uint64_t)si * C + c);
+            l->lane = (uint32_t)((uint64_t)c * n_shots + (uint64_t)si);   /* core-major lanes */
+            l->core = c;
         }
         run_shot(s);
         uint32_t key = 0;

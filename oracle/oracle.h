@@ -161,8 +161,7 @@ typedef struct {
     uint32_t status, flags, t_end, ip, qclk_end, n_instr;
     uint32_t n_events, n_trace, n_meas, meas_bits;
     uint32_t regs[16];
-    uint32_t *ev;      /* [ev_cap][4] */
-    uint16_t *amp;     /* [ev_cap]    */
+    uint32_t *ev;      /* [ev_cap][4] event records (include/dpemu.h) */
     uint32_t *tr;      /* [tr_cap][4] */
     uint32_t *meas;    /* [meas_cap][2] */
 } oracle_lane_out;
@@ -170,6 +169,11 @@ typedef struct {
 int rtl_run_shot(const oracle_shot_cfg *cfg, const uint32_t *const *progs, const uint32_t *n_instr,
                  uint64_t shot, uint32_t horizon, uint32_t ev_cap, uint32_t tr_cap,
                  uint32_t meas_cap, oracle_lane_out *out);
+
+/* per-clock batch over shots (OpenMP), dpemu summary rows; returns shots all-DONE */
+int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
+                      const uint32_t *n_instr, const uint32_t *prog_table, uint64_t shot_begin,
+                      uint64_t n_shots, uint32_t horizon, uint32_t *summary, int n_threads);
 
 /* ---- event-driven model, dpemu_run-compatible batch entry ------------------ */
 int fast_run(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
@@ -182,8 +186,7 @@ typedef struct {
     uint32_t n_channels, n_lanes, n_samples, event_cap;
     const uint32_t *ch;          /* [n_channels][8]: lane, elem, spc, interp, env_off, env_len, freq_off, freq_len */
     const uint32_t *summary;     /* [n_lanes][8] */
-    const uint32_t *ev_main;     /* [event_cap][n_lanes][4] */
-    const uint16_t *ev_amp;      /* [event_cap][n_lanes] */
+    const uint32_t *events;      /* [event_cap][n_lanes][4] */
     const uint32_t *env, *freq;
     uint32_t *iq;                /* [n_channels][n_samples] */
 } oracle_dds_args;

@@ -56,8 +56,9 @@ uint32_t oracle_meas_bit(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m
     if (meas_model != DPEMU_MEAS_READOUT) return state;
     int64_t z = (int64_t)(r[1] & 0xFFFFu) + (r[1] >> 16) + (r[2] & 0xFFFFu) + (r[2] >> 16) - 131070;
     int64_t s = ((int64_t)ro_sep * (int64_t)(amp & 0xFFFFu)) >> 16;
-    if (ro_win) {   /* window: (s * min(W, ro_win) * floor(2^24 / ro_win)) >> 24, W = env bits 23:12 */
-        uint32_t w = (env >> 12) & 0xFFFu;
+    const uint32_t w = (env >> 12) & 0xFFFu;
+    if (ro_win && w) {   /* window: (s * min(W, ro_win) * floor(2^24 / ro_win)) >> 24, W = env bits 23:12;
+                            W = 0 is a CW envelope (plays until the next pulse): no scaling */
         s = (s * (int64_t)((w < ro_win ? w : ro_win) * ((1u << 24) / ro_win))) >> 24;
     }
     int64_t x = (state ? s : -s) + ((z * (int64_t)ro_sigma) >> 16);

@@ -22,6 +22,9 @@
 #include "oracle.h"
 
 #include <stdlib.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <string.h>
 
 /* ctrl.v:84-91 */
@@ -491,10 +494,10 @@ static void put_event(oracle_lane_out *lo, uint32_t cap, uint32_t t, const rtl_c
 {
     if (lo->n_events < cap) {
         uint32_t *e = lo->ev + 4 * lo->n_events;
-        e[0] = t; e[1] = o->qclk;
-        e[2] = (o->env & 0xFFFFFF) | ((o->cfg & 0xF) << 24) | (kind << 28);
-        e[3] = (o->phase & 0x1FFFF) | ((o->freq & 0x1FF) << 17);
-        lo->amp[lo->n_events] = (uint16_t)o->amp;
+        e[0] = t;
+        e[1] = (o->env & 0xFFFFFF) | ((o->cfg & 0xF) << 24) | (kind << 28);
+        e[2] = (o->phase & 0x1FFFF) | ((o->freq & 0x1FF) << 17);
+        e[3] = o->amp & 0xFFFF;
     } else lo->flags |= DPEMU_F_EVENT_OVF;
     lo->n_events++;
 }
@@ -571,4 +574,76 @@ int rtl_run_shot(const oracle_shot_cfg *cfg, const uint32_t *const *progs, const
     }
     free(s);
     return all_done;
+}
+
+/* ---------------------------------------------------------------------- */
+/* per-clock batch: the CPU baseline closest to the Verilator testbench     */
+/* ---------------------------------------------------------------------- */
+/*
+ * Shots [shot_begin, shot_begin + n_shots) of a dpemu program set, one
+ * rtl_run_shot per shot, OpenMP over shots: the per-clock analogue of the
+ * reference's Verilator/cocotb run (cocotb/proc/Makefile:1-14), which cannot
+ * run in this image.  Events, traces and measurements go to per-thread
+ * buffers of the config's caps (the same work as a dpemu run); the summary
+ * rows (dpemu layout, include/dpemu.h) go to `summary` when it is non-null.
+ * `horizon`: cycles simulated past the first decode at most.  Returns the
+ * number of shots whose every core reached DONE.
+ */
+int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
+                      const uint32_t *n_instr, const uint32_t *prog_table, uint64_t shot_begin,
+                      uint64_t n_shots, uint32_t horizon, uint32_t *summary, int n_threads)
+{
+    const uint32_t C = cfg->cores_per_shot;
+    if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1))) return -1;
+    oracle_shot_cfg sc;
+    memset(&sc, 0, sizeof sc);
+    sc.cores = C; sc.fproc_mode = cfg->fproc_mode; sc.sync_external = 0;
+    sc.meas_elem = cfg->meas_elem; sc.meas_latency = cfg->meas_latency; sc.sync_latency = cfg->sync_latency;
+    sc.sync_mask = cfg->sync_mask; sc.seed = cfg->seed; sc.lut_mask = cfg->lut_mask;
+    memcpy(sc.p1_threshold, cfg->p1_threshold, sizeof sc.p1_threshold);
+    memcpy(sc.lut_table, cfg->lut_table, sizeof sc.lut_table);
+    sc.meas_model = cfg->meas_model; sc.ro_sep = cfg->ro_sep; sc.ro_sigma = cfg->ro_sigma;
+    sc.ro_thr = cfg->ro_thr; sc.ro_win = cfg->ro_win;
+    const uint32_t ev_cap = cfg->event_cap ? cfg->event_cap : 1, tr_cap = cfg->trace_cap ? cfg->trace_cap : 1;
+    const uint32_t ms_cap = cfg->meas_cap ? cfg->meas_cap : 1;
+    int64_t done = 0;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#else
+    (void)n_threads;
+#endif
+    #pragma omp parallel reduction(+ : done)
+    {
+        oracle_lane_out *lo = (oracle_lane_out *)calloc(C, sizeof(oracle_lane_out));
+        uint32_t *ev = (uint32_t *)malloc((size_t)C * ev_cap * 16);
+        uint32_t *tr = (uint32_t *)malloc((size_t)C * tr_cap * 16);
+        uint32_t *ms = (uint32_t *)malloc((size_t)C * ms_cap * 8);
+        for (uint32_t c = 0; c < C; c++) {
+            lo[c].ev = ev + (size_t)c * ev_cap * 4;
+            lo[c].tr = tr + (size_t)c * tr_cap * 4; lo[c].meas = ms + (size_t)c * ms_cap * 2;
+        }
+        const uint32_t *progs[DPEMU_MAX_CORES];
+        uint32_t ni[DPEMU_MAX_CORES];
+        #pragma omp for schedule(dynamic, 4)
+        for (int64_t si = 0; si < (int64_t)n_shots; si++) {
+            const uint64_t shot = shot_begin + (uint64_t)si;
+            const uint32_t g = (uint32_t)((shot / cfg->shots_per_group) % cfg->n_groups);
+            for (uint32_t c = 0; c < C; c++) {
+                const uint32_t p = prog_table[(uint64_t)g * C + c];
+                progs[c] = words + 4 * (uint64_t)offsets[p];
+                ni[c] = n_instr[p];
+            }
+            done += rtl_run_shot(&sc, progs, ni, shot, horizon, cfg->event_cap, cfg->trace_cap, cfg->meas_cap, lo);
+            if (summary)
+                for (uint32_t c = 0; c < C; c++) {
+                    uint32_t *sm = summary + 8 * ((uint64_t)c * n_shots + (uint64_t)si);   /* core-major */
+                    sm[0] = lo[c].t_end;
+                    sm[1] = (lo[c].ip & 0xFFFF) | ((lo[c].status & 0xFF) << 16) | ((lo[c].flags & 0xFF) << 24);
+                    sm[2] = lo[c].n_events; sm[3] = lo[c].n_instr; sm[4] = lo[c].qclk_end;
+                    sm[5] = lo[c].n_meas; sm[6] = lo[c].meas_bits; sm[7] = lo[c].n_trace;
+                }
+        }
+        free(lo); free(ev); free(tr); free(ms);
+    }
+    return done;
 }

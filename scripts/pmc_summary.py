@@ -1,6 +1,6 @@
 """Summarise rocprofv3 kernel-trace + PMC passes of the bench into per-kernel JSON.
 
-usage: python scripts/pmc_summary.py <prof root (e.g. gpurun_out/r01)> <tag> [dest dir]
+usage: python scripts/pmc_summary.py <prof root (e.g. gpurun_out/r01)> <tag> [dest dir] [key=substr|substr,...]
 
 Reads <root>/prof_trace or <root>/trace (--kernel-trace --stats) and every
 other subdirectory's PMC pass (counter_collection.csv), groups dispatches by (kernel, grid size),
@@ -54,6 +54,11 @@ def which(name):
 def main():
     root, tag = sys.argv[1], sys.argv[2]
     dest = sys.argv[3] if len(sys.argv) > 3 else root
+    if len(sys.argv) > 4:          # kernel keys of this run: key=substr|substr,...
+        KERNELS.clear()
+        for item in sys.argv[4].split(','):
+            k, subs = item.split('=')
+            KERNELS[k] = tuple(subs.split('|'))
     os.makedirs(dest, exist_ok=True)
     # kernel trace: per (kernel, grid) durations
     dur = collections.defaultdict(list)

@@ -1,0 +1,24 @@
+#!/bin/bash
+# rocprofv3 kernel trace + separate PMC passes over any python command.
+# usage: scripts/prof_cmd.sh <out dir under gpurun_out> <python args...>
+# e.g.   scripts/prof_cmd.sh gpurun_out/rb scripts/rb_probe.py --steps 3
+# Each pass runs under its own time limit; the script stops at the first failure.
+out=$1; shift
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+export TMPDIR=/tmp
+mkdir -p $out
+run() {   # name, limit, rocprofv3 options...
+    local name=$1 lim=$2; shift 2
+    timeout -k 10 $lim rocprofv3 "$@" -d $out/$name -o $name --output-format csv -- python3 "${ARGS[@]}" \
+        > $out/$name.log 2>&1
+    local rc=$?
+    echo "$name rc=$rc"
+    return $rc
+}
+ARGS=("$@")
+run trace 300 --kernel-trace --stats || exit $?
+run fetch 300 --pmc FETCH_SIZE || exit $?
+run write 300 --pmc WRITE_SIZE || exit $?
+run sq1 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU || exit $?
+run sq2 300 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE || exit $?
+find $out/trace -name "*kernel_stats.csv" -exec cat {} \;

@@ -32,7 +32,17 @@ def test_abi_version_and_struct_sizes():
     assert L.dpemu_abi_version() == _abi.ABI_VERSION
     # dpemu_config: 12 u32 + 2 u64 + 2 u32 + 64 u32 + 256 u64 + the readout model's 4 x 32 bit
     assert C.sizeof(_abi.Config) == 12 * 4 + 16 + 8 + 64 * 4 + 256 * 8 + 16
-    assert C.sizeof(_abi.Outputs) == 7 * 8
+    assert C.sizeof(_abi.Outputs) == 6 * 8
+    assert C.sizeof(_abi.DDSChannels) == 4 * 4 + 8 * 8
+
+
+def test_output_struct_matches_header():
+    """the ctypes mirror lists dpemu_outputs' fields in the header's order"""
+    with open(os.path.join(REPO, 'include', 'dpemu.h')) as f:
+        txt = f.read()
+    body = re.search(r'typedef struct dpemu_outputs \{(.*?)\} dpemu_outputs;', txt, re.S).group(1)
+    fields = re.findall(r'\*\s*(\w+);', body)
+    assert fields == [n for n, _ in _abi.Outputs._fields_] == list(_abi.OUTPUT_NAMES)
 
 
 def test_sin_lut_symmetry():
@@ -61,5 +71,9 @@ def test_config_validation():
         _abi.make_config(4, max_cycles=2 ** 31)
     with pytest.raises(ValueError):
         _abi.make_config(4, lut_mask=0)
+    with pytest.raises(ValueError):
+        _abi.make_config(4, event_cap=2 ** 21)
+    with pytest.raises(ValueError):
+        _abi.make_config(4, readout=dict(sep=1, win=4096))
     cfg = _abi.make_config(8, p1=[0.0, 1.0, 0.5])
     assert cfg.p1_threshold[0] == 0 and cfg.p1_threshold[1] == 0xFFFFFFFF and cfg.p1_threshold[2] == 2 ** 31

@@ -30,14 +30,12 @@ def events(lane_events, event_cap=16):
     n_lanes = len(lane_events)
     summary = np.zeros((n_lanes, 8), np.uint32)
     ev = np.zeros((event_cap, n_lanes, 4), np.uint32)
-    amp = np.zeros((event_cap, n_lanes), np.uint16)
     for L, evs in enumerate(lane_events):
         summary[L, 2] = len(evs)
         for k, e in enumerate(evs[:event_cap]):
-            ev[k, L] = (e['t'], e['t'], (e.get('env', 0) & 0xFFFFFF) | (e.get('cfg', 0) << 24)
-                        | (e.get('kind', 0) << 28), (e.get('phase', 0) & 0x1FFFF) | (e.get('freq', 0) << 17))
-            amp[k, L] = e.get('amp', 0)
-    return summary, ev, amp
+            ev[k, L] = (e['t'], (e.get('env', 0) & 0xFFFFFF) | (e.get('cfg', 0) << 24) | (e.get('kind', 0) << 28),
+                        (e.get('phase', 0) & 0x1FFFF) | (e.get('freq', 0) << 17), e.get('amp', 0) & 0xFFFF)
+    return summary, ev
 
 
 def s16(x):
@@ -80,10 +78,10 @@ def test_oracle_vs_float_model(spc, interp):
     freq_buf = el.get_freq_buffer([None, f])
     L = len(env_buf) // 4
     st = dict(t=7, cfg=1, env=el.get_env_word(0, len(env_buf)), phase=12345, freq=1, amp=50000)
-    summary, ev, amp = events([[dict(t=2, kind=1), st]])
+    summary, ev = events([[dict(t=2, kind=1), st]])
     n_samples = 4 * ((st['t'] + 40) * spc // 4)
     desc = np.array([[0, 1, spc, interp, 0, len(env_buf), 0, len(freq_buf)]], np.uint32)
-    iq = oracle.dds(desc, summary, ev, amp, env_buf, freq_buf, n_samples, 16)
+    iq = oracle.dds(desc, summary, ev, env_buf, freq_buf, n_samples, 16)
     I, Q = split_iq(iq[0])
     got = I.astype(float) + 1j * Q.astype(float)
     want = np.array([float_model(j, spc, interp, 7, 2, env_buf, 0, L, int(freq_buf[16]), 12345,
@@ -107,9 +105,9 @@ def test_selection_rules():
            dict(t=10, cfg=0, env=sq, amp=65535),
            dict(t=11, cfg=0, env=cw, amp=32768),    # overrides the square mid-pulse
            dict(t=20, cfg=0, env=sq, amp=0)]
-    summary, ev, amp = events([evs])
+    summary, ev = events([evs])
     desc = np.array([[0, 0, spc, interp, 0, len(env_buf), 0, len(freq_buf)]], np.uint32)
-    iq = oracle.dds(desc, summary, ev, amp, env_buf, freq_buf, 4 * 24, 16)
+    iq = oracle.dds(desc, summary, ev, env_buf, freq_buf, 4 * 24, 16)
     I, Q = split_iq(iq[0])
     cyc_I = I.reshape(-1, spc)[:, 0]
     cyc_Q = Q.reshape(-1, spc)[:, 0]
@@ -128,11 +126,11 @@ def test_pulse_reset_phase_reference():
     freq_buf = el.get_freq_buffer([10e6])
     cw = el.get_cw_env_word(0)
     base = [dict(t=0, cfg=2, env=cw, amp=65535)]
-    s0, e0, a0 = events([base])
-    s1, e1, a1 = events([base + [dict(t=50, kind=1)]])
+    s0, e0 = events([base])
+    s1, e1 = events([base + [dict(t=50, kind=1)]])
     desc = np.array([[0, 2, spc, 1, 0, len(env_buf), 0, len(freq_buf)]], np.uint32)
-    iq0 = oracle.dds(desc, s0, e0, a0, env_buf, freq_buf, 4 * 80, 16)[0]
-    iq1 = oracle.dds(desc, s1, e1, a1, env_buf, freq_buf, 4 * 80, 16)[0]
+    iq0 = oracle.dds(desc, s0, e0, env_buf, freq_buf, 4 * 80, 16)[0]
+    iq1 = oracle.dds(desc, s1, e1, env_buf, freq_buf, 4 * 80, 16)[0]
     np.testing.assert_array_equal(iq0[:200], iq1[:200])
     np.testing.assert_array_equal(iq1[200:200 + 4 * 30], iq0[:4 * 30])     # phase restarts at t=50
 
@@ -142,11 +140,11 @@ def test_plan_from_workload_and_oracle_timeline():
     ps = ProgramSet(workloads.config1_linear())
     cfg = _abi.make_config(ps.cores_per_shot, n_groups=ps.n_groups, event_cap=8, meas_cap=2)
     out = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, 2, 1,
-                          want=('summary', 'ev_main', 'ev_amp'))
+                          want=('summary', 'events'))
     params = {i: (e['samples_per_clk'], e['interp_ratio']) for i, e in enumerate(workloads.ELEMS)}
     plan = ChannelPlan(ps, cfg, 0, 2, [(1, 0, 0), (1, 0, 1), (1, 0, 2)], params)
-    assert plan.desc[:, 0].tolist() == [ps.cores_per_shot] * 3
-    iq = oracle.dds(plan.desc, out['summary'], out['ev_main'], out['ev_amp'], plan.env, plan.freq,
+    assert plan.desc[:, 0].tolist() == [1] * 3               # core 0 of shot 1: lane 0 * 2 + 1
+    iq = oracle.dds(plan.desc, out['summary'], out['events'], plan.env, plan.freq,
                     4 * 1400 * 4, 8)
     first = []
     for c in range(3):
@@ -154,9 +152,9 @@ def test_plan_from_workload_and_oracle_timeline():
         I, Q = split_iq(iq[c])
         nz = np.nonzero((I != 0) | (Q != 0))[0]
         first.append(int(nz[0]) // spc if len(nz) else None)
-    ev = out['ev_main'][:, ps.cores_per_shot]
-    strobe_t = {int((w[2] >> 24) & 3): int(w[0]) for w in ev[:int(out['summary'][ps.cores_per_shot, 2])]
-                if (w[2] >> 28) == 0}
+    ev = out['events'][:, 1]
+    strobe_t = {int((w[1] >> 24) & 3): int(w[0]) for w in ev[:int(out['summary'][1, 2])]
+                if (w[1] >> 28) == 0}
     # envelopes may open with zero samples (the readout's cosine ramp): the
     # first non-zero output lies in the strobe's first few cycles
     for c in range(3):

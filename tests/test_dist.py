@@ -82,11 +82,11 @@ def test_shard_range_partitions():
 
 
 def test_sample_lanes_whole_shots():
-    lanes = sharding.sample_lanes(100, 8, 5)
+    lanes = sharding.sample_lanes(100, 8, 5)          # core-major lanes: L = core * 100 + shot
     assert len(lanes) == 40
-    shots = lanes.reshape(5, 8) // 8
+    shots = lanes.reshape(5, 8) % 100
     assert (shots == shots[:, :1]).all() and len(set(shots[:, 0])) == 5
-    assert (lanes.reshape(5, 8) % 8 == np.arange(8)).all()
+    assert (lanes.reshape(5, 8) // 100 == np.arange(8)).all()
     assert len(sharding.sample_lanes(0, 8, 5)) == 0
 
 
@@ -114,6 +114,7 @@ def test_two_rank_gloo_matches_unsharded(tmp_path):
     assert gathered.shape == (world, N_SAMPLE * 8, 8)
     for r in range(world):
         begin, n = sharding.shard_range(N_TOTAL, r, world)
-        lanes = begin * 8 + sharding.sample_lanes(n, 8, N_SAMPLE)
+        loc = sharding.sample_lanes(n, 8, N_SAMPLE)
+        lanes = (loc // n) * N_TOTAL + begin + loc % n          # the same (shot, core) in the unsharded run
         np.testing.assert_array_equal(gathered[r], full['summary'][lanes].astype(np.int64))
     assert float(np.load(tmp_path / 'slowest.npy')[0]) == float(world)

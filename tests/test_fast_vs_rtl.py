@@ -47,11 +47,10 @@ def compare(cfg, fast, rtl, n_shots):
     stats = {'done': 0, 'other': 0, 'events': 0}
     for s in range(n_shots):
         for c in range(C):
-            L = s * C + c
+            L = c * n_shots + s                     # core-major lanes
             r = rtl[s][c]
             ne = min(int(summ['n_events'][L]), EV_CAP)
-            fev = fast['ev_main'][:ne, L]
-            famp = fast['ev_amp'][:ne, L]
+            fev = fast['events'][:ne, L]
             nt = min(int(summ['n_trace'][L]), TR_CAP)
             ftr = fast['trace'][:nt, L]
             nm = min(int(summ['n_meas'][L]), MEAS_CAP)
@@ -66,7 +65,6 @@ def compare(cfg, fast, rtl, n_shots):
                 assert summ['n_instr'][L] == r['n_instr'], ctx
                 assert summ['n_events'][L] == r['n_events'], ctx
                 np.testing.assert_array_equal(fev, r['events'], err_msg=ctx)
-                np.testing.assert_array_equal(famp, r['amp'], err_msg=ctx)
                 assert summ['n_trace'][L] == r['n_trace'], ctx
                 np.testing.assert_array_equal(ftr, r['trace'], err_msg=ctx)
                 assert summ['n_meas'][L] == r['n_meas'], ctx

@@ -2,7 +2,9 @@
 
 The event timelines come from the GPU interpreter (itself bit-exact against
 oracle_fast, tests/test_gpu_parity.py); both DDS implementations consume the
-same device-resident events, copied to the host for the oracle.
+same device-resident events, copied to the host for the oracle.  The library
+ships one synthesis path (dds_index_kernel + dds_tile_kernel with its quad
+sweep and generic per-sample sweep), so these tests cover exactly what ships.
 """
 
 import numpy as np
@@ -27,39 +29,6 @@ def emu():
     e.close()
 
 
-def make_emu(rows, seg=1, index=1, yform=1, spt=4):
-    """an Emulator whose DDS uses the segment kernel for eligible channels
-    (seg=1) or the chunk kernel for all (seg=0), with `rows` quad rows per
-    thread in the chunk kernel (0 = eight contiguous samples), fed by the
-    per-channel event index (index=1, the default) or compacting events in
-    every workgroup (index=0), the chunk kernel's quad sweep in Y form
-    (yform=1, the default; rows apply to the X/Y form only); the knobs are
-    read once, at dpemu_create"""
-    import os
-    knobs = {'DPEMU_DDS_ROWS': str(rows), 'DPEMU_DDS_SEG': str(seg), 'DPEMU_DDS_INDEX': str(index),
-             'DPEMU_DDS_YFORM': str(yform), 'DPEMU_DDS_SPT': str(spt)}
-    old = {k: os.environ.get(k) for k in knobs}
-    os.environ.update(knobs)
-    try:
-        return Emulator(0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
-@pytest.fixture(scope='module', params=[(0, 0, 1, 1, 4), (0, 0, 1, 1, 8), (0, 1, 1, 1, 4), (0, 0, 1, 0, 4),
-                                        (2, 0, 1, 0, 4), (0, 1, 0, 1, 4), (0, 0, 0, 1, 4)],
-                ids=lambda r: ('seg' if r[1] else 'chunk_rows{}'.format(r[0])) + ('' if r[2] else '_noindex')
-                + ('' if r[3] or r[1] else '_xy') + ('_spt8' if r[4] == 8 else ''))
-def emu_path(request):
-    e = make_emu(*request.param)
-    yield e
-    e.close()
-
-
 def host(t):
     return t.cpu().numpy()
 
@@ -78,13 +47,13 @@ def check_equal(gpu_iq, ref_iq, ctx=''):
 def run_and_synthesize(emu, ps, cfg, n_shots, channels, n_samples, shot0=0):
     import torch
     emu.load(ps)
-    out = alloc_device_outputs(cfg, n_shots, want=('summary', 'ev_main', 'ev_amp'))
+    out = alloc_device_outputs(cfg, n_shots, want=('summary', 'events'))
     emu.run_device(cfg, n_shots, shot0, out)
     plan = ChannelPlan(ps, cfg, shot0, n_shots, channels, ELEM_PARAMS)
     iq = emu.synthesize(plan, out, n_samples)
     torch.cuda.synchronize()
-    ref = oracle.dds(plan.desc, host(out['summary']), host(out['ev_main']), host(out['ev_amp']),
-                     plan.env, plan.freq, n_samples, cfg.event_cap)
+    ref = oracle.dds(plan.desc, host(out['summary']), host(out['events']), plan.env, plan.freq, n_samples,
+                     cfg.event_cap)
     return host(iq), ref
 
 
@@ -127,7 +96,6 @@ def test_synthetic_edges_multi_chunk(emu):
     cap, n_lanes = 40, 5
     summary = np.zeros((n_lanes, 8), np.uint32)
     ev = np.zeros((cap, n_lanes, 4), np.uint32)
-    amp = np.zeros((cap, n_lanes), np.uint16)
     env_tab = pack_iq16(np.exp(1j * rng.uniform(0, 2 * np.pi, 4 * 64)) * rng.uniform(0, 1, 4 * 64))
     freq_tab = np.concatenate([DDSElementConfig(samples_per_clk=s).get_freq_buffer([f])
                                for s, f in ((16, 91.7e6), (3, -13.1e6), (5, 250e6), (1, 0.0))])
@@ -140,23 +108,21 @@ def test_synthetic_edges_multi_chunk(emu):
         envw = (A | (Ln << 12)).astype(np.uint32)
         cfgw = rng.integers(0, 4, n).astype(np.uint32)
         ev[:n, L, 0] = t
-        ev[:n, L, 1] = t
-        ev[:n, L, 2] = envw | (cfgw << 24) | (kind << 28)
-        ev[:n, L, 3] = rng.integers(0, 1 << 17, n).astype(np.uint32) | (rng.integers(0, 5, n).astype(np.uint32) << 17)
-        amp[:n, L] = rng.integers(0, 65536, n)
+        ev[:n, L, 1] = envw | (cfgw << 24) | (kind << 28)
+        ev[:n, L, 2] = rng.integers(0, 1 << 17, n).astype(np.uint32) | (rng.integers(0, 5, n).astype(np.uint32) << 17)
+        ev[:n, L, 3] = rng.integers(0, 65536, n)
         summary[L, 2] = n + (5 if L == 2 else 0)    # lane 2 overflowed: count > cap
-    ev[cap - 10, 3, :2] = 10 ** 9                   # lane 3's last event is beyond the window
+    ev[cap - 10:, 3, 0] = 10 ** 9                   # lane 3's last events are beyond the window
     desc = []
     for L in range(n_lanes):
         for e, (spc, interp) in enumerate(((16, 1), (3, 3), (5, 2), (1, 1))):
             desc.append((L, e, spc, interp, 0, len(env_tab), 0, len(freq_tab) if L != 4 else 20))
     desc = np.array(desc, np.uint32)
     n_samples = 2 * 65536 + 4 * 37
-    ref = oracle.dds(desc, summary, ev, amp, env_tab, freq_tab, n_samples, cap)
+    ref = oracle.dds(desc, summary, ev, env_tab, freq_tab, n_samples, cap)
 
     dev = {'summary': torch.from_numpy(summary.view(np.int32)).cuda(),
-           'ev_main': torch.from_numpy(ev.view(np.int32)).cuda(),
-           'ev_amp': torch.from_numpy(amp.view(np.int16)).cuda()}
+           'events': torch.from_numpy(ev.view(np.int32)).cuda()}
     plan = ChannelPlan.__new__(ChannelPlan)
     plan.desc, plan.env, plan.freq = desc, env_tab, freq_tab
     plan.n_lanes, plan.event_cap, plan._dev = n_lanes, cap, None
@@ -172,7 +138,7 @@ def test_bad_arguments_fail_loudly(emu):
     ps = ProgramSet(workloads.config1_linear())
     cfg = _abi.make_config(ps.cores_per_shot, event_cap=8, meas_cap=2)
     emu.load(ps)
-    out = alloc_device_outputs(cfg, 2, want=('summary', 'ev_main', 'ev_amp'))
+    out = alloc_device_outputs(cfg, 2, want=('summary', 'events'))
     emu.run_device(cfg, 2, 0, out)
     plan = ChannelPlan(ps, cfg, 0, 2, [(0, 0, 0)], ELEM_PARAMS)
     with pytest.raises(DpemuError):
@@ -189,7 +155,6 @@ def synthetic_timelines(rng, n_lanes, cap, n_cycles, env_len, n_freq):
     overflowed lane and an empty lane"""
     summary = np.zeros((n_lanes, 8), np.uint32)
     ev = np.zeros((cap, n_lanes, 4), np.uint32)
-    amp = np.zeros((cap, n_lanes), np.uint16)
     for L in range(1, n_lanes):                     # lane 0 stays empty
         n = cap if L == 2 else cap - 2 * L
         t = np.sort(rng.integers(0, n_cycles, n)).astype(np.uint32)
@@ -200,13 +165,12 @@ def synthetic_timelines(rng, n_lanes, cap, n_cycles, env_len, n_freq):
         envw = (A | (Ln << 12)).astype(np.uint32)
         cfgw = rng.integers(0, 4, n).astype(np.uint32)
         ev[:n, L, 0] = t
-        ev[:n, L, 1] = t
-        ev[:n, L, 2] = envw | (cfgw << 24) | (kind << 28)
-        ev[:n, L, 3] = (rng.integers(0, 1 << 17, n).astype(np.uint32)
+        ev[:n, L, 1] = envw | (cfgw << 24) | (kind << 28)
+        ev[:n, L, 2] = (rng.integers(0, 1 << 17, n).astype(np.uint32)
                         | (rng.integers(0, n_freq + 1, n).astype(np.uint32) << 17))   # n_freq: no entry
-        amp[:n, L] = rng.integers(0, 65536, n)
+        ev[:n, L, 3] = rng.integers(0, 65536, n)
         summary[L, 2] = n + (7 if L == 2 else 0)    # lane 2 overflowed: count > cap
-    return summary, ev, amp
+    return summary, ev
 
 
 def plan_from(desc, env_tab, freq_tab, n_lanes, cap):
@@ -228,13 +192,13 @@ SWEEP_CASES = {   # (samples per clock, interp) of the four elements
 
 
 @pytest.mark.parametrize('case', list(SWEEP_CASES))
-def test_sweep_edges(emu_path, case):
-    """every pulse rule against oracle_dds on every sweep variant: CW, pulse
-    end inside a thread's samples (odd env lengths), non-power-of-two interp
+def test_sweep_edges(emu, case):
+    """every pulse rule against oracle_dds on both sweeps: CW, pulse end
+    inside a thread's samples (odd env lengths), non-power-of-two interp
     (generic sweep), resets inside pulses, odd env / freq offsets, missing
     freq entries, env words past the table, ragged tail, overflowed and empty
-    lanes; 'bad_words' puts Q = -32768 into env and rotation words (the
-    segment kernel's per-sample fallback)"""
+    lanes; 'bad_words' puts Q = -32768 into env and rotation words (no Y
+    form: the workgroup takes the generic sweep)"""
     import torch
     rng = np.random.default_rng(11)
     cap, n_lanes, n_cycles = 48, 6, 9000
@@ -244,7 +208,7 @@ def test_sweep_edges(emu_path, case):
     if case == 'bad_words':
         env_tab[::37] = (env_tab[::37] & 0xFFFF0000) | 0x8000
         freq_tab[3 + 16 + 5] = (freq_tab[3 + 16 + 5] & 0xFFFF0000) | 0x8000
-    summary, ev, amp = synthetic_timelines(rng, n_lanes, cap, n_cycles, 280, 3)
+    summary, ev = synthetic_timelines(rng, n_lanes, cap, n_cycles, 280, 3)
     desc = []
     for L in range(n_lanes):
         for e, (spc, interp) in enumerate(SWEEP_CASES[case]):
@@ -253,31 +217,30 @@ def test_sweep_edges(emu_path, case):
             desc.append((L, e, spc, interp, env_off, env_len, 3 if e % 2 else 1, len(freq_tab) - 3))
     desc = np.array(desc, np.uint32)
     n_samples = 16 * n_cycles + 4 * 37                   # ragged last tile
-    ref = oracle.dds(desc, summary, ev, amp, env_tab, freq_tab, n_samples, cap)
+    ref = oracle.dds(desc, summary, ev, env_tab, freq_tab, n_samples, cap)
     dev = {'summary': torch.from_numpy(summary.view(np.int32)).cuda(),
-           'ev_main': torch.from_numpy(ev.view(np.int32)).cuda(),
-           'ev_amp': torch.from_numpy(amp.view(np.int16)).cuda()}
-    iq = emu_path.synthesize(plan_from(desc, env_tab, freq_tab, n_lanes, cap), dev, n_samples)
+           'events': torch.from_numpy(ev.view(np.int32)).cuda()}
+    iq = emu.synthesize(plan_from(desc, env_tab, freq_tab, n_lanes, cap), dev, n_samples)
     torch.cuda.synchronize()
     check_equal(host(iq), ref, 'sweep edges ' + case)
     assert (ref != 0).sum() > 10000
 
 
-def test_paths_agree_on_config5_slice(emu_path):
+def test_config5_slice(emu):
     """the bench's config-5 shape (RB timelines, qdrv + rdrv at 16 samples/clk)
     on a few sequences, full length, against oracle_dds"""
     ps = ProgramSet(workloads.config4_rb(n_seq=4, depth=200, n_cores=8))
     cfg = _abi.make_config(8, n_groups=ps.n_groups, event_cap=512, meas_cap=4)
     ch = [(q, c, e) for q in range(4) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
     import torch
-    emu_path.load(ps)
-    out = alloc_device_outputs(cfg, 4, want=('summary', 'ev_main', 'ev_amp'))
-    emu_path.run_device(cfg, 4, 0, out)
+    emu.load(ps)
+    out = alloc_device_outputs(cfg, 4, want=('summary', 'events'))
+    emu.run_device(cfg, 4, 0, out)
     torch.cuda.synchronize()
     n_samples = ((int(out['summary'][:, 0].max().item()) + 8) * 16 + 3) // 4 * 4
     plan = ChannelPlan(ps, cfg, 0, 4, ch, ELEM_PARAMS)
-    iq = emu_path.synthesize(plan, out, n_samples)
+    iq = emu.synthesize(plan, out, n_samples)
     torch.cuda.synchronize()
-    ref = oracle.dds(plan.desc, host(out['summary']), host(out['ev_main']), host(out['ev_amp']),
-                     plan.env, plan.freq, n_samples, cfg.event_cap, threads=8)
+    ref = oracle.dds(plan.desc, host(out['summary']), host(out['events']), plan.env, plan.freq, n_samples,
+                     cfg.event_cap, threads=8)
     check_equal(host(iq), ref, 'config5 slice')

@@ -19,7 +19,7 @@ from tests.progfuzz import pack_programs, random_case, shaped_case
 
 pytestmark = pytest.mark.gpu
 
-ALL_OUT = ('summary', 'ev_main', 'ev_amp', 'trace', 'meas', 'regs', 'hist')
+ALL_OUT = ('summary', 'events', 'trace', 'meas', 'regs', 'hist')
 
 
 @pytest.fixture(scope='module')
@@ -42,14 +42,14 @@ def compare_all(gpu, ref, ctx=''):
 
 def run_pair(emu, ps, cfg, n_shots, shot0=0):
     """GPU run and oracle; the execution variants (LDS-staged programs,
-    group-major thread order, histogram strategy, program-major fetch, the
-    general interpreter for pulse-only programs) must produce the same bytes"""
+    histogram strategy, program-major fetch, the general interpreter for
+    branch-free programs) must produce the same bytes"""
     emu.load(ps)
     g = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
     f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n_shots, want=ALL_OUT)
     base = cfg.exec_flags
-    for flags in (_abi.X_PROG_LDS | _abi.X_GROUP_MAJOR | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT | _abi.X_PROG_MAJOR,
-                  _abi.X_GENERAL):
+    for flags in (_abi.X_PROG_LDS | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT | _abi.X_PROG_MAJOR,
+                  _abi.X_GENERAL | _abi.X_PROG_LDS):
         cfg.exec_flags = flags
         g2 = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
         compare_all(g2.arrays, g.arrays, 'execution variant {:#x}'.format(flags))
@@ -68,7 +68,7 @@ def test_fuzz_gpu_vs_fast(emu, seed):
                            meas_cap=16, fproc_mode=mode, meas_latency=1 + seed % 23,
                            sync_latency=1 + seed % 3, sync_mask=(0b0111 if seed % 5 == 0 and C == 4 else 0),
                            seed=seed)
-    n_shots = 333 if seed % 2 else 100 * ps.n_groups     # odd: natural order; even: group-major
+    n_shots = 333 if seed % 2 else 100 * ps.n_groups
     g, f = run_pair(emu, ps, cfg, n_shots, shot0=seed * 1000)
     compare_all(g, f, 'seed {}'.format(seed))
 
@@ -156,9 +156,9 @@ def test_config1_golden_program(emu, golden_dir):
     s = _abi.unpack_summary(g['summary'])
     assert (s['status'] == _abi.ST_DONE).all()
     assert (s['n_events'] == 4).all()            # pulse_reset + 3 strobes
-    ev = g['ev_main'][:, 0]
-    assert [int(e[0]) for e in ev[:4]] == [0, 8, 24, 324]     # reset @0; cstrobe at cmd_time + 3 (qclk = t - 1)
-    assert [int(e[1]) for e in ev[1:4]] == [7, 23, 323]       # qclk at cstrobe = cmd_time + 2
+    ev = g['events'][:, 0]
+    assert [int(e[0]) for e in ev[:4]] == [0, 8, 24, 324]     # reset @0; cstrobe at cmd_time + 3 = qclk T + 2
+    assert [int(e[1]) >> 28 for e in ev[:4]] == [1, 0, 0, 0]  # pulse_reset, then three strobes
 
 
 @pytest.mark.parametrize('name', ['test_fproc_hold', 'test_hw_virtualz_out', 'test_linear_compile_out',
@@ -175,7 +175,7 @@ def test_clean_room_assembled_goldens(emu, name):
                            p1=0.5, seed=len(name))
     g, f = run_pair(emu, ps, cfg, 3000, shot0=11)
     compare_all(g, f, name)
-    st = _abi.unpack_summary(g['summary'])['status'].reshape(-1, ps.cores_per_shot)
+    st = _abi.by_shot(_abi.unpack_summary(g['summary'])['status'], ps.cores_per_shot).T     # [shot, core]
     # two goldens never finish by construction: in test_multirst_cfg core Q1
     # waits (jump_fproc func_id 0) on a measurement it never makes; in
     # test_simple_loop the loop register is never incremented
@@ -276,9 +276,10 @@ def test_ramsey_full_size_sharding_invariant(emu):
     assert int(full.arrays['hist'].sum()) == N
     assert (full.summary['status'] == _abi.ST_DONE).all()
     half = [emu.run(N // 2, s, cfg=cfg, outputs=('summary', 'hist')) for s in (0, N // 2)]
-    assert np.array_equal(np.concatenate([h.arrays['summary'] for h in half]), full.arrays['summary'])
+    joined = np.concatenate([_abi.by_shot(h.arrays['summary'], 8) for h in half], axis=1)   # [core, shot, 8]
+    assert np.array_equal(joined, _abi.by_shot(full.arrays['summary'], 8))
     assert np.array_equal(half[0].arrays['hist'] + half[1].arrays['hist'], full.arrays['hist'])
-    t_end = full.summary['t_end'].reshape(N, 8)
+    t_end = _abi.by_shot(full.summary['t_end'], 8).T                                       # [shot, core]
     grp = np.arange(N) % 100
     for k in (0, 37, 99):
         rows = t_end[grp == k]

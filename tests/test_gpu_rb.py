@@ -1,0 +1,116 @@
+"""Config 4 at its stated size on the GPU (BASELINE.json configs[3]):
+10^5 distinct 2-core randomized-benchmarking sequences of depth 200 (about
+1.5 * 10^8 commands, a 2.4 GB device-resident program image), 10 shots per
+sequence = 10^6 shots = 2 * 10^6 (shot, core) lanes in one launch.
+
+* bit-exact: 2,000 shots in 50 windows spread over the whole program table,
+  compared with oracle_fast on every output array -- lanes of the full-size
+  launch (summaries, events, amplitudes, measurements, final registers) and
+  the same windows run as small launches with register traces;
+* full-size properties: every lane DONE, histogram total and per-sequence
+  counts, sharding invariance (two half-size launches = the full launch).
+
+Programs are longer than hdl/proc.sv:12's 256-deep cmd_mem, within
+sim_modules/toplevel_sim.sv:5's 2^16 (SURVEY.md §7 hard part 6).
+"""
+
+import numpy as np
+import pytest
+
+import oracle
+from distributed_processor_amd import _abi, isa, workloads
+from distributed_processor_amd.emulator import Emulator, alloc_device_outputs
+
+pytestmark = pytest.mark.gpu
+
+N_SEQ, DEPTH, SPG = 100000, 200, 10
+N_SHOTS = N_SEQ * SPG
+WINDOWS, WIN = 50, 40
+
+
+@pytest.fixture(scope='module')
+def rb():
+    import torch
+    ps = workloads.config4_rb_set(N_SEQ, DEPTH)
+    ops = ps.words[:, 3] >> 28
+    strobes = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
+                              ps.offsets.astype(np.int64))
+    alus = np.add.reduceat((ops == isa.OP_REG_ALU).astype(np.int64), ps.offsets.astype(np.int64))
+    cfg = _abi.make_config(2, n_groups=N_SEQ, shots_per_group=SPG, max_cycles=1 << 20,
+                           event_cap=int(strobes.max()) + 1, trace_cap=int(alus.max()) + 1, meas_cap=2,
+                           meas_latency=64, seed=0xC0FFEE, p1=0.5)
+    emu = Emulator(0)
+    emu.load(ps)
+    out = alloc_device_outputs(cfg, N_SHOTS, want=('summary', 'events', 'meas', 'regs', 'hist'))
+    for t in out.values():
+        t.zero_()                                        # slots past a lane's count stay 0, as in the oracle's
+    emu.run_device(cfg, N_SHOTS, 0, out)
+    torch.cuda.synchronize()
+    yield emu, ps, cfg, out
+    del out
+    emu.close()
+    torch.cuda.empty_cache()
+
+
+def window_starts():
+    return [int(x) for x in np.linspace(0, N_SHOTS - WIN, WINDOWS).astype(np.int64) + np.arange(WINDOWS) % 7]
+
+
+def test_full_table_windows_bit_exact(rb):
+    import torch
+    emu, ps, cfg, out = rb
+    assert emu.last_kernel()
+    for w0 in window_starts():
+        f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, w0, WIN,
+                            want=('summary', 'events', 'meas', 'regs'))
+        # the window's lanes of the full launch, core-major like the window run's
+        shots = torch.arange(w0, w0 + WIN, device='cuda')
+        lanes = torch.cat([shots, N_SHOTS + shots])
+        got = {'summary': out['summary'][lanes], 'events': out['events'][:, lanes],
+               'meas': out['meas'][:, lanes], 'regs': out['regs'][:, lanes]}
+        for k, v in got.items():
+            a = v.cpu().numpy().view(f[k].dtype)
+            assert np.array_equal(a, f[k]), 'shots [{}, {}) {}'.format(w0, w0 + WIN, k)
+
+
+def test_full_table_windows_with_traces(rb):
+    """the same windows as small launches (the small-grid kernel) with every
+    output, register traces included"""
+    emu, ps, cfg, _ = rb
+    outs = ('summary', 'events', 'trace', 'meas', 'regs', 'hist')
+    for w0 in window_starts()[::5]:
+        g = emu.run(WIN, w0, cfg=cfg, outputs=outs).arrays
+        f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, w0, WIN, want=outs)
+        for k in outs:
+            assert np.array_equal(g[k], f[k]), 'shots [{}, {}) {}'.format(w0, w0 + WIN, k)
+
+
+def test_full_size_properties(rb):
+    import torch
+    emu, ps, cfg, out = rb
+    s = _abi.unpack_summary(out['summary'].cpu().numpy().view(np.uint32))
+    assert (s['status'] == _abi.ST_DONE).all()
+    assert (s['flags'] == 0).all()                       # no late pulse, no overflow
+    assert (s['n_events'] <= cfg.event_cap).all()
+    hist = out['hist'].cpu().numpy()
+    assert hist.sum() == N_SHOTS
+    assert (hist.sum(axis=1) == SPG).all()               # every sequence ran its 10 shots
+    # per lane: the executed instruction count is the program length
+    prog = ps.table.reshape(N_SEQ, 2)[np.arange(N_SHOTS) // SPG]               # [shot, core]
+    assert np.array_equal(_abi.by_shot(s['n_instr'], 2).T, ps.n_instr[prog])
+    # sharding invariance: two half-size launches reproduce the full launch
+    half = N_SHOTS // 2
+    for r in range(2):
+        o = alloc_device_outputs(cfg, half, want=('summary', 'meas', 'hist'))
+        o['meas'].zero_()
+        emu.run_device(cfg, half, r * half, o)
+        torch.cuda.synchronize()
+        for c in range(2):                               # core-major lanes: core c's shots of the half
+            full = slice(c * N_SHOTS + r * half, c * N_SHOTS + (r + 1) * half)
+            part = slice(c * half, (c + 1) * half)
+            assert torch.equal(o['summary'][part], out['summary'][full])
+            assert torch.equal(o['meas'][:, part], out['meas'][:, full])
+        g0 = r * half // SPG
+        assert torch.equal(o['hist'][g0:g0 + half // SPG], out['hist'][g0:g0 + half // SPG])
+        assert int(o['hist'].sum()) == half
+        del o
