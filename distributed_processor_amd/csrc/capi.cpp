@@ -117,6 +117,39 @@ static hipError_t timing_start(dpemu_ctx *ctx, hipStream_t stream, hipEvent_t *s
     return hipEventRecord(e.first, stream);
 }
 
+// Macro image of a branch-free program (macro.hip): from its decoded
+// commands u[0, n) (and the zero = DONE guard past the end), macros of up to
+// two consecutive reg_alu / inc_qclk commands followed by the next other
+// command, until the first terminal command (done / 0000 / hang) -- the
+// program's last macro, which the kernel re-reads once a lane has finished.
+// Per macro 8 u32: {imm0, ctl0, imm1, ctl1} then the pulse slot's decode_cmd
+// word (w bit 31 = no command).  ctl = present[31] inc_qclk[30] rs0[15:12]
+// rd[11:8] rs1[7:4] in0_reg[3] alu_op[2:0].
+static void build_macros(const uint32_t *u, uint32_t n, std::vector<uint32_t> &out)
+{
+    static const uint32_t zero[4] = {0, 0, 0, 0};
+    uint32_t k = 0;
+    for (;;) {
+        uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, MACRO_ABSENT};
+        const uint32_t *c = k < n ? u + 4ull * k : zero;
+        for (int a = 0; a < 2; a++) {
+            const uint32_t op4 = c[1] >> 28;
+            if (op4 != 0x1 && op4 != 0x6) break;
+            m[2 * a] = c[0];
+            m[2 * a + 1] = 0x80000000u | (op4 == 0x6 ? 0x40000000u : 0u) | (c[1] & 0xFFFu) | (((c[3] >> 20) & 15u) << 12);
+            k++;
+            c = k < n ? u + 4ull * k : zero;
+        }
+        const uint32_t op4 = c[1] >> 28;
+        if (op4 != 0x1 && op4 != 0x6) {        // the slot's command (else: a third ALU command opens the next macro)
+            memcpy(m + 4, c, 16);
+            k++;
+        }
+        out.insert(out.end(), m, m + 8);
+        if (op4 == 0x0 || op4 == 0xA || op4 >= 0xD) return;
+    }
+}
+
 static void free_programs(dpemu_ctx *ctx)
 {
     for (void *q : {(void *)ctx->d_uops, (void *)ctx->d_uops_t, (void *)ctx->d_macro, (void *)ctx->d_moff,
@@ -259,6 +292,21 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words,
         HIPCHK(ctx, hipMalloc(&ctx->d_uops_t, t_cmds * 16));
         HIPCHK(ctx, hipMemcpy(ctx->d_uops_t, ut.data(), t_cmds * 16, hipMemcpyHostToDevice));
     }
+    // ... and the macro image of branch-free programs with register commands
+    if (linear && !straight && max_len < 65536u) {
+        std::vector<uint32_t> mac, moff(n_programs + 1);
+        mac.reserve(tot * 4 + 8ull * n_programs);
+        for (uint32_t pr = 0; pr < n_programs; pr++) {
+            moff[pr] = (uint32_t)(mac.size() / 8);
+            build_macros(&uops[4ull * goff[pr]], n_instr[pr], mac);
+            if (mac.size() / 8 >= (1ull << 32)) return fail(ctx, DPEMU_E_INVALID, "macro image exceeds 2^32 macros");
+        }
+        moff[n_programs] = (uint32_t)(mac.size() / 8);
+        HIPCHK(ctx, hipMalloc(&ctx->d_macro, mac.size() * 4));
+        HIPCHK(ctx, hipMemcpy(ctx->d_macro, mac.data(), mac.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMalloc(&ctx->d_moff, moff.size() * 4));
+        HIPCHK(ctx, hipMemcpy(ctx->d_moff, moff.data(), moff.size() * 4, hipMemcpyHostToDevice));
+    }
     HIPCHK(ctx, hipMemcpy(ctx->d_offsets, goff.data(), n_programs * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->d_ninstr, n_instr, n_programs * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->d_table, prog_table, (uint64_t)n_groups * C * 4, hipMemcpyHostToDevice));
@@ -334,6 +382,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.fetch_stride = cmd_major ? ctx->n_programs : 1u;
     p.offsets = ctx->d_offsets; p.n_instr = ctx->d_ninstr; p.prog_table = ctx->d_table;
     p.max_len = ctx->max_len;
+    p.macros = ctx->d_macro; p.macro_off = ctx->d_moff;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
     p.summary = out->summary;
     p.events = reinterpret_cast<uint4 *>(out->events);
@@ -403,6 +452,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     const bool small = blocks <= 4 * 256;
     const int fetch_batch = small ? 4 : 1;
     const bool uniform = ctx->straight && ctx->max_len < 65536u && !(cfg->exec_flags & DPEMU_X_GENERAL);
+    const bool macro = !uniform && ctx->d_macro && !(cfg->exec_flags & DPEMU_X_GENERAL);
     int src = cmd_major ? STRAIGHT_ROWS : STRAIGHT_PROG;
     if (uniform) {
         const uint64_t per_cu = std::min<uint64_t>(8, std::max<uint64_t>(1, (blocks + 255) / 256));
@@ -459,6 +509,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
+    else if (macro) HIPCHK(ctx, launch_macro(p, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, stream));
     {
@@ -466,6 +517,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
         if (uniform)
             snprintf(name, sizeof name, "straight_kernel<%s,fb%d>",
                      src == STRAIGHT_ROWS ? "rows" : src == STRAIGHT_PROG ? "prog" : "lds", fetch_batch);
+        else if (macro)
+            snprintf(name, sizeof name, "macro_kernel");
         else
             snprintf(name, sizeof name, "interp_kernel<feat=0x%x>", feat);
         ctx->last_kernel = name;

@@ -104,6 +104,8 @@ struct KParams {
                                   //   fetch adjacent commands
     const uint32_t *offsets, *n_instr, *prog_table;   // uops: a zero guard command follows every program
     uint32_t max_len;             // longest program; the command-major image's guard row
+    const uint4 *macros;          // macro.hip image: 2 x uint4 per macro (capi.cpp build_macros)
+    const uint32_t *macro_off;    // [n_programs + 1]: program p's macros [macro_off[p], macro_off[p + 1])
     const uint32_t *p1_thr;
     const uint64_t *lut_table;
     // outputs (device, nullable); lane L = core * n_shots + shot (core-major)
@@ -141,6 +143,9 @@ hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
 enum { STRAIGHT_ROWS = 0, STRAIGHT_PROG = 1, STRAIGHT_LDS = 2 };
 constexpr uint32_t STRAIGHT_LDS_MAX = 9216;   // commands (144 KiB) of dynamic LDS per workgroup
 hipError_t launch_straight(const KParams &p, int src, int fb, hipStream_t stream);
+// branch-free programs with reg_alu / inc_qclk (macro.hip)
+hipError_t launch_macro(const KParams &p, hipStream_t stream);
+constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no command; ALU ctl bit 31: present
 
 // ---- DDS ------------------------------------------------------------------
 // Two launches per synthesis (dds.hip): dds_index_kernel compacts each
