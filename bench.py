@@ -1,31 +1,39 @@
 """Benchmark: batched emulation of assembled distproc machine code on MI355X.
 
-Workload (BASELINE.json configs[1]): 8-core (8-qubit) parallel Ramsey sweep,
-100 delay points selected by shot, no branching, 10^6 shots per GPU.  One
-step = one pass of the hot path over one batch: the interpreter kernel
-emulates every (shot, core) lane cycle-exactly and writes the full pulse-event
-timeline, lane summaries, measurement records and the outcome histogram to
-HBM; with N > 1 ranks the histograms are all-reduced over RCCL (the path's
-only exchange).  Shots shard by global index (weak scaling).
+One JSON line on rank 0.  The headline (BASELINE.json configs[1]) is config 2:
+8-core (8-qubit) parallel Ramsey sweep, 100 delay points selected by shot, no
+branching, 10^6 shots per GPU.  One step = one pass of the hot path over one
+batch: the interpreter emulates every (shot, core) lane cycle-exactly and
+writes the full pulse-event timeline, lane summaries, measurement records and
+the outcome histogram to HBM; with N > 1 ranks the histograms are all-reduced
+over RCCL (the path's only exchange), overlapped with the next
+batch (sharding.HistogramPipeline).  Shots shard by global index (weak
+scaling).  After the timed steps a fixed sample of lane timelines is gathered
+to every rank (sharding.gather_sample).
 
-Active-reset leg (config 3, under "active_reset"): fproc_meas branching and
-sync barriers on the general interpreter kernel, 1.25*10^6 shots per GPU.
+Sub-objects on the same line, each with its own roofline and CPU baselines:
+  "dds"           config 5: RB timelines (8 cores, depth 200) synthesised to
+                  int16 I/Q on 16 channels per sequence at 16 samples/clk
+  "active_reset"  config 3: fproc_meas branching + sync barriers, 1.25*10^6
+                  shots per GPU (10^7 over 8 GPUs)
+  "rb"            config 4 at its stated size: 10^5 distinct 2-core depth-200
+                  RB sequences x 10 shots per GPU
 
-DDS leg (config 5, reported under "dds" on the same line): the config-4 RB
-timelines (8 cores, depth 200) synthesised to int16 I/Q on 16 channels per
-sequence at 16 samples/clk; GSamples/s (whole job) and the DDS kernel's HBM
-write roofline.
-
-Metric: emulated core-shots/s (whole job).  Also reported: emulated qclk
-cycles/s and instructions/s, the interpreter's HBM roofline fraction, and
-the CPU baseline (oracle_fast, the event-driven C restatement, on the host
-cores; the Verilator/cocotb testbench itself cannot run here or on the box).
+CPU baselines (rank 0, one GPU): the reference's Verilator/cocotb testbench
+cannot run here or on the box, so each leg reports
+oracle_fast (the event-driven C restatement, OpenMP over shots, every core
+this process may use) as `cpu_baseline.value`, and oracle_rtl (the per-clock
+restatement: one evaluation per clock like Verilator) at 1 thread and at all
+cores beside it; each a median of 5 timed runs of a fixed sample after one
+warm-up run.
 
     python bench.py --gpus 1 --steps 20 --warmup 3
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 
 import argparse
+import csv
+import glob
 import json
 import os
 import sys
@@ -36,30 +44,102 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-PROFILE_TAG = 'r01'            # profiles/<tag>_{interp,dds}_pmc.json: PMC passes of this workload
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s
+VALU_PEAK = 7.7e11             # wave64 integer-VALU instructions/s, measured (profiles/r01_valu_peak.jsonl)
+PROFILE_TAG = 'r02'            # profiles/<tag>_*: rocprofv3 kernel stats and PMC passes of this bench
 
 
-def build_workload(n_points=100, n_cores=8):
-    from distributed_processor_amd import workloads
-    from distributed_processor_amd.emulator import ProgramSet
-    return ProgramSet(workloads.config2_ramsey(n_cores=n_cores, n_points=n_points))
+# ---------------------------------------------------------------------------- helpers
+def host_cores():
+    """threads for the CPU baselines: every core this process may run on
+    (sched_getaffinity), within the job's CPU share when the harness sets one
+    (OMP_NUM_THREADS); both recorded"""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get('OMP_NUM_THREADS')
+    use = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return use, {'nproc': aff, 'os_cpu_count': os.cpu_count(), 'omp_num_threads': omp}
 
 
-def kernel_pass(emu, steps, step, drain=None):
-    """Run `steps` more steps with the library's HIP events recorded around
-    each main kernel launch (dpemu_set_kernel_timing), outside the timed
-    region; emu.kernel_times() then holds one duration per launch."""
-    import torch
-    torch.cuda.synchronize()
-    emu.kernel_times()                                # drop earlier records
-    emu.kernel_timing(True)
-    for _ in range(steps):
-        step()
-    if drain is not None:
-        drain()
-    torch.cuda.synchronize()
-    emu.kernel_timing(False)
+def median_rate(run, units_per_n, n0, target_s=0.8, reps=5):
+    """one warm-up / calibration run of n0, then `reps` timed runs of a fixed
+    n sized to ~target_s each; returns (median units/s, n, [seconds])"""
+    t = time.perf_counter()
+    run(n0)
+    dt = max(time.perf_counter() - t, 1e-4)
+    n = max(1, int(n0 * target_s / dt))
+    times = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        run(n)
+        times.append(time.perf_counter() - t)
+    return n * units_per_n / float(np.median(times)), n, times
+
+
+def cpu_baselines(ps, cfg, horizon, what):
+    """oracle_fast (all cores) and oracle_rtl (1 thread, all cores) on the leg's workload"""
+    import oracle
+    threads, info = host_cores()
+    C = cfg.cores_per_shot
+    want = ('summary', 'events', 'meas', 'hist')
+    fast = lambda k: lambda n: oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n, k, want)
+    rtl = lambda k: lambda n: oracle.rtl_run_batch(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n, horizon, k)
+    f_rate, f_n, f_t = median_rate(fast(threads), C, 2000)
+    r1_rate, r1_n, r1_t = median_rate(rtl(1), C, 20)
+    ra_rate, ra_n, ra_t = median_rate(rtl(threads), C, 20 * threads)
+    return dict(value=f_rate, unit='core-shots/s', cores=threads, kind='port', **info,
+                method='median of 5 timed runs of a fixed sample after one warm-up run',
+                sample='{}: {} shots x {} cores per oracle_fast run (event-driven C restatement, OpenMP over '
+                       'shots, {} threads)'.format(what, f_n, C, threads),
+                oracle_fast={'value': f_rate, 'threads': threads, 'shots_per_run': f_n,
+                             'run_s': [round(x, 4) for x in f_t]},
+                oracle_rtl={'value_1_thread': r1_rate, 'value_all_cores': ra_rate, 'threads': threads,
+                            'shots_per_run': [r1_n, ra_n],
+                            'note': 'per-clock restatement of hdl/ (one evaluation per clock, the closest '
+                                    'stand-in for the Verilator testbench of cocotb/proc/Makefile:1-14, '
+                                    'which cannot run here)'})
+
+
+def pmc(name):
+    """per-launch PMC summary of a kernel from profiles/<tag>_<name>_pmc.json (scripts/pmc_summary.py)"""
+    path = os.path.join(REPO, 'profiles', '{}_{}_pmc.json'.format(PROFILE_TAG, name))
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def rocprof_avg_ms(kernel_substr):
+    """the committed rocprofv3 --stats average of a kernel (profiles/<tag>_*kernel_stats.csv)"""
+    for path in sorted(glob.glob(os.path.join(REPO, 'profiles', PROFILE_TAG + '*kernel_stats.csv'))):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                if kernel_substr in r.get('Name', ''):
+                    return float(r['AverageNs']) * 1e-6
+    return None
+
+
+def valu_view(prof):
+    if not prof:
+        return None
+    return {k: prof.get(k) for k in ('valu_insts_per_wave', 'valu_issue_pct', 'valu_busy_pct',
+                                     'valu_lane_util_pct', 'duration_ns', 'kernel', 'SQ_INSTS_VALU')}
+
+
+def hbm_roofline(alg_bytes, kernel_ms, ms_per_step, kernel, prof, rocprof_key):
+    """HBM roofline of a kernel: algorithmic bytes / kernel time.  The kernel
+    time is the median HIP-event duration of the launches, capped at the
+    step's own time (the event pair cannot make the kernel longer than the
+    whole step); the committed rocprof average gives a second fraction"""
+    k_ms = min(kernel_ms, ms_per_step)
+    gbs = alg_bytes / (k_ms * 1e-3) / 1e9
+    r = {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS,
+         'traffic': prof.get('hbm_bytes_per_launch') if prof else None, 'bytes_per_launch': alg_bytes,
+         'kernel_ms': k_ms, 'kernel_ms_events': kernel_ms, 'kernel': kernel}
+    rp = rocprof_avg_ms(rocprof_key)
+    if rp:
+        r['kernel_ms_rocprof'] = rp
+        r['frac_rocprof'] = alg_bytes / (rp * 1e-3) / 1e9 / HBM_PEAK_GBS
+    return r
 
 
 def bytes_per_lane(summary_np, cfg):
@@ -70,67 +150,125 @@ def bytes_per_lane(summary_np, cfg):
     return 32.0 + 16.0 * n_ev + 8.0 * n_me
 
 
-def cpu_baseline(ps, cfg, target_s=12.0):
-    """oracle_fast on the host cores over a bounded sample of the same workload."""
-    import oracle
-    threads = os.cpu_count() or 1
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except Exception:
-        pass
-    threads = min(threads, 16)
-    chunk = 20000
-    want = ('summary', 'events', 'meas', 'hist')
-    oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, 1000, threads, want)  # warm
-    done = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < target_s:
-        oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, done, chunk, threads, want)
-        done += chunk
-    dt = time.perf_counter() - t0
-    return {'value': done * cfg.cores_per_shot / dt, 'unit': 'core-shots/s', 'cores': threads,
-            'kind': 'port',
-            'sample': '{} shots x {} cores of the same Ramsey workload, oracle_fast (event-driven C '
-                      'restatement, OpenMP) in {}-shot chunks, {:.1f} s'.format(done, cfg.cores_per_shot, chunk, dt)}
-
-
-def dds_workload(n_seq):
-    """config 5: the config-4 RB timelines (8 cores, depth 200) synthesised on
-    16 channels per sequence (8 cores x {qdrv, rdrv}) at 16 samples/clk"""
-    from distributed_processor_amd import workloads
-    from distributed_processor_amd.emulator import ProgramSet
-    return ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
-
-
-def dds_cpu_baseline(plan, host_ev, n_samples, target_s=8.0):
-    """oracle_dds (scalar C restatement, OpenMP over channels) on whole
-    channels of the same timelines until ~target_s of CPU work"""
-    import oracle
-    threads = min(len(os.sched_getaffinity(0)), 16)
-    per = max(threads, 16)
-    done = 0
-    t0 = time.perf_counter()
-    i = 0
-    while time.perf_counter() - t0 < target_s and i < plan.n_channels:
-        d = plan.desc[i:i + per]
-        oracle.dds(d, host_ev['summary'], host_ev['events'], plan.env, plan.freq,
-                   n_samples, plan.event_cap, threads)
-        done += len(d) * n_samples
-        i += per
-    dt = time.perf_counter() - t0
-    return {'value': done / dt / 1e9, 'unit': 'GSamples/s', 'cores': threads, 'kind': 'port',
-            'sample': '{} channels x {} samples of the config-5 timelines, oracle_dds (scalar C '
-                      'restatement, OpenMP over channels), {:.1f} s'.format(done // n_samples, n_samples, dt)}
-
-
-def dds_leg(emu, args, world, rank, stream):
-    """time K synthesis steps of config 5; returns the 'dds' sub-object"""
+def timed(step, drain, steps, warmup, world):
+    """warm-up, then exactly `steps` steps between barrier + synchronize;
+    returns the max over ranks of the wall time"""
     import torch
-    import torch.distributed as dist
+    from distributed_processor_amd import sharding
+    for _ in range(warmup):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    return sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
+
+
+def kernel_pass(emu, steps, step, drain):
+    """`steps` more steps with the library's HIP events around each main
+    kernel launch, outside the timed region; returns their median ms"""
+    import torch
+    torch.cuda.synchronize()
+    emu.kernel_times()
+    emu.kernel_timing(True)
+    for _ in range(steps):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    emu.kernel_timing(False)
+    kt = emu.kernel_times()
+    assert len(kt) == steps, kt
+    return float(np.median(kt))
+
+
+def fill_gbps(device='cuda'):
+    """a torch fill of 1 GiB on this box (HIP events): the store rate the
+    HBM roofline's 8 TB/s compares against, measured (boxes differ)"""
+    import torch
+    buf = torch.empty(1 << 28, dtype=torch.int32, device=device)
+    for _ in range(3):
+        buf.fill_(1)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        buf.fill_(2)
+    b.record()
+    torch.cuda.synchronize()
+    gbs = buf.numel() * 4 * 10 / (a.elapsed_time(b) * 1e-3) / 1e9
+    del buf
+    return gbs
+
+
+# ---------------------------------------------------------------------------- legs
+def leg_ramsey(emu, args, world, rank, stream):
+    """config 2 (the headline line)"""
+    import torch
+    from distributed_processor_amd import _abi, sharding, workloads
+    from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
+    ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
+    emu.load(ps)
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, trace_cap=0, meas_cap=2,
+                           meas_latency=64, seed=0x5EED, p1=0.5)
+    shot0, n = sharding.weak_shard(args.shots, rank)
+    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
+    pipe = sharding.HistogramPipeline(out['hist'])
+
+    def launch(h):
+        out['hist'] = h
+        emu.run_device(cfg, n, shot0, out, stream)
+    step = lambda: pipe.step(launch)
+    dt = timed(step, pipe.drain, args.steps, args.warmup, world)
+    kernel_ms = kernel_pass(emu, args.steps, step, pipe.drain)
+    kernel = emu.last_kernel()
+    # accounting from the last step's outputs (identical every step)
+    summ = out['summary'].cpu().numpy().view(np.uint32)
+    s = _abi.unpack_summary(summ)
+    assert (s['status'] == _abi.ST_DONE).all(), 'not every lane reached DONE'
+    assert int(pipe.result().sum().item()) == n * world
+    # the north star's timeline gather: a fixed sample of lanes (summaries and
+    # their event records) from every rank, after the timed region
+    lanes = torch.from_numpy(sharding.sample_lanes(n, 8, 16)).to('cuda')
+    sample = torch.cat([out['summary'][lanes], out['events'][:, lanes].permute(1, 0, 2).reshape(len(lanes), -1)], 1)
+    gathered = sharding.gather_sample(sample)
+    assert gathered.shape[0] == world and torch.equal(gathered[rank], sample)
+    ms_step = dt / args.steps * 1e3
+    alg = float(bytes_per_lane(summ, cfg).sum())
+    prof = pmc('ramsey')
+    roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'straight_kernel')
+    roof['valu'] = valu_view(prof)
+    res = {'value': n * 8 * world * args.steps / dt, 'ms_per_step': ms_step,
+           'shots_per_s': n * world * args.steps / dt,
+           'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * args.steps / dt,
+           'instructions_per_s': float(s['n_instr'].astype(np.float64).sum()) * world * args.steps / dt,
+           'kernel_ms': kernel_ms, 'roofline': roof,
+           'timeline_gather': {'ranks': int(gathered.shape[0]), 'lanes_per_rank': int(len(lanes)),
+                               'bytes': int(gathered.numel() * gathered.element_size())},
+           'config': {'workload': 'config2_ramsey_8core_100pt', 'shots_per_gpu': n, 'cores_per_shot': 8,
+                      'global_shots_per_step': n * world, 'parallelism': 'shots sharded, {} GPU(s)'.format(world)}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res['cpu_baseline'] = cpu_baselines(ps, cfg, 4096, 'config 2 Ramsey')
+    del out
+    torch.cuda.empty_cache()
+    return res
+
+
+def leg_dds(emu, args, world, rank, stream):
+    """config 5: DDS over the config-4 RB timelines, 8 cores x {qdrv, rdrv}"""
+    import torch
     from distributed_processor_amd import _abi, sharding, workloads
     from distributed_processor_amd.dds import ChannelPlan
-    from distributed_processor_amd.emulator import alloc_device_outputs
-    ps = dds_workload(args.dds_seqs)
+    from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
+    ps = ProgramSet(workloads.config4_rb(n_seq=args.dds_seqs, depth=200, n_cores=8))
     emu.load(ps)
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=512, meas_cap=4,
                            meas_latency=64, seed=0x5EED)
@@ -138,8 +276,7 @@ def dds_leg(emu, args, world, rank, stream):
     ev = alloc_device_outputs(cfg, n, want=('summary', 'events'))
     emu.run_device(cfg, n, shot0, ev, stream)
     torch.cuda.synchronize()
-    summ = ev['summary'].cpu().numpy().view(np.uint32)
-    s = _abi.unpack_summary(summ)
+    s = _abi.unpack_summary(ev['summary'].cpu().numpy().view(np.uint32))
     assert (s['status'] == _abi.ST_DONE).all() and (s['n_events'] <= cfg.event_cap).all()
     n_cyc = int(s['t_end'].max()) + 8
     n_samples = (n_cyc * 16 + 3) // 4 * 4
@@ -147,52 +284,44 @@ def dds_leg(emu, args, world, rank, stream):
     chans = [(shot0 + q, c, e) for q in range(n) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
     plan = ChannelPlan(ps, cfg, shot0, n, chans, params)
     iq = torch.empty((plan.n_channels, n_samples), dtype=torch.int32, device='cuda')
-    for _ in range(args.warmup):
-        emu.synthesize(plan, ev, n_samples, iq, stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        emu.synthesize(plan, ev, n_samples, iq, stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
-    kernel_pass(emu, args.steps, lambda: emu.synthesize(plan, ev, n_samples, iq, stream))
-    kt = emu.kernel_times()
-    assert len(kt) == args.steps, kt
-    kernel_ms = float(np.mean(kt))                    # HIP events around the DDS kernel, same stream
+    step = lambda: emu.synthesize(plan, ev, n_samples, iq, stream)
+    dt = timed(step, lambda: None, args.steps, args.warmup, world)
+    kernel_ms = kernel_pass(emu, args.steps, step, lambda: None)
     samples = plan.n_channels * n_samples
-    gbs = samples * 4 / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(REPO, 'profiles', PROFILE_TAG + '_dds_pmc.json')
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get('hbm_bytes_per_launch')
+    ms_step = dt / args.steps * 1e3
+    prof = pmc('dds')
+    roof = hbm_roofline(samples * 4, kernel_ms, ms_step, 'dpemu::dds_tile_kernel', prof, 'dds_tile_kernel')
     res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
-           'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s',
-           'ms_per_step': dt / args.steps * 1e3, 'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
-           'step': 'dds_index_kernel (per-channel event index) + dds_chunk_kernel; kernel_ms and the roofline '
-                   'hold dds_chunk_kernel alone, value and ms_per_step the whole step',
+           'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s', 'ms_per_step': ms_step,
+           'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
+           'step': 'dds_index_kernel (per-channel event index + tile windows) + dds_tile_kernel; kernel_ms and '
+                   'the roofline hold dds_tile_kernel alone, value and ms_per_step the whole step',
+           'step_roofline_frac': samples * 4 / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
            'config': {'workload': 'config5_dds_rb8', 'sequences_per_gpu': n, 'channels_per_gpu': plan.n_channels,
                       'samples_per_channel': n_samples, 'rb_depth': 200},
-           'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                        'frac': gbs / HBM_PEAK_GBS, 'traffic': traffic, 'bytes_per_launch': samples * 4,
-                        'kernel': 'dpemu::dds_tile_kernel'}}
+           'roofline': roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        threads, info = host_cores()
         host_ev = {k: v.cpu().numpy() for k, v in ev.items()}
-        res['cpu_baseline'] = dds_cpu_baseline(plan, host_ev, n_samples, args.cpu_seconds * 2 / 3)
-    del iq
+
+        def run(k):
+            oracle.dds(plan.desc[:k], host_ev['summary'], host_ev['events'], plan.env, plan.freq, n_samples,
+                       plan.event_cap, threads)
+        rate, k, times = median_rate(run, n_samples, max(threads, 16))
+        res['cpu_baseline'] = dict(value=rate / 1e9, unit='GSamples/s', cores=threads, kind='port', **info,
+                                   method='median of 5 timed runs of a fixed sample after one warm-up run',
+                                   sample='{} channels x {} samples of the config-5 timelines per run, oracle_dds '
+                                          '(C restatement, OpenMP over channels)'.format(k, n_samples))
+    del iq, ev
+    torch.cuda.empty_cache()
     return res
 
 
-def active_reset_leg(emu, args, world, rank, stream):
-    """config 3 (BASELINE configs[2]): 8-core active reset -- readout, fproc_meas
-    branch to a conditional X180, sync barriers -- 10^7 shots per step over 8
-    GPUs, i.e. 1.25*10^6 shots per GPU (weak).  Runs on the general
-    interpreter kernel (fproc + sync).  Returns the 'active_reset' sub-object."""
+def leg_active_reset(emu, args, world, rank, stream):
+    """config 3 (BASELINE configs[2]): 8-core active reset -- readout,
+    fproc_meas branch to a conditional X180, sync barriers -- 10^7 shots per
+    step over 8 GPUs, i.e. 1.25*10^6 shots per GPU (weak)"""
     import torch
     from distributed_processor_amd import _abi, sharding, workloads
     from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
@@ -200,65 +329,107 @@ def active_reset_leg(emu, args, world, rank, stream):
     emu.load(ps)
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
                            meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5)
-    n_per = args.ar_shots
-    out = alloc_device_outputs(cfg, n_per, want=('summary', 'events', 'meas', 'hist'))
-    shot0, n = sharding.weak_shard(n_per, rank)
+    shot0, n = sharding.weak_shard(args.ar_shots, rank)
+    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
+    pipe = sharding.HistogramPipeline(out['hist'])
 
-    def step():
-        out['hist'].zero_()
+    def launch(h):
+        out['hist'] = h
         emu.run_device(cfg, n, shot0, out, stream)
-        sharding.allreduce_histogram(out['hist'])
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
-    kernel_pass(emu, args.steps, step)
-    kt = emu.kernel_times()
-    kernel_ms = float(np.mean(kt))
+    step = lambda: pipe.step(launch)
+    dt = timed(step, pipe.drain, args.steps, args.warmup, world)
+    kernel_ms = kernel_pass(emu, args.steps, step, pipe.drain)
     summ = out['summary'].cpu().numpy().view(np.uint32)
     s = _abi.unpack_summary(summ)
     assert (s['status'] == _abi.ST_DONE).all(), 'config 3: not every lane reached DONE'
-    assert int(out['hist'].sum().item()) == n * world
+    assert int(pipe.result().sum().item()) == n * world
     alg = float(bytes_per_lane(summ, cfg).sum())
-    gbs = alg / (kernel_ms * 1e-3) / 1e9
+    prof = pmc('active_reset')
+    ms_step = dt / args.steps * 1e3
+    roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + emu.last_kernel(), prof, 'interp_kernel')
+    roof['valu'] = valu_view(prof)
     res = {'metric': 'emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
                      '1.25e6 shots/GPU)',
            'value': n * 8 * world * args.steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * args.steps / dt,
-           'ms_per_step': dt / args.steps * 1e3, 'kernel_ms': kernel_ms, 'kernel': 'dpemu::' + emu.last_kernel(),
+           'ms_per_step': ms_step, 'kernel_ms': kernel_ms,
            'instructions_per_s': float(s['n_instr'].astype(np.float64).sum()) * world * args.steps / dt,
-           'config': {'workload': 'config3_active_reset_8core', 'shots_per_gpu': n,
-                      'global_shots_per_step': n * world},
-           'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                        'frac': gbs / HBM_PEAK_GBS, 'bytes_per_launch': alg}}
-    pmc = os.path.join(REPO, 'profiles', PROFILE_TAG + '_active_reset_pmc.json')
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            prof = json.load(f)
-        res['roofline']['traffic'] = prof.get('hbm_bytes_per_launch')
-        res['roofline']['valu'] = {k: prof.get(k) for k in ('valu_insts_per_wave', 'valu_issue_pct',
-                                                            'valu_lane_util_pct', 'duration_ns', 'kernel')}
+           'config': {'workload': 'config3_active_reset_8core', 'shots_per_gpu': n, 'global_shots_per_step': n * world},
+           'roofline': roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle
-        threads = min(len(os.sched_getaffinity(0)), 16)
-        want = ('summary', 'events', 'meas', 'hist')
-        done, chunk, t0 = 0, 20000, time.perf_counter()
-        while time.perf_counter() - t0 < args.cpu_seconds / 3:
-            oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, done, chunk, threads, want)
-            done += chunk
-        dtc = time.perf_counter() - t0
-        res['cpu_baseline'] = {'value': done * 8 / dtc, 'unit': 'core-shots/s', 'cores': threads, 'kind': 'port',
-                               'sample': '{} shots x 8 cores of config 3, oracle_fast (OpenMP), {:.1f} s'.format(
-                                   done, dtc)}
+        res['cpu_baseline'] = cpu_baselines(ps, cfg, 8192, 'config 3 active reset')
     del out
+    torch.cuda.empty_cache()
+    return res
+
+
+def leg_rb(emu, args, world, rank, stream):
+    """config 4 at its stated size: 10^5 distinct 2-core RB sequences of depth
+    200 (1.5*10^8 commands, a 2.4 GB program image), 10 shots each = 10^6
+    shots = 2*10^6 lanes per GPU.  Branch-free programs with register
+    commands: macro_kernel.  Divergent: a wave's lanes run ~7 different
+    programs.  VALU-bound: the roofline is VALU issue against
+    the measured peak, with the VALU ops per emulated instruction and the
+    active lanes per VALU instruction (divergence) from the PMC pass."""
+    import torch
+    from distributed_processor_amd import _abi, isa, sharding, workloads
+    from distributed_processor_amd.emulator import alloc_device_outputs
+    t0 = time.perf_counter()
+    ps = workloads.config4_rb_set(args.rb_seqs, 200)
+    gen_s = time.perf_counter() - t0
+    emu.load(ps)
+    torch.cuda.synchronize()
+    load_s = time.perf_counter() - t0 - gen_s
+    ops = ps.words[:, 3] >> 28
+    strobes = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
+                              ps.offsets.astype(np.int64))
+    cfg = _abi.make_config(2, n_groups=ps.n_groups, shots_per_group=args.rb_spg, max_cycles=1 << 20,
+                           event_cap=int(strobes.max()) + 1, trace_cap=0, meas_cap=2, meas_latency=64,
+                           seed=0x5EED, p1=0.5)
+    shot0, n = sharding.weak_shard(args.rb_seqs * args.rb_spg, rank)
+    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
+    pipe = sharding.HistogramPipeline(out['hist'])
+
+    def launch(h):
+        out['hist'] = h
+        emu.run_device(cfg, n, shot0, out, stream)
+    step = lambda: pipe.step(launch)
+    steps = max(1, args.steps // 4)
+    dt = timed(step, pipe.drain, steps, min(args.warmup, 2), world)
+    kernel_ms = kernel_pass(emu, steps, step, pipe.drain)
+    summ = out['summary'].cpu().numpy().view(np.uint32)
+    s = _abi.unpack_summary(summ)
+    assert (s['status'] == _abi.ST_DONE).all(), 'config 4: not every lane reached DONE'
+    assert int(pipe.result().sum().item()) == n * world
+    instrs = float(s['n_instr'].astype(np.float64).sum())
+    ms_step = dt / steps * 1e3
+    k_ms = min(kernel_ms, ms_step)
+    prof = pmc('rb')
+    alg = float(bytes_per_lane(summ, cfg).sum())
+    hbm = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + emu.last_kernel(), prof, 'macro_kernel')
+    if prof and prof.get('SQ_INSTS_VALU'):
+        valu_per_launch = float(prof['SQ_INSTS_VALU'])
+        achieved = valu_per_launch / (k_ms * 1e-3)
+        roof = {'bound': 'valu', 'achieved': achieved, 'peak': VALU_PEAK, 'unit': 'wave64 VALU instr/s',
+                'frac': achieved / VALU_PEAK, 'kernel_ms': k_ms, 'kernel': hbm['kernel'],
+                'valu_ops_per_instruction': valu_per_launch * 64 / instrs,
+                'active_lanes_per_valu_pct': prof.get('valu_lane_util_pct'),
+                'valu_insts_per_launch': valu_per_launch, 'hbm': hbm, 'valu': valu_view(prof)}
+    else:
+        roof = hbm
+    res = {'metric': 'emulated core-shots/s (config 4: 2-qubit RB, 1e5 sequences x depth 200, 10 shots each)',
+           'value': n * 2 * world * steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * steps / dt,
+           'ms_per_step': ms_step, 'kernel_ms': kernel_ms, 'steps': steps,
+           'instructions_per_s': instrs * world * steps / dt,
+           'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * steps / dt,
+           'config': {'workload': 'config4_rb_2core_1e5seq_depth200', 'sequences': args.rb_seqs,
+                      'shots_per_sequence': args.rb_spg, 'shots_per_gpu': n, 'commands': int(ps.words.shape[0]),
+                      'program_image_bytes': int(ps.words.nbytes), 'event_cap': cfg.event_cap,
+                      'generate_s': gen_s, 'load_s': load_s},
+           'roofline': roof}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res['cpu_baseline'] = cpu_baselines(ps, cfg, 1 << 20, 'config 4 RB')
+    del out
+    torch.cuda.empty_cache()
     return res
 
 
@@ -267,15 +438,13 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--shots', type=int, default=10 ** 6, help='shots per GPU per step')
+    ap.add_argument('--shots', type=int, default=10 ** 6, help='config-2 shots per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-seconds', type=float, default=12.0)
-    ap.add_argument('--spg', type=int, default=1,
-                    help='shots per delay point run back to back (1: delay k = shot mod 100)')
-    ap.add_argument('--exec-flags', type=int, default=0, help='DPEMU_X_* execution knobs')
     ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
-    ap.add_argument('--no-dds', action='store_true')
-    ap.add_argument('--ar-shots', type=int, default=1250000, help='config-3 shots per GPU per step (0: skip the leg)')
+    ap.add_argument('--ar-shots', type=int, default=1250000, help='config-3 shots per GPU per step')
+    ap.add_argument('--rb-seqs', type=int, default=100000, help='config-4 RB sequences')
+    ap.add_argument('--rb-spg', type=int, default=10, help='config-4 shots per sequence')
+    ap.add_argument('--legs', default='dds,active_reset,rb', help='sub-legs to run (comma list; "" for none)')
     args = ap.parse_args()
 
     import torch
@@ -291,127 +460,35 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
 
-    from distributed_processor_amd import _abi, sharding
-    from distributed_processor_amd.emulator import Emulator, alloc_device_outputs
-
-    ps = build_workload()
+    from distributed_processor_amd.emulator import Emulator
     emu = Emulator(local)
-    emu.load(ps)
-    n = args.shots
-    spg = args.spg
-    cfg = _abi.make_config(8, n_groups=ps.n_groups, shots_per_group=spg, max_cycles=1 << 20, event_cap=8,
-                           trace_cap=0, meas_cap=2, meas_latency=64, seed=0x5EED, p1=0.5,
-                           exec_flags=args.exec_flags)
-    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
     stream = torch.cuda.current_stream()
-    shot0, n = sharding.weak_shard(n, rank)
-    # double-buffered histogram: batch k's all-reduce (the path's only exchange,
-    # RCCL) runs on RCCL's stream while batch k+1's kernel runs
-    hists = [out['hist'], torch.zeros_like(out['hist'])]
-    pending = [None, None]
-    n_steps = [0]
-
-    def step():
-        b = n_steps[0] % 2
-        n_steps[0] += 1
-        if pending[b] is not None:
-            pending[b].wait()                          # this buffer's previous exchange is done
-            pending[b] = None
-        out['hist'] = hists[b]
-        out['hist'].zero_()
-        emu.run_device(cfg, n, shot0, out, stream)
-        pending[b] = sharding.allreduce_histogram(out['hist'], async_op=True)
-
-    def drain():
-        for b in range(2):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
-
-    for _ in range(args.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = sharding.max_over_ranks(time.perf_counter() - t0, device='cuda')
-    # the roofline's kernel time: a second pass of the same steps with HIP
-    # events recorded around the interpreter kernel, so the event records stay
-    # out of the timed region (they cost ~4 % of a step)
-    kernel_pass(emu, args.steps, step, drain)
-    kt = emu.kernel_times()
-    assert len(kt) == args.steps, kt
-    kernel_ms = float(np.mean(kt))
-    kernel_name = emu.last_kernel()
-
-    # accounting from the last step's outputs (identical every step)
-    summ = out['summary'].cpu().numpy().view(np.uint32)
-    s = _abi.unpack_summary(summ)
-    assert (s['status'] == _abi.ST_DONE).all(), 'not every lane reached DONE'
-    hist_total = int(out['hist'].sum().item())
-    assert hist_total == n * world, hist_total
-    lanes = n * cfg.cores_per_shot
-    cycles = float(s['t_end'].astype(np.float64).sum())
-    instrs = float(s['n_instr'].astype(np.float64).sum())
-    alg_bytes = float(bytes_per_lane(summ, cfg).sum())
-
-    total_core_shots = lanes * world * args.steps
-    value = total_core_shots / dt
-    achieved_gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
-
-    # rocprofv3 PMC passes of this workload (scripts/gpu_r01.sh -> profiles/): HBM
-    # bytes per launch, and the VALU view (instructions per wave, issue share,
-    # active lanes per VALU instruction = divergence)
-    traffic, valu = None, None
-    pmc = os.path.join(REPO, 'profiles', PROFILE_TAG + '_interp_pmc.json')
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            prof = json.load(f)
-        traffic = prof.get('hbm_bytes_per_launch')
-        valu = {k: prof.get(k) for k in ('valu_insts_per_wave', 'valu_issue_pct', 'valu_lane_util_pct',
-                                         'duration_ns', 'kernel')}
-        valu['source'] = os.path.relpath(pmc, REPO)
-
+    main_leg = leg_ramsey(emu, args, world, rank, stream)
     result = {
         'metric': 'emulated core-shots/s (config 2: 8-core Ramsey, 100 delays, 1e6 shots/GPU)',
-        'value': value,
+        'value': main_leg['value'],
         'unit': 'core-shots/s',
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
-        'ms_per_step': dt / args.steps * 1e3,
+        'ms_per_step': main_leg['ms_per_step'],
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'u32',
         'data': 'synthetic (assembled Ramsey programs, Philox outcomes p=0.5)',
-        'config': {'workload': 'config2_ramsey_8core_100pt', 'shots_per_gpu': n, 'cores_per_shot': 8,
-                   'shots_per_delay_point': spg,
-                   'global_shots_per_step': n * world, 'parallelism': 'shots sharded, {} GPU(s)'.format(world)},
-        'shots_per_s': value / 8,
-        'qclk_cycles_per_s': cycles * world * args.steps / dt,
-        'instructions_per_s': instrs * world * args.steps / dt,
-        'kernel_ms': kernel_ms,
-        'roofline': {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': achieved_gbs / HBM_PEAK_GBS, 'traffic': traffic,
-                     'bytes_per_launch': alg_bytes, 'kernel_ms': kernel_ms,
-                     'kernel': 'dpemu::' + kernel_name, 'valu': valu},
+        'config': main_leg['config'],
+        'collective_world_size': dist.get_world_size() if dist.is_initialized() else 1,
+        'collective_backend': dist.get_backend() if dist.is_initialized() else None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result['cpu_baseline'] = cpu_baseline(ps, cfg, args.cpu_seconds)
-    if not args.no_dds:
-        result['dds'] = dds_leg(emu, args, world, rank, stream)
-    if args.ar_shots > 0:
-        result['active_reset'] = active_reset_leg(emu, args, world, rank, stream)
+    for k in ('shots_per_s', 'qclk_cycles_per_s', 'instructions_per_s', 'kernel_ms', 'roofline', 'timeline_gather',
+              'cpu_baseline'):
+        if k in main_leg:
+            result[k] = main_leg[k]
+    fns = {'dds': leg_dds, 'active_reset': leg_active_reset, 'rb': leg_rb}
+    for name in [x for x in args.legs.split(',') if x]:
+        result[name] = fns[name](emu, args, world, rank, stream)
+    result['box'] = {'fill_GBps': fill_gbps(), 'device': torch.cuda.get_device_name(local)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     emu.close()

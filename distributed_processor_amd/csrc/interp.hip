@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         __syncthreads();
     }
     if constexpr (PLDS) {
-        const uint32_t b = stage_programs(p, s_prog, s_pref, s_scan, spos);
+        const uint32_t b = stage_programs(p, s_prog, s_pref, s_scan, spos, core);
         if (valid) base = b;
     }
     if constexpr (!STRAIGHT) {

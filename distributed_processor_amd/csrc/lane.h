@@ -123,7 +123,7 @@ __device__ __forceinline__ uint4 event_record(uint32_t te, uint32_t pe, uint32_t
 // the footprint within the dynamic LDS: host-checked).  Every thread of the
 // workgroup calls it (barriers).  s_pref: BLOCK + 1 words, s_scan: BLOCK / 64.
 __device__ __forceinline__ uint32_t stage_programs(const KParams &p, uint4 *s_prog, uint32_t *s_pref,
-                                                   uint32_t *s_scan, uint32_t spos)
+                                                   uint32_t *s_scan, uint32_t spos, uint32_t my_core)
 {
     const uint32_t tid = threadIdx.x, C = p.C;
     const uint32_t n_shots = p.n_lanes >> p.log2C;
@@ -153,7 +153,52 @@ __device__ __forceinline__ uint32_t stage_programs(const KParams &p, uint4 *s_pr
     }
     __syncthreads();
     const uint32_t sp = min(spos, spl);                  // threads past the run: any slot
-    return s_pref[group_step(p, sp, sp0) * C + (threadIdx.x & (C - 1))];
+    return s_pref[group_step(p, sp, sp0) * C + my_core];
+}
+
+// Thread -> (shot, core) of the branch-free kernels (straight.hip, macro.hip):
+// workgroup b covers the run's shots [b S, (b + 1) S), S = BLOCK / C, all C
+// cores, CORE-major inside the workgroup (thread = core * S + shot), so a
+// wave's lanes are consecutive shots of one core -- consecutive output lanes:
+// every event / summary store of a wave is one contiguous run (the
+// interpreter with fproc / sync keeps a shot's cores in one wave instead).
+__device__ __forceinline__ void block_core_major(const KParams &p, uint32_t &sl, uint32_t &core)
+{
+    const uint32_t S_log2 = 8u - p.log2C;                // BLOCK = 256
+    core = threadIdx.x >> S_log2;
+    sl = (blockIdx.x << S_log2) + (threadIdx.x & ((1u << S_log2) - 1u));
+}
+
+// the outcome histogram for block_core_major workgroups: each lane ORs its
+// last measurement into its shot's key in LDS, then one thread per shot
+// counts the key (every thread of the workgroup calls it: barriers)
+__device__ __forceinline__ void count_outcome_block(const KParams &p, uint32_t *s_hist, uint32_t *s_key, bool valid,
+                                                    uint32_t core, uint32_t sl, uint32_t grp, uint32_t last_bit)
+{
+    if (!p.hist && !p.hist_rep) return;                  // uniform
+    const uint32_t tid = threadIdx.x, S_log2 = 8u - p.log2C, S = 1u << S_log2;
+    if (tid < S) s_key[tid] = 0u;
+    __syncthreads();
+    if (valid && last_bit) atomicOr(&s_key[tid & (S - 1u)], 1u << core);
+    __syncthreads();
+    const bool mine = valid && core == 0u;               // thread (core 0, shot): the shot's count
+    const uint32_t key = mine ? s_key[tid] : 0u;
+    const uint64_t bin = (uint64_t)grp * (1ull << p.C) + key;
+    if (p.hist_rep) {
+        uint32_t *rep = p.hist_rep + (uint64_t)(blockIdx.x % p.hist_reps) * p.hist_stride;
+        if (p.hist_lds) {
+            if (mine) atomicAdd(&s_hist[bin], 1u);
+            __syncthreads();
+            const uint32_t bins = p.n_groups << p.C;
+            for (uint32_t i = tid; i < bins; i += BLOCK)
+                if (s_hist[i]) atomicAdd(&rep[i], s_hist[i]);
+        } else if (mine) {
+            atomicAdd(&rep[bin], 1u);
+        }
+    } else if (mine) {
+        atomicAdd(&p.hist[bin], 1ull);
+    }
+    (void)sl;
 }
 
 // dpemu_outputs::summary row of a lane (include/dpemu.h)

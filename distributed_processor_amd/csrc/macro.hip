@@ -49,28 +49,29 @@ __device__ __forceinline__ uint32_t alu_macro(uint32_t op, uint32_t a, uint32_t 
     return r;
 }
 
-__global__ void __launch_bounds__(BLOCK) macro_kernel(const KParams p)
+// 6 waves per SIMD: the register budget of the prefetched loop (80 VGPRs);
+// same-process A/B on config 4 (scripts/ab.py): 4.76 ms vs 5.05 without the
+// prefetch and 6.7 when squeezed to 7 waves (spills)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6))) macro_kernel(const KParams p)
 {
     __shared__ uint32_t s_hist[HIST_LDS_MAX];
     __shared__ uint32_t s_regs[16][BLOCK];
+    __shared__ uint32_t s_key[BLOCK];
     const uint32_t tid = threadIdx.x;
     const uint32_t C = p.C;
-    const uint32_t pos = blockIdx.x * BLOCK + tid;
-    const bool valid = pos < p.n_lanes;
-    const uint32_t core = pos & (C - 1);
-    const uint32_t sl = pos >> p.log2C;              // shot within the run
+    uint32_t sl, core;                                // shot within the run, core (core-major workgroup)
+    block_core_major(p, sl, core);
+    const bool valid = sl < p.n_shots;
     const uint32_t lane = out_lane(p, sl, core);      // output lane index (core-major)
-    const uint64_t shot = p.shot_begin + sl;
     const uint32_t n_lanes = p.n_lanes;
 
-    uint32_t grp = 0, mb = 0, ml = 0;
+    uint32_t mb = 0, ml = 0;
     if (valid) {
-        grp = shot_group(p, sl);
+        const uint32_t grp = shot_group(p, sl);
         const uint32_t prog = p.prog_table[(uint64_t)grp * C + core];
         mb = p.macro_off[prog];
         ml = p.macro_off[prog + 1] - 1u;             // the terminal macro
     }
-    const uint32_t thr = valid ? p.p1_thr[core] : 0u;
     if (p.hist_lds) {
         for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
         __syncthreads();
@@ -106,7 +107,8 @@ __global__ void __launch_bounds__(BLOCK) macro_kernel(const KParams p)
             const bool is_meas = kind == 0u && ((pe >> 24) & 3u) == p.meas_elem;   // meas_elem 0xFF: none
             uint32_t bit = 0;
             if (is_meas) {
-                bit = meas_bit(p, shot, core, n_meas, thr, pa, pe);
+                // (shot and threshold re-derived here: few registers in the loop)
+                bit = meas_bit(p, p.shot_begin + sl, core, n_meas, p.p1_thr[core], pa, pe);
                 if (p.meas && n_meas < p.meas_cap)
                     p.meas[(uint64_t)n_meas * n_lanes + lane] = make_uint2(te + r + p.meas_latency, bit);
             }
@@ -256,9 +258,15 @@ __global__ void __launch_bounds__(BLOCK) macro_kernel(const KParams p)
     const uint4 *mbase = p.macros;
     auto addr = [&](uint32_t m) __attribute__((always_inline)) -> const uint4 * { return mbase + 2ull * min(mb + m, ml); };
 
-    for (uint32_t m = 0; __ballot(st == 0u); m++) {
-        const uint4 *q = addr(m);
-        const uint4 a = q[0], u = q[1];
+    // one macro ahead: macro m + 1 is in flight while macro m executes
+    uint4 an = addr(0u)[0], un = addr(0u)[1];
+    for (uint32_t m = 1; __ballot(st == 0u); m++) {
+        const uint4 a = an, u = un;
+        {
+            const uint4 *q = addr(m);                   // the next macro: in flight during this one
+            an = q[0];
+            un = q[1];
+        }
         alu_step(a.x, a.y);
         alu_step(a.z, a.w);
         pulse_step(u);
@@ -275,7 +283,7 @@ __global__ void __launch_bounds__(BLOCK) macro_kernel(const KParams p)
 #pragma unroll
         for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = s_regs[r][tid];
     }
-    count_outcome(p, s_hist, valid, core, grp, last_bit);
+    count_outcome_block(p, s_hist, s_key, valid, core, sl, valid ? shot_group(p, sl) : 0u, last_bit);
 }
 
 hipError_t launch_macro(const KParams &p, hipStream_t stream)

@@ -45,13 +45,13 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
     __shared__ uint32_t s_hist[HIST_LDS_MAX];
     __shared__ uint32_t s_pref[LDS ? BLOCK + 1 : 1];
     __shared__ uint32_t s_scan[BLOCK / 64];
+    __shared__ uint32_t s_key[BLOCK];
     extern __shared__ uint4 s_prog[];
     const uint32_t tid = threadIdx.x;
     const uint32_t C = p.C;
-    const uint32_t pos = blockIdx.x * BLOCK + tid;
-    const bool valid = pos < p.n_lanes;
-    const uint32_t core = pos & (C - 1);
-    const uint32_t sl = pos >> p.log2C;              // shot within the run
+    uint32_t sl, core;                                // shot within the run, core (core-major workgroup)
+    block_core_major(p, sl, core);
+    const bool valid = sl < p.n_shots;
     const uint32_t lane = out_lane(p, sl, core);      // output lane index (core-major)
     const uint64_t shot = p.shot_begin + sl;
     const uint32_t n_lanes = p.n_lanes;
@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
         for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
         __syncthreads();
     }
-    if constexpr (LDS) base = stage_programs(p, s_prog, s_pref, s_scan, sl);
+    if constexpr (LDS) base = stage_programs(p, s_prog, s_pref, s_scan, sl, core);
 
     const uint32_t max_cycles = p.max_cycles;
     uint32_t t = 0, pe = 0, pp = 0, pa = 0;            // next DECODE cycle; pulse register image
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
 #pragma unroll
         for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = 0u;
     }
-    count_outcome(p, s_hist, valid, core, grp, last_bit);
+    count_outcome_block(p, s_hist, s_key, valid, core, sl, grp, last_bit);
 }
 
 template <int SRC, int FB>

@@ -93,6 +93,13 @@ def instr(d) -> Instr:
         return d
     d = dict(d)
     name = d.pop('name')
+    if name == 'sync':
+        # the documented form {'name': 'sync', 'barrier_id': id, 'qubits': [...]}
+        # (compiler.py:78-82): qubits / qubit name the scope; none = the whole program
+        q = d.pop('qubits', None)
+        q = d.pop('qubit', None) if q is None else q
+        if d.get('scope') is None and q is not None:
+            d['scope'] = [q] if isinstance(q, str) else list(q)
     if 'scope' in d and d['scope'] is not None:
         d['scope'] = set(d['scope'])
     if name == 'pulse' and 'scope' not in d:
@@ -552,6 +559,19 @@ def compile_blocks(prog: ScheduleIR, proc_grouping=DEFAULT_PROC_GROUPING) -> Dic
     return progs
 
 
+def sync_mask(program: Dict[tuple, List[dict]], core_order: Sequence[tuple]) -> int:
+    """the dpemu_config.sync_mask a compiled program implies: bit c set for
+    the proc group at index c of ``core_order`` (the emulator's core order)
+    when its program holds a sync.  A sync over a subset of cores needs this
+    mask -- the default mask is every core, and a core that never syncs would
+    leave the barrier waiting (ST_DEADLOCK)."""
+    mask = 0
+    for c, g in enumerate(core_order):
+        if any(st.get('op') == 'sync' for st in program.get(g, ())):
+            mask |= 1 << c
+    return mask
+
+
 class CompiledProgram:
     """The attribute surface ``GlobalAssembler`` reads (``compiler.py:338-366``)."""
 
@@ -683,8 +703,8 @@ def make_basic_blocks(flat: Sequence[Instr]) -> 'OrderedDict[str, List[Instr]]':
 
 def scope_blocks(blocks, qubit_grouping=DEFAULT_QUBIT_GROUPING) -> Dict[str, set]:
     """``ir/passes.py:207-234`` (ScopeProgram): instruction scopes (qubits ->
-    channels), block scopes, and unscoped barrier / delay / idle -> the whole
-    program's scope."""
+    channels), block scopes, and unscoped barrier / delay / idle (and sync, an
+    addition) -> the whole program's scope."""
     scoper = QubitScoper(qubit_grouping)
     scopes = {}
     for name, instrs in blocks.items():
@@ -702,7 +722,7 @@ def scope_blocks(blocks, qubit_grouping=DEFAULT_QUBIT_GROUPING) -> Dict[str, set
     everything = set().union(*scopes.values()) if scopes else set()
     for instrs in blocks.values():
         for ins in instrs:
-            if ins.name in ('barrier', 'delay', 'idle') and ins.scope is None:
+            if ins.name in ('barrier', 'delay', 'idle', 'sync') and ins.scope is None:
                 ins.scope = set(everything)
     return scopes
 

@@ -70,6 +70,53 @@ def allreduce_histogram(hist, group=None, async_op=False):
     return None if async_op else hist
 
 
+class HistogramPipeline:
+    """Per-batch launches with the histogram exchange overlapped (bench.py).
+
+    Batch k's kernel writes its outcome histogram into buffer k % n_buffers;
+    the buffer's all-reduce is enqueued asynchronously right after the launch
+    (on RCCL's stream, ordered after the kernel), so batch k's exchange runs
+    while batch k + 1's kernel does.  Before a buffer is zeroed for reuse, the
+    exchange that last used it is waited for.  ``drain()`` waits for every
+    pending exchange; ``result()`` is then the histogram of the last batch,
+    summed over ranks.  One rank: no collectives, the same call sequence.
+    """
+
+    def __init__(self, hist, n_buffers=2, group=None):
+        import torch
+        if n_buffers < 1:
+            raise ValueError('n_buffers must be >= 1')
+        self.bufs = [hist] + [torch.zeros_like(hist) for _ in range(n_buffers - 1)]
+        self.pending = [None] * n_buffers
+        self.group = group
+        self.k = 0
+
+    def step(self, launch):
+        """launch(hist): enqueue one batch writing into (accumulating on) hist"""
+        b = self.k % len(self.bufs)
+        self.k += 1
+        if self.pending[b] is not None:
+            self.pending[b].wait()                    # this buffer's previous exchange is done
+            self.pending[b] = None
+        h = self.bufs[b]
+        h.zero_()
+        launch(h)
+        self.pending[b] = allreduce_histogram(h, group=self.group, async_op=True)
+        return h
+
+    def drain(self):
+        for b, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[b] = None
+
+    def result(self):
+        """the last batch's rank-summed histogram (after drain)"""
+        if self.k == 0:
+            raise RuntimeError('no batch has run')
+        return self.bufs[(self.k - 1) % len(self.bufs)]
+
+
 def gather_sample(t, group=None):
     """Every rank's equal-shape tensor ``t`` stacked along a new leading rank
     axis (one all_gather).  Collects a sampled subset of lanes' timelines or

@@ -1,0 +1,84 @@
+"""Same-process A/B of libdpemu.so builds (scripts/ab_libs.sh) on one workload.
+
+    python scripts/ab.py --libs ab_build/libdpemu_a.so,ab_build/libdpemu_b.so --workload rb
+
+Every library runs the same launches, interleaved (A B A B ...), with HIP
+events around the kernel (dpemu_kernel_times); the outputs of all libraries
+must be identical.  Prints one JSON line: median kernel ms per library.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def workload(name):
+    from distributed_processor_amd import _abi, isa, workloads
+    from distributed_processor_amd.emulator import ProgramSet
+    if name == 'rb':
+        ps = workloads.config4_rb_set(100000, 200)
+        ops = ps.words[:, 3] >> 28
+        ev = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
+                             ps.offsets.astype(np.int64))
+        cfg = _abi.make_config(2, n_groups=ps.n_groups, shots_per_group=10, max_cycles=1 << 20,
+                               event_cap=int(ev.max()) + 1, meas_cap=2, seed=0x5EED)
+        return ps, cfg, 10 ** 6
+    if name == 'ramsey':
+        ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
+        cfg = _abi.make_config(8, n_groups=100, max_cycles=1 << 20, event_cap=8, meas_cap=2, seed=0x5EED)
+        return ps, cfg, 10 ** 6
+    if name == 'ar':
+        ps = ProgramSet(workloads.config3_active_reset(8))
+        cfg = _abi.make_config(8, max_cycles=50000, event_cap=16, meas_cap=4,
+                               meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED)
+        return ps, cfg, 1250000
+    raise ValueError(name)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--libs', required=True)
+    ap.add_argument('--workload', default='rb')
+    ap.add_argument('--reps', type=int, default=4)
+    ap.add_argument('--steps', type=int, default=5)
+    a = ap.parse_args()
+    import torch
+    from distributed_processor_amd.emulator import Emulator, alloc_device_outputs
+    libs = [os.path.abspath(x) for x in a.libs.split(',')]
+    ps, cfg, n = workload(a.workload)
+    emus = [Emulator(0, lib_path=l) for l in libs]
+    for e in emus:
+        e.load(ps)
+    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))   # one buffer set for all
+    ref = None
+    times = [[] for _ in emus]
+    same = True
+    for rep in range(a.reps):
+        order = range(len(emus)) if rep % 2 == 0 else reversed(range(len(emus)))
+        for i in order:
+            e = emus[i]
+            e.kernel_timing(True)
+            for _ in range(a.steps):
+                out['hist'].zero_()
+                e.run_device(cfg, n, 0, out)
+            torch.cuda.synchronize()
+            kt = e.kernel_times()
+            e.kernel_timing(False)
+            if rep:
+                times[i] += kt
+            snap = {k: out[k].clone() for k in ('summary', 'meas', 'hist')}
+            if ref is None:
+                ref = snap
+            else:
+                same &= all(torch.equal(ref[k], snap[k]) for k in ref)
+    print(json.dumps({'workload': a.workload, 'same_outputs': bool(same), 'kernels': [e.last_kernel() for e in emus],
+                      'median_ms': {os.path.basename(l): float(np.median(t)) for l, t in zip(libs, times)},
+                      'min_ms': {os.path.basename(l): float(np.min(t)) for l, t in zip(libs, times)}}))
+
+
+if __name__ == '__main__':
+    main()

@@ -3,9 +3,11 @@
 Each rank emulates its shard of the global shot range and the ranks combine
 outcome histograms with ``sharding.allreduce_histogram`` and a sampled lane
 gather with ``sharding.gather_sample`` -- the same calls bench.py makes over
-RCCL on GPUs.  The per-rank emulation here is oracle_fast (the checker: no
-GPU in this container); the GPU kernel is pinned to it bit for bit by
-tests/test_gpu_parity.py, including a sharding-invariance test at 10^6 shots.
+RCCL on GPUs -- and bench.py's batch loop itself, ``sharding.HistogramPipeline``
+(double-buffered, asynchronous exchange), runs here with a CPU stand-in for the
+kernel.  The per-rank emulation is oracle_fast (the checker: no GPU in this
+container); the GPU kernel is pinned to it bit for bit by
+tests/test_gpu_parity.py, including sharding-invariance tests at 10^6 shots.
 Rank 0 checks the combined result against one unsharded run.
 """
 
@@ -24,6 +26,7 @@ from distributed_processor_amd.emulator import ProgramSet
 
 N_TOTAL = 1001          # odd: uneven shards
 N_SAMPLE = 7
+N_BATCH, N_BATCHES = 301, 5
 
 
 def _free_port():
@@ -58,10 +61,25 @@ def _rank_main(rank, world, port, out_dir):
         sample = torch.from_numpy(out['summary'][lanes].astype(np.int64))
         gathered = sharding.gather_sample(sample)
         slowest = sharding.max_over_ranks(float(rank + 1))
+        # bench.py's batch loop: batch b = global shots [b * N_BATCH, (b + 1) * N_BATCH),
+        # this rank's share of it emulated by the stand-in "kernel" (oracle_fast
+        # accumulating into the pipeline's buffer, as the GPU kernel does)
+        pipe = sharding.HistogramPipeline(torch.zeros_like(hist))
+        for b in range(N_BATCHES):
+            b0, bn = sharding.shard_range(N_BATCH, rank, world)
+
+            def launch(h, b=b, b0=b0, bn=bn):
+                o = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, b * N_BATCH + b0, bn,
+                                    threads=1, want=('hist',))
+                h += torch.from_numpy(o['hist'].astype(np.int64))
+            pipe.step(launch)
+        pipe.drain()
+        last_two = torch.stack([pipe.bufs[(N_BATCHES - 2) % 2], pipe.result()])
         if rank == 0:
             np.save(os.path.join(out_dir, 'hist.npy'), hist.numpy())
             np.save(os.path.join(out_dir, 'gathered.npy'), gathered.numpy())
             np.save(os.path.join(out_dir, 'slowest.npy'), np.array([slowest]))
+            np.save(os.path.join(out_dir, 'pipeline.npy'), last_two.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -118,3 +136,22 @@ def test_two_rank_gloo_matches_unsharded(tmp_path):
         lanes = (loc // n) * N_TOTAL + begin + loc % n          # the same (shot, core) in the unsharded run
         np.testing.assert_array_equal(gathered[r], full['summary'][lanes].astype(np.int64))
     assert float(np.load(tmp_path / 'slowest.npy')[0]) == float(world)
+    # the pipeline's last two batches, summed over ranks = the unsharded batches
+    last_two = np.load(tmp_path / 'pipeline.npy')
+    for j, b in enumerate((N_BATCHES - 2, N_BATCHES - 1)):
+        ref = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, b * N_BATCH, N_BATCH, threads=2,
+                              want=('hist',))['hist'].astype(np.int64)
+        np.testing.assert_array_equal(last_two[j], ref)
+
+
+def test_pipeline_single_rank_and_buffer_reuse():
+    """one rank: the pipeline is the plain batch loop; a buffer is zeroed
+    before its reuse, so every batch's histogram is that batch alone"""
+    h = torch.zeros(4, dtype=torch.int64)
+    pipe = sharding.HistogramPipeline(h, n_buffers=2)
+    for b in range(5):
+        pipe.step(lambda t, b=b: t.add_(b + 1))
+    pipe.drain()
+    assert pipe.result().tolist() == [5] * 4 and pipe.bufs[1 - (5 - 1) % 2].tolist() == [4] * 4
+    with pytest.raises(RuntimeError):
+        sharding.HistogramPipeline(h).result()

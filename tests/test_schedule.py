@@ -579,6 +579,38 @@ def test_sync_circuits_never_late_cpu():
         assert not (s['flags'] & _abi.F_LATE).any(), (k, circ)
 
 
+def test_sync_over_a_subset_of_cores():
+    """a sync scoped to a subset of the cores (the 'qubits' spelling of its
+    scope) lands only on those cores; an unscoped sync lands on every core.
+    The subset sync needs the sync_mask sc.sync_mask derives: with the
+    default all-cores mask the core that never syncs leaves the barrier
+    waiting (ST_DEADLOCK); with the derived mask every lane finishes"""
+    import oracle
+    from distributed_processor_amd.emulator import ProgramSet
+    chans = hw.load_channel_configs(os.path.join(GOLDEN, 'channel_config.json'))
+    circ = [{'name': 'X90', 'qubit': ['Q0']}, {'name': 'X90', 'qubit': ['Q1']},
+            {'name': 'sync', 'barrier_id': 1, 'qubits': ['Q0']},
+            {'name': 'read', 'qubit': ['Q0']}, {'name': 'read', 'qubit': ['Q1']}]
+    compiled = sc.compile_circuit(circ, TABLE, hw.FPGAConfig.rtl_exact())
+    order = sorted(compiled.program, key=lambda g: chans[g[0]].core_ind)
+    has_sync = [any(s['op'] == 'sync' for s in compiled.program[g]) for g in order]
+    assert has_sync == [True, False]
+    assert sc.sync_mask(compiled.program, order) == 0b01
+
+    unscoped = sc.compile_circuit(circ[:2] + [{'name': 'sync', 'barrier_id': 2}] + circ[3:], TABLE,
+                                  hw.FPGAConfig.rtl_exact())
+    assert all(any(s['op'] == 'sync' for s in st) for st in unscoped.program.values())
+    assert sc.sync_mask(unscoped.program, order) == 0b11
+
+    ps = ProgramSet([assemble(compiled)])
+    for mask, status in ((0, _abi.ST_DEADLOCK), (sc.sync_mask(compiled.program, order), _abi.ST_DONE)):
+        cfg = _abi.make_config(2, max_cycles=1 << 16, event_cap=16, meas_cap=4, sync_mask=mask, seed=1)
+        f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, 16, want=('summary',))
+        s = _abi.unpack_summary(f['summary'])
+        assert (s['status'][:16] == status).all(), (mask, s['status'])
+        assert (s['status'][16:] == _abi.ST_DONE).all(), mask
+
+
 @pytest.mark.gpu
 def test_sync_circuits_gpu_vs_oracle():
     from distributed_processor_amd.emulator import Emulator, ProgramSet
