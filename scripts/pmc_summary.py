@@ -24,10 +24,11 @@ import json
 import os
 import sys
 
-# summary key -> kernel-name substrings: the bench's config 2 runs on
-# straight_kernel (branch-free programs), config 3 on the general interp_kernel
-KERNELS = {'interp': ('straight_kernel',), 'active_reset': ('interp_kernel',), 'dds': ('dds_kernel', 'dds_chunk_kernel'),
-           'dds_index': ('dds_index_kernel',), 'hist_reduce': ('hist_reduce_kernel',)}
+# summary key -> kernel-name substrings, one per bench leg: config 2 runs on
+# straight_kernel (pulse-only programs), config 3 on the general
+# interp_kernel, config 4 on macro_kernel, config 5 on dds_tile_kernel
+KERNELS = {'ramsey': ('straight_kernel',), 'active_reset': ('interp_kernel',), 'rb': ('macro_kernel',),
+           'dds': ('dds_tile_kernel',), 'dds_index': ('dds_index_kernel',), 'hist_reduce': ('hist_reduce_kernel',)}
 
 
 # wave64 integer-VALU instructions per second, whole chip: the best rate of
