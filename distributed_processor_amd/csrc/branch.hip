@@ -1,0 +1,377 @@
+// branch.hip -- the interpreter for programs with jumps, fproc_meas reads
+// and sync barriers (rows a1-a11; config 3, active reset) on CDNA4 (gfx950).
+//
+// Same lane mapping, lockstep loop and outputs as interp_kernel (interp.hip):
+// one thread = one (shot, core) lane, a shot's C cores adjacent lanes of ONE
+// wavefront, each iteration retires at most one command per lane and
+// advances its next-DECODE cycle by hdl/ctrl.v's closed-form latency
+// (oracle/fast_model.c).  What differs is how a command retires: the general
+// interpreter dispatches on the opcode (a switch -- under divergence every
+// taken case runs -- whose cases write the loop-carried state on different
+// paths, which the register allocator pays for with copies of all of it on
+// every iteration); here every lane evaluates ONE branch-free datapath, like
+// the gateware does:
+//
+//   wait      = cmd_time - qclk(D)                    pulse trigger / idle
+//   alu_out   = alu(in0, reg[rs1] | qclk(D) | fproc)   alu.v:20-50
+//   next ip   = jump ? target : ip + 1                instr_ptr.v, proc.sv:124
+//   next D    = (tT | R | D) + latency(op)            ctrl.v, 4-bit table per opcode
+//
+// and writes its state once, through selects; branches guard only stores,
+// LDS writes, the measurement draw and the rare reset-hold arithmetic.
+// The cross-core phases are wave-uniform and only run when some lane needs
+// them: the fproc_meas bound before an fproc read, the sync barrier after
+// the iteration's commands (so the last arrival releases the barrier in the
+// same iteration).  The meas_lut back end (FEAT_LUT) and LDS-staged programs
+// stay on interp_kernel.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "lane.h"
+
+namespace dpemu {
+
+namespace {
+
+enum : uint32_t { B_RUN = 0, B_SYNC = 1, B_FIN = 3 };
+
+// decode-to-decode latency per op4 past the command's base cycle (D, the
+// trigger cycle tT for pulse-with-trigger / idle, the fproc ready cycle R):
+// pulse 3, reg_alu / jump_i / inc_qclk / alu_fproc 4, jump_cond / jump_fproc 6
+constexpr uint64_t LATENCY = 0x0003303304646440ull;
+
+__device__ __forceinline__ uint32_t alu_eval(uint32_t op, uint32_t a, uint32_t b)
+{
+    // alu.v:20-50; le = sub[31] ^ overflow == signed a < b
+    const uint32_t sub = a - b;
+    const uint32_t lt = (int32_t)a < (int32_t)b;
+    uint32_t r = a;                 // 0: id0
+    r = (op == 1) ? a + b : r;
+    r = (op == 2) ? sub : r;
+    r = (op == 3) ? (uint32_t)(sub == 0) : r;
+    r = (op == 4) ? lt : r;
+    r = (op == 5) ? (lt ^ 1u) : r;
+    r = (op == 6) ? b : r;
+    r = (op == 7) ? 0u : r;
+    return r;
+}
+
+// group reductions over the C adjacent lanes of a shot (all lanes converged)
+template <int OP>   // 0 = min, 1 = max
+__device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t C)
+{
+    for (uint32_t m = 1; m < C; m <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)m, 64);
+        v = OP == 0 ? (o < v ? o : v) : (o > v ? o : v);
+    }
+    return v;
+}
+
+}  // namespace
+
+template <int FEAT>
+__global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
+{
+    constexpr bool FPROC = (FEAT & FEAT_FPROC) != 0;
+    constexpr bool SYNC = (FEAT & FEAT_SYNC) != 0;
+    constexpr int MT = FPROC ? MEAS_LOOKUP : 1;
+
+    __shared__ uint32_t s_regs[16][BLOCK];
+    __shared__ uint32_t s_mt[MT][BLOCK];              // measurements {valid cycle << 1 | bit}, readable by the shot
+    __shared__ uint32_t s_hist[HIST_LDS_MAX];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t C = p.C;
+    const uint32_t pos = blockIdx.x * BLOCK + tid;   // thread position; a shot's cores are adjacent
+    const bool valid = pos < p.n_lanes;
+    const uint32_t core = pos & (C - 1);
+    const uint32_t spos = pos >> p.log2C;
+    const uint32_t lane = out_lane(p, spos, core);   // output lane index (core-major)
+    const uint64_t shot = p.shot_begin + spos;
+    const uint32_t wl = tid & 63;
+    const uint32_t leader_tid = tid & ~(C - 1);
+    const uint32_t n_lanes = p.n_lanes, max_cycles = p.max_cycles;
+
+    uint32_t nprog = 0, grp = 0, prog = 0, base = 0;
+    if (valid) {
+        grp = shot_group(p, spos);
+        prog = p.prog_table[(uint64_t)grp * C + core];
+        base = p.offsets[prog];
+        nprog = p.n_instr[prog];
+    }
+    // command k of this lane's program, zero (DONE) past its end, in bounds for
+    // any k: the program-major image has a zero guard after every program, the
+    // command-major copy zeros past each program's end and a guard row
+    const bool cmd_major = p.fetch_stride != 1u;
+    const uint32_t fetch_off = cmd_major ? prog : base, k_max = cmd_major ? p.max_len : nprog;
+    const uint32_t thr_core = valid ? p.p1_thr[core] : 0u;
+    if (p.hist_lds) {
+        for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
+    if constexpr (FPROC) {
+#pragma unroll
+        for (int m = 0; m < MT; m++) s_mt[m][tid] = INF32;
+    }
+
+    uint32_t mode = valid ? B_RUN : B_FIN;
+    // qclk(x) = x + qoff for every decode after the first (hdl/qclk.v: it
+    // counts from 0 at cycle 1 after the reset hold; inc_qclk and the sync
+    // restart reload it).  A lane's FIRST decode is the only one that can
+    // fall in the reset hold (qclk(0) = qclk(1) = 0): it takes the peeled
+    // first step below.
+    uint32_t ip = 0, t = 0, qoff = 0xFFFFFFFFu;
+    uint32_t pe = 0, pp = 0, pa = 0;                 // pulse regs: env|cfg<<24, phase|freq<<17, amp
+    uint32_t wait_d = 0, status = 0, flags = 0, t_end = 0;
+    uint32_t n_ev = 0, n_tr = 0, n_meas = 0, n_exec = 0, meas_bits = 0, last_bit = 0;
+    const bool is_part = SYNC ? (((p.sync_mask >> core) & 1ull) != 0) : false;
+    uint4 *const ev_lane = p.events + lane;          // event slot k of this lane at ev_lane[k * n_lanes]
+
+    // pulse_iface strobe at cycle te (kind 0: trigger, 1: phase reset) with the
+    // current pulse registers for lanes with `ok`; readout-element triggers
+    // draw the measurement.  Overflow flags come from the final counts.
+    auto emit = [&](bool ok, uint32_t te, uint32_t kind) __attribute__((always_inline)) {
+        if (ok) {
+            if (n_ev < p.event_cap && p.events) ev_lane[(uint64_t)n_ev * n_lanes] = event_record(te, pe, pp, pa, kind);
+            n_ev++;
+            if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {   // meas_elem 0xFF: none
+                const uint32_t bit = meas_bit(p, shot, core, n_meas, thr_core, pa, pe);
+                const uint32_t tv = te + p.meas_latency;
+                if constexpr (FPROC) {
+                    if (n_meas < (uint32_t)MT) s_mt[n_meas < (uint32_t)MT ? n_meas : 0u][tid] = (tv << 1) | bit;
+                }
+                if (p.meas && n_meas < p.meas_cap) p.meas[(uint64_t)n_meas * n_lanes + lane] = make_uint2(tv, bit);
+                meas_bits |= (n_meas < 32u ? bit : 0u) << (n_meas & 31u);
+                last_bit = bit;
+                n_meas++;
+            }
+        }
+    };
+
+    auto emit_trace = [&](bool ok, uint32_t tt, uint32_t addr, uint32_t val) __attribute__((always_inline)) {
+        if (ok) {
+            if (n_tr < p.trace_cap && p.trace) p.trace[(uint64_t)n_tr * n_lanes + lane] = make_uint4(tt, addr, val, 0u);
+            n_tr++;
+        }
+    };
+
+    // latest measurement of group lane q with valid cycle <= d (slots in time order, INF = empty)
+    auto meas_lookup = [&](uint32_t q_tid, uint32_t d) -> uint32_t {
+        uint32_t res = 0;
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+            const uint32_t e = s_mt[m][q_tid];
+            if (e != INF32 && (e >> 1) <= d) res = e & 1u;
+        }
+        return res;
+    };
+
+    // sync barrier keys: a participant's SYNC decode while it waits, its next
+    // decode while it runs (a lower bound of its arrival), INF once finished
+    auto sync_maxkey = [&]() -> uint32_t {
+        const uint32_t key = is_part ? ((mode == B_SYNC) ? wait_d : (mode == B_RUN) ? t : INF32) : 0u;
+        return group_reduce<1>(key, C);
+    };
+
+    auto finish = [&](bool stop, uint32_t st, uint32_t at) __attribute__((always_inline)) {
+        status = stop ? st : status;
+        t_end = stop ? at : t_end;
+        mode = stop ? B_FIN : mode;
+    };
+
+    // One lockstep iteration: every running lane retires at most one command.
+    // FIRST: the peeled first iteration, where every lane decodes at cycle 0
+    // inside the reset hold.  Returns whether any lane is still live.
+    auto iteration = [&](auto first_tag) -> bool {
+        constexpr bool FIRST = decltype(first_tag)::value;
+        // max_cycles at decode
+        finish(mode == B_RUN && t > max_cycles, ST_MAX_CYCLES, t);
+        const bool run = mode == B_RUN;
+        const uint4 u = p.fetch[(uint64_t)min(ip, k_max) * p.fetch_stride + fetch_off];
+        const uint32_t op = u.y >> 28;
+
+        // ---- fproc_meas bound (FPROC): a read at D needs every meas_valid <= D
+        // known, i.e. the group's lower bound on its next strobe + meas_latency > D
+        bool stall = false;
+        if constexpr (FPROC) {
+            const bool fp = run && (op == 4u || op == 5u);
+            if (__any(fp)) {
+                uint32_t bound = run ? t + 2u : INF32;
+                if constexpr (SYNC) {
+                    if (__any(mode == B_SYNC)) {
+                        const uint32_t maxkey = sync_maxkey();
+                        if (mode == B_SYNC && is_part && maxkey != INF32) bound = maxkey + p.sync_latency + 5u;
+                    }
+                }
+                const uint32_t gmin = group_reduce<0>(bound, C);
+                stall = fp && !((uint64_t)gmin + p.meas_latency > (uint64_t)t);
+            }
+        }
+        const bool go = run && !stall;
+        n_exec += go ? 1u : 0u;
+        const uint32_t D = t;
+        // qclk at this decode (0 in the reset hold)
+        const uint32_t qD = FIRST ? 0u : D + qoff;
+
+        // ---- pulse-class and terminal commands (0, 8-F): one branch-free datapath ----
+        // pulse write / trigger, idle, pulse reset (ctrl.v: D + 3, or tT + 3
+        // after the cmd_time wait), done, hang.  The commands between a
+        // program's syncs and branches are almost all of this class.
+        const bool pcls = (0xFF01u >> op) & 1u;
+        {
+            const bool pg = go && pcls;
+            const bool waits = (0x1200u >> op) & 1u;    // 9: pulse trigger, C: idle
+            // tT = the first cycle >= D with qclk == cmd_time
+            uint32_t wait = u.x - qD;
+            bool big = false, dbl = false;
+            if constexpr (FIRST) {                       // qclk(0) = qclk(1) = 0 (proc.sv:125-136)
+                dbl = u.x == 0u;
+                const uint64_t w = dbl ? 0ull : 1ull + u.x;
+                wait = (uint32_t)w;
+                big = (w >> 32) != 0ull;
+            }
+            const bool late = waits && (big || wait >= 0x80000000u);
+            const bool over = waits && (big || wait > max_cycles - D);
+            const uint32_t tT = D + (waits ? wait : 0u);
+            const bool cont = pg && ((0x1B00u >> op) & 1u) && !over;   // 8, 9, B, C in the budget
+            // pulse_reg.sv:59-97 (write enables are zero except for 8 / 9):
+            // immediates, then reg[rs0] into register-sourced fields
+            uint32_t pe2 = pe, pp2 = pp, pa2 = pa;
+            pulse_write(u, pe2, pp2, pa2);
+            if (cont && (u.w & UOP_ANY_RS)) {
+                const uint32_t r0 = s_regs[(u.w >> 20) & 15u][tid];
+                if (u.w & UOP_RS_ENV) pe2 |= r0 & 0xFFFFFFu;
+                if (u.w & UOP_RS_PH) pp2 |= r0 & 0x1FFFFu;
+                if (u.w & UOP_RS_FR) pp2 |= (r0 & 0x1FFu) << 17;
+                if (u.w & UOP_RS_AMP) pa2 = r0 & 0xFFFFu;
+            }
+            pe = cont ? pe2 : pe;
+            pp = cont ? pp2 : pp;
+            pa = cont ? pa2 : pa;
+            // strobes: trigger at tT + 2 (cmd_time 0 in the reset hold strobes
+            // twice), phase reset at D
+            const bool rst = op == 0xBu;
+            emit(cont && (op == 9u || rst), rst ? D : tT + 2u, rst ? 1u : 0u);
+            if constexpr (FIRST) {
+                const bool two = cont && dbl && op == 9u;
+                emit(two, tT + 3u, 0u);
+                flags |= two ? F_DOUBLE_STROBE : 0u;
+            }
+            flags |= (pg && late) ? F_LATE : 0u;
+            if (__any(pg && !cont))
+                finish(pg && !cont, over ? ST_MAX_CYCLES : op >= 0xDu ? ST_HUNG_OPCODE : ST_DONE, D);
+            ip = cont ? ((ip + 1u) & 0xFFFFu) : ip;
+            t = cont ? tT + 3u : t;
+        }
+        // ---- register, jump, fproc and sync commands (1-7) ----
+        if (__any(go && !pcls)) {
+            const bool sg = go && !pcls;
+            const bool is_fp = op == 4u || op == 5u;
+            const uint32_t reg0 = s_regs[(u.w >> 20) & 15u][tid];
+            const uint32_t reg1 = s_regs[(u.y >> 4) & 15u][tid];
+            uint32_t data = 0;
+            const uint32_t R = D + 2u;                   // fproc_meas.sv:18-35: ready two cycles after the read
+            if constexpr (FPROC) {
+                if (__any(sg && is_fp)) {
+                    if (sg && is_fp) data = meas_lookup(leader_tid + (((u.z >> 16) & 0xFFu) & (C - 1u)), D);
+                }
+            }
+            const uint32_t in0 = (u.y & 8u) ? reg0 : u.x;
+            const uint32_t out = alu_eval(u.y & 7u, in0, op == 6u ? qD : is_fp ? data : reg1);
+            // not reached (the host picks kernels by opcode): fproc / sync without the feature
+            const bool absent = (!FPROC && is_fp) || (!SYNC && op == 7u);
+            const bool r_over = FPROC && is_fp && R > max_cycles;
+            const bool fin = r_over || absent;
+            const bool cont = sg && !fin;
+            const bool to_sync = SYNC && cont && op == 7u;
+            const bool adv = cont && !to_sync;
+            const uint32_t t_next = (is_fp ? R : D) + (uint32_t)((LATENCY >> (4u * op)) & 15u);
+            const bool take = op == 2u || ((op == 3u || op == 5u) && (out & 1u));
+            const uint32_t ip_next = take ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+            // reg_file write (reg_alu, alu_fproc) and the register / qclk trace
+            const bool wr = cont && (op == 1u || op == 4u);
+            if (wr) s_regs[(u.y >> 8) & 15u][tid] = out;
+            const bool inc = cont && op == 6u;
+            emit_trace(wr || inc, (op == 4u ? R : D) + 3u, inc ? TRACE_QCLK_LOAD : (u.y >> 8) & 15u,
+                       inc ? out + 3u : out);
+            qoff = inc ? out - D : qoff;                 // qclk(D + 3) = out + 3
+            finish(sg && fin, r_over ? ST_MAX_CYCLES : ST_DEADLOCK, D);
+            wait_d = to_sync ? D : wait_d;
+            mode = to_sync ? B_SYNC : mode;
+            ip = adv ? ip_next : ip;
+            t = adv ? t_next : t;
+        }
+
+        // ---- sync barrier (SYNC): complete when every participant waits; the
+        // last arrival releases it in the same iteration ----
+        if constexpr (SYNC) {
+            if (__any(mode == B_SYNC)) {
+                const uint32_t maxkey = sync_maxkey();
+                const uint64_t b = __ballot(is_part && mode == B_SYNC);
+                const uint64_t pm = __ballot(is_part);
+                const bool all_arrived = group_bits(b, wl, C) == group_bits(pm, wl, C) && group_bits(pm, wl, C) != 0ull;
+                const bool rel = mode == B_SYNC && is_part && all_arrived;
+                const uint32_t S = maxkey + p.sync_latency;   // sync.ready; qclk restarts at S + 2
+                const bool ok = rel && S <= max_cycles;
+                emit_trace(ok, S + 2u, TRACE_QCLK_RST, 0u);
+                qoff = ok ? 0u - (S + 2u) : qoff;
+                ip = ok ? ((ip + 1u) & 0xFFFFu) : ip;
+                t = ok ? S + 3u : t;
+                mode = ok ? B_RUN : mode;
+                finish(rel && !ok, ST_MAX_CYCLES, wait_d);
+                // a shot in which no lane retired or was released can never progress
+                finish(group_bits(__ballot(go || rel), wl, C) == 0ull && mode == B_SYNC, ST_DEADLOCK, wait_d);
+            }
+        }
+        if constexpr (FPROC) {   // this iteration's s_mt writes before the next iteration's reads
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        return __any(mode != B_FIN);
+    };
+
+    if (__any(mode != B_FIN) && iteration(std::true_type{})) {
+        // internal-error guard: a correct run retires an instruction of >= 3
+        // cycles in some lane of every live shot each iteration, so it never trips
+        for (uint32_t iter = 2; iteration(std::false_type{});) {
+            if (++iter > p.iter_guard) {
+                flags |= mode != B_FIN ? F_GUARD : 0u;
+                finish(mode != B_FIN, ST_DEADLOCK, t);
+                break;
+            }
+        }
+    }
+    flags |= (n_ev > p.event_cap ? F_EVENT_OVF : 0u) | (n_meas > min(p.meas_cap, MEAS_LOOKUP) ? F_MEAS_OVF : 0u) |
+             ((p.trace_cap && n_tr > p.trace_cap) ? F_TRACE_OVF : 0u);
+
+    if (valid && p.summary) {
+        const uint32_t qclk_end = t_end == 0u ? 0u : t_end + qoff;   // t_end = 0: finished in the reset hold
+        write_summary(p, lane, t_end, ip, status, flags, n_ev, n_exec, qclk_end, n_meas, meas_bits, n_tr);
+    }
+    if (valid && p.regs_out) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = s_regs[r][tid];
+    }
+    count_outcome(p, s_hist, valid, core, grp, last_bit);
+}
+
+hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream)
+{
+    const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
+    if (blocks == 0) return hipSuccess;
+    switch (feat & (FEAT_FPROC | FEAT_SYNC)) {
+    case 0: hipLaunchKernelGGL(branch_kernel<0>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    case FEAT_FPROC: hipLaunchKernelGGL(branch_kernel<FEAT_FPROC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    case FEAT_SYNC: hipLaunchKernelGGL(branch_kernel<FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
+    default:
+        hipLaunchKernelGGL(branch_kernel<FEAT_FPROC | FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace dpemu

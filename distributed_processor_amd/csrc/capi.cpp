@@ -506,10 +506,16 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             hist_stride = stride;
         }
     }
+    // the branch-free datapath (branch.hip) for every other program, except
+    // the meas_lut back end and LDS-staged programs, which the general
+    // interpreter runs (and DPEMU_X_GENERAL: everything on it)
+    const bool branch = !uniform && !macro && !(feat & (FEAT_LUT | FEAT_PROG_LDS)) &&
+                        !(cfg->exec_flags & DPEMU_X_GENERAL);
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
     else if (macro) HIPCHK(ctx, launch_macro(p, stream));
+    else if (branch) HIPCHK(ctx, launch_branch(p, feat, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, stream));
     {
@@ -519,6 +525,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
                      src == STRAIGHT_ROWS ? "rows" : src == STRAIGHT_PROG ? "prog" : "lds", fetch_batch);
         else if (macro)
             snprintf(name, sizeof name, "macro_kernel");
+        else if (branch)
+            snprintf(name, sizeof name, "branch_kernel<feat=0x%x>", feat & (FEAT_FPROC | FEAT_SYNC));
         else
             snprintf(name, sizeof name, "interp_kernel<feat=0x%x>", feat);
         ctx->last_kernel = name;

@@ -201,18 +201,173 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
             break;
         }
 
-        // ---------------- fetch + decode (RUN lanes) ----------------
+        // ---------------- fetch (RUN lanes) ----------------
         bool run = (mode == M_RUN);
         if (run && t > p.max_cycles) { finish(ST_MAX_CYCLES, t); run = false; }
         uint4 u = make_uint4(0u, 0u, 0u, 0u);             // past the program: op4 0 = DONE
         if (run && ip < nprog) u = PLDS ? s_prog[base + ip] : p.fetch[(uint64_t)ip * p.fetch_stride + fetch_off];
         const uint32_t op4 = u.y >> 28;
-        const uint32_t alu = u.y & 7u;
-        const uint32_t reg0 = STRAIGHT ? 0u : s_regs[(u.w >> 20) & 15u][tid];
-        const uint32_t reg1 = STRAIGHT ? 0u : s_regs[(u.y >> 4) & 15u][tid];
-        const uint32_t in0 = (u.y & 8u) ? reg0 : u.x;
-        const uint32_t qD = (t < qa_t) ? 0u : qa_q + (t - qa_t);
         const bool is_fproc = run && (op4 == 4u || op4 == 5u);
+
+        // fproc_meas read at D = t (pending in a running lane): it needs every
+        // meas_valid <= D known, i.e. the group's strobe bound + meas_latency > D
+        auto fproc_stall = [&](uint32_t gmin) -> bool {
+            if constexpr (FPROC) {
+                if (is_fproc && p.fproc_mode == 0u) return !((uint64_t)gmin + p.meas_latency > (uint64_t)t);
+            }
+            return false;
+        };
+
+        // Retire the fetched command u (opcode op) in a running, unstalled
+        // lane: hdl/ctrl.v's decode-to-decode latency in closed form
+        // (DESIGN.md §2).  Called with a wave-uniform op from the fast path
+        // (a scalar switch: only that opcode's code runs) and with the lane's
+        // own op4 from the general path.  Registers are read where a command
+        // uses them.
+        auto retire = [&](const uint32_t op) {
+            n_exec++;
+            const uint32_t D = t;
+            const uint32_t alu = u.y & 7u;
+            auto reg = [&](uint32_t r) -> uint32_t { return STRAIGHT ? 0u : s_regs[r & 15u][tid]; };
+            auto in0 = [&]() -> uint32_t { return (u.y & 8u) ? reg(u.w >> 20) : u.x; };
+            auto qclk = [&](uint32_t d) -> uint32_t { return (d < qa_t) ? 0u : qa_q + (d - qa_t); };
+            switch (op) {
+            case 0x0: case 0xA:
+                finish(ST_DONE, D);
+                break;
+            case 0xB:
+                emit_event(D, 1u);
+                ip = (ip + 1u) & 0xFFFFu; t = D + 3u;
+                break;
+            case 0x8: case 0x9: case 0xC: {
+                bool go = true;
+                uint32_t tT = D;
+                bool dbl = false;
+                if (op != 0x8) {
+                    const uint32_t T = u.x;
+                    uint64_t wait;
+                    if (D < qa_t) { dbl = (T == 0u); wait = dbl ? 0ull : (uint64_t)(qa_t - D) + (uint32_t)(T - qa_q); }
+                    else wait = (uint32_t)(T - qclk(D));
+                    if (wait >= 0x80000000ull) flags |= F_LATE;
+                    if (wait > (uint64_t)(p.max_cycles - D)) { finish(ST_MAX_CYCLES, D); go = false; }
+                    else tT = D + (uint32_t)wait;
+                }
+                if (go && op != 0xC) {
+                    // pulse_reg.sv:59-97: immediates, then reg[rs0] into register-sourced fields
+                    pulse_write(u, pe, pp, pa);
+                    if (!STRAIGHT && (u.w & UOP_ANY_RS)) {
+                        const uint32_t r0 = reg(u.w >> 20);
+                        if (u.w & UOP_RS_ENV) pe |= r0 & 0xFFFFFFu;
+                        if (u.w & UOP_RS_PH) pp |= r0 & 0x1FFFFu;
+                        if (u.w & UOP_RS_FR) pp |= (r0 & 0x1FFu) << 17;
+                        if (u.w & UOP_RS_AMP) pa = r0 & 0xFFFFu;
+                    }
+                }
+                if (go) {
+                    if (op == 0x9) {
+                        emit_event(tT + 2u, 0u);
+                        if (dbl) { emit_event(tT + 3u, 0u); flags |= F_DOUBLE_STROBE; }
+                    }
+                    ip = (ip + 1u) & 0xFFFFu;
+                    t = tT + 3u;
+                }
+                break;
+            }
+            case 0x1: {
+                if constexpr (!STRAIGHT) {
+                    const uint32_t out = alu_op(alu, in0(), reg(u.y >> 4));
+                    const uint32_t rd = (u.y >> 8) & 15u;
+                    s_regs[rd][tid] = out;
+                    emit_trace(D + 3u, rd, out);
+                    ip = (ip + 1u) & 0xFFFFu; t = D + 4u;
+                }
+                break;
+            }
+            case 0x2:
+                ip = u.z & 0xFFFFu; t = D + 4u;
+                break;
+            case 0x3: {
+                const uint32_t out = alu_op(alu, in0(), reg(u.y >> 4));
+                ip = (out & 1u) ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                t = D + 6u;
+                break;
+            }
+            case 0x6: {
+                const uint32_t out = alu_op(alu, in0(), qclk(D));
+                qa_t = D + 3u; qa_q = out + 3u;
+                emit_trace(D + 3u, TRACE_QCLK_LOAD, out + 3u);
+                ip = (ip + 1u) & 0xFFFFu; t = D + 4u;
+                break;
+            }
+            case 0x7:
+                if constexpr (SYNC) { mode = M_SYNC; wait_d = D; }
+                else { finish(ST_DEADLOCK, D); }   // not reached: host selects SYNC kernels
+                break;
+            case 0x4: case 0x5: {
+                const uint32_t id = (u.z >> 16) & 0xFFu;
+                bool have = false;
+                uint32_t R = 0, data = 0;
+                if constexpr (XMEAS) {
+                    if (p.fproc_mode == 0u) {
+                        R = D + 2u;
+                        data = meas_lookup(leader_tid + (id & (C - 1)), D);
+                        have = true;
+                    } else if (id == 0u) {
+                        // core_state_mgr WAIT_MEAS: first own meas_valid at >= D + 1
+#pragma unroll
+                        for (int m = MT - 1; m >= 0; m--) {
+                            const uint32_t e = s_mt[m][tid];
+                            if (e != INF32 && (e >> 1) >= D + 1u) { R = e >> 1; data = e & 1u; have = true; }
+                        }
+                        if (!have) { finish(ST_DEADLOCK, D); }
+                    } else {
+                        mode = M_LUT; wait_d = D;
+                    }
+                } else {
+                    finish(ST_DEADLOCK, D);          // not reached: host selects FPROC kernels
+                }
+                if (have) {
+                    if (R > p.max_cycles) finish(ST_MAX_CYCLES, D);
+                    else {
+                        const uint32_t out = alu_op(alu, in0(), data);
+                        if (op == 4u) {
+                            const uint32_t rd = (u.y >> 8) & 15u;
+                            s_regs[rd][tid] = out;
+                            emit_trace(R + 3u, rd, out);
+                            ip = (ip + 1u) & 0xFFFFu; t = R + 4u;
+                        } else {
+                            ip = (out & 1u) ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                            t = R + 6u;
+                        }
+                    }
+                }
+                break;
+            }
+            default:                                     // 0xD-0xF: hang in DECODE
+                finish(ST_HUNG_OPCODE, D);
+                break;
+            }
+        };
+
+        // ---------------- fast path: one opcode for the whole wave ----------------
+        // Every live lane runs and all fetched the same opcode (the batched-
+        // experiment shape: one program structure, per-core / per-group
+        // parameters): no lane waits in a barrier or on the LUT, so the
+        // cross-core phase reduces to the fproc bound, and a scalar switch runs
+        // only that opcode's semantics.
+        if constexpr (!LUT && !STRAIGHT) {
+            const uint64_t run_m = __ballot(run);
+            if (run_m) {
+                const uint32_t op_u = __builtin_amdgcn_readlane(op4, (int)__builtin_ctzll(run_m));
+                if (!__ballot(mode != M_FIN && !(run && op4 == op_u))) {
+                    uint32_t gmin = INF32;
+                    if (op_u == 4u || op_u == 5u) gmin = group_reduce<0>(run ? t + 2u : INF32, C);
+                    if (run && !fproc_stall(gmin)) retire(op_u);
+                    if constexpr (FPROC || XMEAS) wave_fence();
+                    continue;
+                }
+            }
+        }
 
         // ---------------- cross-core phase (converged) ----------------
         uint32_t gmin = INF32;
@@ -262,15 +417,16 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
             if constexpr (LUT) any_run_grp = group_bits(__ballot(mode == M_RUN), wl, C) != 0ull;
         }
 
-        // ---------------- execute ----------------
+        // ---------------- execute (any opcode per lane) ----------------
         bool executed = false;
         if constexpr (STRAIGHT) {
             // pulse / idle / pulse_reset / done / hang only: the timing of ctrl.v in
-            // closed form with few state merges (the generic switch below costs ~2x
+            // closed form with few state merges (the generic switch costs ~2x
             // the VALU instructions per command)
             if (run) {
                 n_exec++;
                 const uint32_t D = t;
+                const uint32_t qD = (D < qa_t) ? 0u : qa_q + (D - qa_t);
                 const bool pw = op4 == 0x8u || op4 == 0x9u;
                 const bool waits = op4 == 0x9u || op4 == 0xCu;
                 const bool pulse_cls = pw || op4 == 0xBu || op4 == 0xCu;
@@ -301,135 +457,9 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                     t = tT + 3u;
                 }
             }
-        } else if (run) {
-            bool stall = false;
-            if constexpr (FPROC) {
-                // fproc_meas read at D = t needs every meas_valid <= D known
-                if (is_fproc && p.fproc_mode == 0u) {
-                    const uint64_t h = (uint64_t)gmin + p.meas_latency;
-                    stall = !(h > (uint64_t)t);
-                }
-            }
-            if (!stall) {
-                executed = true;
-                n_exec++;
-                const uint32_t D = t;
-                switch (STRAIGHT && op4 >= 0x1 && op4 <= 0x7 ? 0xFu : op4) {   // not reached if STRAIGHT
-                case 0x0: case 0xA:
-                    finish(ST_DONE, D);
-                    break;
-                case 0xD: case 0xE: case 0xF:
-                    finish(ST_HUNG_OPCODE, D);
-                    break;
-                case 0xB:
-                    emit_event(D, 1u);
-                    ip = (ip + 1u) & 0xFFFFu; t = D + 3u;
-                    break;
-                case 0x8: case 0x9: case 0xC: {
-                    bool go = true;
-                    uint32_t tT = D;
-                    bool dbl = false;
-                    if (op4 != 0x8) {
-                        const uint32_t T = u.x;
-                        uint64_t wait;
-                        if (D < qa_t) { dbl = (T == 0u); wait = dbl ? 0ull : (uint64_t)(qa_t - D) + (uint32_t)(T - qa_q); }
-                        else wait = (uint32_t)(T - qD);
-                        if (wait >= 0x80000000ull) flags |= F_LATE;
-                        if (wait > (uint64_t)(p.max_cycles - D)) { finish(ST_MAX_CYCLES, D); go = false; }
-                        else tT = D + (uint32_t)wait;
-                    }
-                    if (go && op4 != 0xC) {
-                        // pulse_reg.sv:59-97: immediates, then reg[rs0] into register-sourced fields
-                        pulse_write(u, pe, pp, pa);
-                        if (u.w & UOP_ANY_RS) {
-                            if (u.w & UOP_RS_ENV) pe |= reg0 & 0xFFFFFFu;
-                            if (u.w & UOP_RS_PH) pp |= reg0 & 0x1FFFFu;
-                            if (u.w & UOP_RS_FR) pp |= (reg0 & 0x1FFu) << 17;
-                            if (u.w & UOP_RS_AMP) pa = reg0 & 0xFFFFu;
-                        }
-                    }
-                    if (go) {
-                        if (op4 == 0x9) {
-                            emit_event(tT + 2u, 0u);
-                            if (dbl) { emit_event(tT + 3u, 0u); flags |= F_DOUBLE_STROBE; }
-                        }
-                        ip = (ip + 1u) & 0xFFFFu;
-                        t = tT + 3u;
-                    }
-                    break;
-                }
-                case 0x1: {
-                    const uint32_t out = alu_op(alu, in0, reg1);
-                    const uint32_t rd = (u.y >> 8) & 15u;
-                    s_regs[rd][tid] = out;
-                    emit_trace(D + 3u, rd, out);
-                    ip = (ip + 1u) & 0xFFFFu; t = D + 4u;
-                    break;
-                }
-                case 0x2:
-                    ip = u.z & 0xFFFFu; t = D + 4u;
-                    break;
-                case 0x3: {
-                    const uint32_t out = alu_op(alu, in0, reg1);
-                    ip = (out & 1u) ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
-                    t = D + 6u;
-                    break;
-                }
-                case 0x6: {
-                    const uint32_t out = alu_op(alu, in0, qD);
-                    qa_t = D + 3u; qa_q = out + 3u;
-                    emit_trace(D + 3u, TRACE_QCLK_LOAD, out + 3u);
-                    ip = (ip + 1u) & 0xFFFFu; t = D + 4u;
-                    break;
-                }
-                case 0x7:
-                    if constexpr (SYNC) { mode = M_SYNC; wait_d = D; }
-                    else { finish(ST_DEADLOCK, D); }   // not reached: host selects SYNC kernels
-                    break;
-                case 0x4: case 0x5: {
-                    const uint32_t id = (u.z >> 16) & 0xFFu;
-                    bool have = false;
-                    uint32_t R = 0, data = 0;
-                    if constexpr (XMEAS) {
-                        if (p.fproc_mode == 0u) {
-                            R = D + 2u;
-                            data = meas_lookup(leader_tid + (id & (C - 1)), D);
-                            have = true;
-                        } else if (id == 0u) {
-                            // core_state_mgr WAIT_MEAS: first own meas_valid at >= D + 1
-#pragma unroll
-                            for (int m = MT - 1; m >= 0; m--) {
-                                const uint32_t e = s_mt[m][tid];
-                                if (e != INF32 && (e >> 1) >= D + 1u) { R = e >> 1; data = e & 1u; have = true; }
-                            }
-                            if (!have) { finish(ST_DEADLOCK, D); }
-                        } else {
-                            mode = M_LUT; wait_d = D;
-                        }
-                    } else {
-                        finish(ST_DEADLOCK, D);          // not reached: host selects FPROC kernels
-                    }
-                    if (have) {
-                        if (R > p.max_cycles) finish(ST_MAX_CYCLES, D);
-                        else {
-                            const uint32_t out = alu_op(alu, in0, data);
-                            if (op4 == 4u) {
-                                const uint32_t rd = (u.y >> 8) & 15u;
-                                s_regs[rd][tid] = out;
-                                emit_trace(R + 3u, rd, out);
-                                ip = (ip + 1u) & 0xFFFFu; t = R + 4u;
-                            } else {
-                                ip = (out & 1u) ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
-                                t = R + 6u;
-                            }
-                        }
-                    }
-                    break;
-                }
-                default:
-                    break;
-                }
-            }
+        } else if (run && !fproc_stall(gmin)) {
+            executed = true;
+            retire(op4);
         }
 
         // ---------------- meas_lut (per shot, by the shot's leader lane) ----------------

@@ -143,6 +143,8 @@ hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
 enum { STRAIGHT_ROWS = 0, STRAIGHT_PROG = 1, STRAIGHT_LDS = 2 };
 constexpr uint32_t STRAIGHT_LDS_MAX = 9216;   // commands (144 KiB) of dynamic LDS per workgroup
 hipError_t launch_straight(const KParams &p, int src, int fb, hipStream_t stream);
+// programs with jumps / fproc_meas / sync (branch.hip): FEAT_FPROC | FEAT_SYNC bits of feat
+hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream);
 // branch-free programs with reg_alu / inc_qclk (macro.hip)
 hipError_t launch_macro(const KParams &p, hipStream_t stream);
 constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no command; ALU ctl bit 31: present

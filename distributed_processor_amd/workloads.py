@@ -147,8 +147,9 @@ def config2_ramsey(n_cores=8, n_points=100, tau_step=4):
 HOLD_CLKS = 64    # hwconfig.FPROC_MEAS_CLKS: idle after the readout window
 
 
-def config3_active_reset(n_cores=8):
-    """sync; read; hold; if (1 == meas) X90 X90; sync; read; done."""
+def config3_active_reset(n_cores=8, extra_pulses=0):
+    """sync; read; hold; if (1 == meas) X90 X90; sync; read; done.
+    extra_pulses: that many X90s after the second readout (per-command cost probes)."""
     prog = {}
     for c in range(n_cores):
         q = qubit_params(c)
@@ -166,7 +167,9 @@ def config3_active_reset(n_cores=8):
         b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t1 + X90_CLKS)
         b.words[jf] = isa.alu_cmd('jump_fproc', 'i', 1, 'eq', jump_cmd_ptr=jf + 2, func_id=c)
         b.emit(isa.sync(1))
-        readout(b, q, 10)
+        t_x = readout(b, q, 10)
+        for k in range(extra_pulses):
+            b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t_x + k * X90_CLKS)
         b.emit(isa.done_cmd())
         prog[str(c)] = b.assembled()
     return prog
