@@ -59,14 +59,21 @@ __device__ __forceinline__ uint32_t alu_eval(uint32_t op, uint32_t a, uint32_t b
     return r;
 }
 
-// group reductions over the C adjacent lanes of a shot (all lanes converged)
+// group reductions over the C adjacent lanes of a shot (all lanes converged):
+// DPP within a row of 16 lanes (quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror and row_mirror: each step pairs every lane with one of the
+// other half of its group), cross-lane permutes above 16
 template <int OP>   // 0 = min, 1 = max
 __device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t C)
 {
-    for (uint32_t m = 1; m < C; m <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)m, 64);
-        v = OP == 0 ? (o < v ? o : v) : (o > v ? o : v);
-    }
+    auto comb = [](uint32_t a, uint32_t b) { return OP == 0 ? (a < b ? a : b) : (a > b ? a : b); };
+#define DPP(x, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x), (ctrl), 0xF, 0xF, false))
+    if (C >= 2) v = comb(v, DPP(v, 0xB1));
+    if (C >= 4) v = comb(v, DPP(v, 0x4E));
+    if (C >= 8) v = comb(v, DPP(v, 0x141));
+    if (C >= 16) v = comb(v, DPP(v, 0x140));
+#undef DPP
+    for (uint32_t m = 16; m < C; m <<= 1) v = comb(v, (uint32_t)__shfl_xor((int)v, (int)m, 64));
     return v;
 }
 
@@ -77,11 +84,19 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 {
     constexpr bool FPROC = (FEAT & FEAT_FPROC) != 0;
     constexpr bool SYNC = (FEAT & FEAT_SYNC) != 0;
+    constexpr bool REGS = (FEAT & FEAT_REGS) != 0;  // some command writes the reg_file (else it reads 0)
+    constexpr bool PLDS = (FEAT & FEAT_PROG_LDS) != 0;   // the workgroup's programs staged in LDS
     constexpr int MT = FPROC ? MEAS_LOOKUP : 1;
 
-    __shared__ uint32_t s_regs[16][BLOCK];
+    __shared__ uint32_t s_regs[REGS ? 16 : 1][REGS ? BLOCK : 1];
     __shared__ uint32_t s_mt[MT][BLOCK];              // measurements {valid cycle << 1 | bit}, readable by the shot
-    __shared__ uint32_t s_hist[HIST_LDS_MAX];
+    __shared__ uint32_t s_pref[PLDS ? BLOCK + 1 : 1];
+    __shared__ uint32_t s_scan[BLOCK / 64];
+    // dynamic LDS: the staged programs (prog_lds_words commands), then the
+    // histogram pre-aggregation bins when hist_lds
+    extern __shared__ uint4 s_dyn[];
+    uint4 *const s_prog = s_dyn;
+    uint32_t *const s_hist = reinterpret_cast<uint32_t *>(s_dyn + (PLDS ? p.prog_lds_words : 0u));
 
     const uint32_t tid = threadIdx.x;
     const uint32_t C = p.C;
@@ -105,15 +120,21 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // command k of this lane's program, zero (DONE) past its end, in bounds for
     // any k: the program-major image has a zero guard after every program, the
     // command-major copy zeros past each program's end and a guard row
-    const bool cmd_major = p.fetch_stride != 1u;
+    if constexpr (PLDS) {
+        const uint32_t b = stage_programs(p, s_prog, s_pref, s_scan, spos, core);
+        if (valid) base = b;
+    }
+    const bool cmd_major = !PLDS && p.fetch_stride != 1u;
     const uint32_t fetch_off = cmd_major ? prog : base, k_max = cmd_major ? p.max_len : nprog;
     const uint32_t thr_core = valid ? p.p1_thr[core] : 0u;
     if (p.hist_lds) {
         for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
         __syncthreads();
     }
+    if constexpr (REGS) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
+        for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
+    }
     if constexpr (FPROC) {
 #pragma unroll
         for (int m = 0; m < MT; m++) s_mt[m][tid] = INF32;
@@ -174,8 +195,15 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // sync barrier keys: a participant's SYNC decode while it waits, its next
     // decode while it runs (a lower bound of its arrival), INF once finished
     auto sync_maxkey = [&]() -> uint32_t {
-        const uint32_t key = is_part ? ((mode == B_SYNC) ? wait_d : (mode == B_RUN) ? t : INF32) : 0u;
-        return group_reduce<1>(key, C);
+        uint32_t key = mode == B_SYNC ? wait_d : t;
+        key = mode == B_FIN ? INF32 : key;
+        return group_reduce<1>(is_part ? key : 0u, C);
+    };
+
+    // reg_file read (hdl/reg_file.v): all zero while no command writes it
+    auto reg = [&](uint32_t r) __attribute__((always_inline)) -> uint32_t {
+        if constexpr (REGS) return s_regs[r & 15u][tid];
+        return 0u;
     };
 
     auto finish = [&](bool stop, uint32_t st, uint32_t at) __attribute__((always_inline)) {
@@ -192,7 +220,8 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         // max_cycles at decode
         finish(mode == B_RUN && t > max_cycles, ST_MAX_CYCLES, t);
         const bool run = mode == B_RUN;
-        const uint4 u = p.fetch[(uint64_t)min(ip, k_max) * p.fetch_stride + fetch_off];
+        const uint4 u = PLDS ? s_prog[fetch_off + min(ip, k_max)]
+                             : p.fetch[(uint64_t)min(ip, k_max) * p.fetch_stride + fetch_off];
         const uint32_t op = u.y >> 28;
 
         // ---- fproc_meas bound (FPROC): a read at D needs every meas_valid <= D
@@ -218,11 +247,13 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         // qclk at this decode (0 in the reset hold)
         const uint32_t qD = FIRST ? 0u : D + qoff;
 
-        // ---- pulse-class and terminal commands (0, 8-F): one branch-free datapath ----
+        // ---- the commands that need no ALU: one branch-free datapath ----
         // pulse write / trigger, idle, pulse reset (ctrl.v: D + 3, or tT + 3
-        // after the cmd_time wait), done, hang.  The commands between a
-        // program's syncs and branches are almost all of this class.
-        const bool pcls = (0xFF01u >> op) & 1u;
+        // after the cmd_time wait), jump_i (D + 4), sync (waits for the
+        // barrier), done, hang -- almost every command of a program between
+        // its measurement-conditioned branches.
+        constexpr uint32_t FAST = 0xFF05u | (SYNC ? 0x80u : 0u);   // 0, 2, (7,) 8-F
+        const bool pcls = (FAST >> op) & 1u;
         {
             const bool pg = go && pcls;
             const bool waits = (0x1200u >> op) & 1u;    // 9: pulse trigger, C: idle
@@ -238,13 +269,15 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             const bool late = waits && (big || wait >= 0x80000000u);
             const bool over = waits && (big || wait > max_cycles - D);
             const uint32_t tT = D + (waits ? wait : 0u);
-            const bool cont = pg && ((0x1B00u >> op) & 1u) && !over;   // 8, 9, B, C in the budget
+            const bool jmp = op == 2u;
+            const bool to_sync = SYNC && pg && op == 7u;
+            const bool cont = pg && (((0x1B04u >> op) & 1u) != 0u) && !over;   // 2, 8, 9, B, C in the budget
             // pulse_reg.sv:59-97 (write enables are zero except for 8 / 9):
             // immediates, then reg[rs0] into register-sourced fields
             uint32_t pe2 = pe, pp2 = pp, pa2 = pa;
             pulse_write(u, pe2, pp2, pa2);
             if (cont && (u.w & UOP_ANY_RS)) {
-                const uint32_t r0 = s_regs[(u.w >> 20) & 15u][tid];
+                const uint32_t r0 = reg(u.w >> 20);
                 if (u.w & UOP_RS_ENV) pe2 |= r0 & 0xFFFFFFu;
                 if (u.w & UOP_RS_PH) pp2 |= r0 & 0x1FFFFu;
                 if (u.w & UOP_RS_FR) pp2 |= (r0 & 0x1FFu) << 17;
@@ -263,17 +296,19 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
                 flags |= two ? F_DOUBLE_STROBE : 0u;
             }
             flags |= (pg && late) ? F_LATE : 0u;
-            if (__any(pg && !cont))
-                finish(pg && !cont, over ? ST_MAX_CYCLES : op >= 0xDu ? ST_HUNG_OPCODE : ST_DONE, D);
-            ip = cont ? ((ip + 1u) & 0xFFFFu) : ip;
-            t = cont ? tT + 3u : t;
+            if (__any(pg && !cont && !to_sync))
+                finish(pg && !cont && !to_sync, over ? ST_MAX_CYCLES : op >= 0xDu ? ST_HUNG_OPCODE : ST_DONE, D);
+            wait_d = to_sync ? D : wait_d;
+            mode = to_sync ? B_SYNC : mode;
+            ip = cont ? (jmp ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu)) : ip;
+            t = cont ? (jmp ? D + 4u : tT + 3u) : t;
         }
-        // ---- register, jump, fproc and sync commands (1-7) ----
+        // ---- reg_alu, jump_cond, alu_fproc / jump_fproc, inc_qclk (1, 3-6) ----
         if (__any(go && !pcls)) {
             const bool sg = go && !pcls;
             const bool is_fp = op == 4u || op == 5u;
-            const uint32_t reg0 = s_regs[(u.w >> 20) & 15u][tid];
-            const uint32_t reg1 = s_regs[(u.y >> 4) & 15u][tid];
+            const uint32_t reg0 = reg(u.w >> 20);
+            const uint32_t reg1 = reg(u.y >> 4);
             uint32_t data = 0;
             const uint32_t R = D + 2u;                   // fproc_meas.sv:18-35: ready two cycles after the read
             if constexpr (FPROC) {
@@ -295,7 +330,9 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             const uint32_t ip_next = take ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
             // reg_file write (reg_alu, alu_fproc) and the register / qclk trace
             const bool wr = cont && (op == 1u || op == 4u);
-            if (wr) s_regs[(u.y >> 8) & 15u][tid] = out;
+            if constexpr (REGS) {
+                if (wr) s_regs[(u.y >> 8) & 15u][tid] = out;
+            }
             const bool inc = cont && op == 6u;
             emit_trace(wr || inc, (op == 4u ? R : D) + 3u, inc ? TRACE_QCLK_LOAD : (u.y >> 8) & 15u,
                        inc ? out + 3u : out);
@@ -355,23 +392,32 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     }
     if (valid && p.regs_out) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = s_regs[r][tid];
+        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = reg(r);
     }
     count_outcome(p, s_hist, valid, core, grp, last_bit);
+}
+
+template <int F>
+static hipError_t launch_f(const KParams &p, uint32_t blocks, hipStream_t stream)
+{
+    const size_t shmem = ((F & FEAT_PROG_LDS) ? (size_t)p.prog_lds_words * sizeof(uint4) : 0) +
+                         (p.hist_lds ? HIST_LDS_MAX * sizeof(uint32_t) : 0);
+    hipLaunchKernelGGL(branch_kernel<F>, dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    return hipGetLastError();
 }
 
 hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
     if (blocks == 0) return hipSuccess;
-    switch (feat & (FEAT_FPROC | FEAT_SYNC)) {
-    case 0: hipLaunchKernelGGL(branch_kernel<0>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
-    case FEAT_FPROC: hipLaunchKernelGGL(branch_kernel<FEAT_FPROC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
-    case FEAT_SYNC: hipLaunchKernelGGL(branch_kernel<FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p); break;
-    default:
-        hipLaunchKernelGGL(branch_kernel<FEAT_FPROC | FEAT_SYNC>, dim3(blocks), dim3(BLOCK), 0, stream, p);
+    switch (feat & (FEAT_FPROC | FEAT_SYNC | FEAT_REGS | FEAT_PROG_LDS)) {
+#define CASE(F) case F: return launch_f<F>(p, blocks, stream);
+#define CASES(L) CASE(L) CASE(L | FEAT_FPROC) CASE(L | FEAT_SYNC) CASE(L | FEAT_FPROC | FEAT_SYNC)
+    CASES(0) CASES(FEAT_REGS) CASES(FEAT_PROG_LDS) CASES(FEAT_REGS | FEAT_PROG_LDS)
+#undef CASES
+#undef CASE
     }
-    return hipGetLastError();
+    return hipErrorInvalidValue;
 }
 
 }  // namespace dpemu

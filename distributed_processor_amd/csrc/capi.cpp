@@ -31,7 +31,7 @@ struct dpemu_ctx {
     uint32_t *d_moff = nullptr;             // its per-program offsets (in macros)
     uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
     uint32_t n_programs = 0, n_groups = 0, C = 0;
-    bool has_fproc = false, has_sync = false, straight = false, linear = false;
+    bool has_fproc = false, has_sync = false, straight = false, linear = false, reg_writes = false;
     uint32_t max_len = 0;              // longest program (commands)
     std::vector<uint64_t> group_len;   // instructions of all C programs of each group
     // run constants
@@ -241,7 +241,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words,
     if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1)))
         return fail(ctx, DPEMU_E_INVALID, "cores_per_shot %u is not a power of two in [1, 64]", C);
     if ((uint64_t)n_groups * C > 0xFFFFFFFFull) return fail(ctx, DPEMU_E_INVALID, "n_groups * C exceeds 2^32");
-    bool fp = false, sy = false, straight = true, linear = true;
+    bool fp = false, sy = false, straight = true, linear = true, rw = false;
     for (uint32_t i = 0; i < n_programs; i++) {
         if (n_instr[i] > 65536u)
             return fail(ctx, DPEMU_E_INVALID, "program %u: %u commands exceed the 2^16-deep cmd_mem", i, n_instr[i]);
@@ -254,6 +254,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words,
             const uint32_t op4 = words[4 * ((uint64_t)offsets[i] + k) + 3] >> 28;
             fp |= (op4 == 4 || op4 == 5);
             sy |= (op4 == 7);
+            rw |= (op4 == 1 || op4 == 4);                  // reg_alu / alu_fproc write the reg_file
             straight &= !(op4 >= 1 && op4 <= 7);
             linear &= !(op4 >= 2 && op4 <= 5) && op4 != 7;     // no jump / fproc / sync: ip advances by 1
         }
@@ -317,6 +318,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words,
     ctx->has_sync = sy;
     ctx->straight = straight;
     ctx->linear = linear;
+    ctx->reg_writes = rw;
     ctx->max_len = max_len;
     ctx->group_len.assign(n_groups, 0);
     for (uint32_t g = 0; g < n_groups; g++)
@@ -506,16 +508,27 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             hist_stride = stride;
         }
     }
-    // the branch-free datapath (branch.hip) for every other program, except
-    // the meas_lut back end and LDS-staged programs, which the general
-    // interpreter runs (and DPEMU_X_GENERAL: everything on it)
-    const bool branch = !uniform && !macro && !(feat & (FEAT_LUT | FEAT_PROG_LDS)) &&
-                        !(cfg->exec_flags & DPEMU_X_GENERAL);
+    // branch.hip for every other program, except the meas_lut back end, which
+    // the general interpreter runs (and DPEMU_X_GENERAL / DPEMU_X_PROG_LDS:
+    // everything on it).  Its workgroup's programs are staged in LDS when
+    // they are few commands: a fetch from LDS does not wait behind the lane's
+    // event stores, which share vmcnt with global loads on gfx950
+    // (DPEMU_X_PROG_MAJOR keeps the global fetch).
+    const bool branch = !uniform && !macro && !(feat & FEAT_LUT) &&
+                        !(cfg->exec_flags & (DPEMU_X_GENERAL | DPEMU_X_PROG_LDS));
+    int bfeat = (feat & (FEAT_FPROC | FEAT_SYNC)) | (ctx->reg_writes ? FEAT_REGS : 0);
+    if (branch) {
+        p.prog_lds_words = 0;
+        if (footprint <= BRANCH_LDS_MAX && !(cfg->exec_flags & DPEMU_X_PROG_MAJOR)) {
+            bfeat |= FEAT_PROG_LDS;
+            p.prog_lds_words = (uint32_t)std::max<uint64_t>(16, (footprint + 15) & ~15ull);
+        }
+    }
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
     else if (macro) HIPCHK(ctx, launch_macro(p, stream));
-    else if (branch) HIPCHK(ctx, launch_branch(p, feat, stream));
+    else if (branch) HIPCHK(ctx, launch_branch(p, bfeat, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, stream));
     {
@@ -526,7 +539,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
         else if (macro)
             snprintf(name, sizeof name, "macro_kernel");
         else if (branch)
-            snprintf(name, sizeof name, "branch_kernel<feat=0x%x>", feat & (FEAT_FPROC | FEAT_SYNC));
+            snprintf(name, sizeof name, "branch_kernel<feat=0x%x>", bfeat);
         else
             snprintf(name, sizeof name, "interp_kernel<feat=0x%x>", feat);
         ctx->last_kernel = name;

@@ -42,7 +42,9 @@ constexpr int FEAT_SYNC = 2;    // SYNC barriers
 constexpr int FEAT_LUT = 4;     // fproc_lut back end
 constexpr int FEAT_PROG_LDS = 8; // the workgroup's programs staged in LDS (fits PROG_LDS_MAX)
 constexpr int FEAT_STRAIGHT = 16; // only pulse / idle / done / hang opcodes: no register file
+constexpr int FEAT_REGS = 32;   // branch.hip: some command writes the reg_file (reg_alu / alu_fproc)
 constexpr uint32_t PROG_LDS_MAX = 1024;   // commands (16 KiB) of dynamic LDS per workgroup
+constexpr uint32_t BRANCH_LDS_MAX = 512;  // commands (8 KiB): branch.hip stages its programs up to this
 
 constexpr uint32_t ST_DONE = DPEMU_ST_DONE, ST_MAX_CYCLES = DPEMU_ST_MAX_CYCLES;
 constexpr uint32_t ST_HUNG_OPCODE = DPEMU_ST_HUNG_OPCODE, ST_DEADLOCK = DPEMU_ST_DEADLOCK;
@@ -143,7 +145,7 @@ hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
 enum { STRAIGHT_ROWS = 0, STRAIGHT_PROG = 1, STRAIGHT_LDS = 2 };
 constexpr uint32_t STRAIGHT_LDS_MAX = 9216;   // commands (144 KiB) of dynamic LDS per workgroup
 hipError_t launch_straight(const KParams &p, int src, int fb, hipStream_t stream);
-// programs with jumps / fproc_meas / sync (branch.hip): FEAT_FPROC | FEAT_SYNC bits of feat
+// programs with jumps / fproc_meas / sync (branch.hip): FEAT_FPROC | FEAT_SYNC | FEAT_REGS | FEAT_PROG_LDS bits of feat
 hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream);
 // branch-free programs with reg_alu / inc_qclk (macro.hip)
 hipError_t launch_macro(const KParams &p, hipStream_t stream);
