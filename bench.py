@@ -191,6 +191,33 @@ def kernel_pass(emu, steps, step, drain):
     return float(np.median(kt))
 
 
+def block_pass(launch, k):
+    """ms per launch of `k` back-to-back launches of one kernel between two
+    HIP events on the launch stream (torch's current stream): per-launch event
+    pairs add their own overhead to a 0.2-ms kernel, a block of k launches
+    only the k - 1 dependent-launch gaps"""
+    import torch
+    launch()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(k):
+        launch()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / k
+
+
+def interp_kernel_ms(emu, cfg, n, shot0, out, stream, steps, step, drain):
+    """the interpreter kernel's time per launch: a block of back-to-back
+    launches without the histogram (whose zeroing / reduction are separate
+    launches of the step), beside the per-launch event median"""
+    nohist = {k: v for k, v in out.items() if k != 'hist'}
+    ev = kernel_pass(emu, steps, step, drain)
+    blk = block_pass(lambda: emu.run_device(cfg, n, shot0, nohist, stream), max(steps, 10))
+    return blk, ev
+
+
 def fill_gbps(device='cuda'):
     """a torch fill of 1 GiB on this box (HIP events): the store rate the
     HBM roofline's 8 TB/s compares against, measured (boxes differ)"""
@@ -228,7 +255,7 @@ def leg_ramsey(emu, args, world, rank, stream):
         emu.run_device(cfg, n, shot0, out, stream)
     step = lambda: pipe.step(launch)
     dt = timed(step, pipe.drain, args.steps, args.warmup, world)
-    kernel_ms = kernel_pass(emu, args.steps, step, pipe.drain)
+    kernel_ms, kernel_ms_ev = interp_kernel_ms(emu, cfg, n, shot0, out, stream, args.steps, step, pipe.drain)
     kernel = emu.last_kernel()
     # accounting from the last step's outputs (identical every step)
     summ = out['summary'].cpu().numpy().view(np.uint32)
@@ -245,6 +272,7 @@ def leg_ramsey(emu, args, world, rank, stream):
     alg = float(bytes_per_lane(summ, cfg).sum())
     prof = pmc('ramsey')
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'straight_kernel')
+    roof['kernel_ms_events'] = kernel_ms_ev
     roof['valu'] = valu_view(prof)
     res = {'value': n * 8 * world * args.steps / dt, 'ms_per_step': ms_step,
            'shots_per_s': n * world * args.steps / dt,
@@ -338,7 +366,8 @@ def leg_active_reset(emu, args, world, rank, stream):
         emu.run_device(cfg, n, shot0, out, stream)
     step = lambda: pipe.step(launch)
     dt = timed(step, pipe.drain, args.steps, args.warmup, world)
-    kernel_ms = kernel_pass(emu, args.steps, step, pipe.drain)
+    kernel = emu.last_kernel()
+    kernel_ms, kernel_ms_ev = interp_kernel_ms(emu, cfg, n, shot0, out, stream, args.steps, step, pipe.drain)
     summ = out['summary'].cpu().numpy().view(np.uint32)
     s = _abi.unpack_summary(summ)
     assert (s['status'] == _abi.ST_DONE).all(), 'config 3: not every lane reached DONE'
@@ -346,7 +375,8 @@ def leg_active_reset(emu, args, world, rank, stream):
     alg = float(bytes_per_lane(summ, cfg).sum())
     prof = pmc('active_reset')
     ms_step = dt / args.steps * 1e3
-    roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + emu.last_kernel(), prof, 'interp_kernel')
+    roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'branch_kernel')
+    roof['kernel_ms_events'] = kernel_ms_ev
     roof['valu'] = valu_view(prof)
     res = {'metric': 'emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
                      '1.25e6 shots/GPU)',
@@ -395,7 +425,8 @@ def leg_rb(emu, args, world, rank, stream):
     step = lambda: pipe.step(launch)
     steps = max(1, args.steps // 4)
     dt = timed(step, pipe.drain, steps, min(args.warmup, 2), world)
-    kernel_ms = kernel_pass(emu, steps, step, pipe.drain)
+    kernel = emu.last_kernel()
+    kernel_ms, kernel_ms_ev = interp_kernel_ms(emu, cfg, n, shot0, out, stream, steps, step, pipe.drain)
     summ = out['summary'].cpu().numpy().view(np.uint32)
     s = _abi.unpack_summary(summ)
     assert (s['status'] == _abi.ST_DONE).all(), 'config 4: not every lane reached DONE'
@@ -405,7 +436,8 @@ def leg_rb(emu, args, world, rank, stream):
     k_ms = min(kernel_ms, ms_step)
     prof = pmc('rb')
     alg = float(bytes_per_lane(summ, cfg).sum())
-    hbm = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + emu.last_kernel(), prof, 'macro_kernel')
+    hbm = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'macro_kernel')
+    hbm['kernel_ms_events'] = kernel_ms_ev
     if prof and prof.get('SQ_INSTS_VALU'):
         valu_per_launch = float(prof['SQ_INSTS_VALU'])
         achieved = valu_per_launch / (k_ms * 1e-3)

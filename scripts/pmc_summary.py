@@ -25,9 +25,9 @@ import os
 import sys
 
 # summary key -> kernel-name substrings, one per bench leg: config 2 runs on
-# straight_kernel (pulse-only programs), config 3 on the general
-# interp_kernel, config 4 on macro_kernel, config 5 on dds_tile_kernel
-KERNELS = {'ramsey': ('straight_kernel',), 'active_reset': ('interp_kernel',), 'rb': ('macro_kernel',),
+# straight_kernel (pulse-only programs), config 3 on branch_kernel (fproc
+# branches, syncs), config 4 on macro_kernel, config 5 on dds_tile_kernel
+KERNELS = {'ramsey': ('straight_kernel',), 'active_reset': ('branch_kernel',), 'rb': ('macro_kernel',),
            'dds': ('dds_tile_kernel',), 'dds_index': ('dds_index_kernel',), 'hist_reduce': ('hist_reduce_kernel',)}
 
 
