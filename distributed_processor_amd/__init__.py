@@ -3,8 +3,8 @@
 Host side of the emulator: ISA encoder/decoder (``isa``), hardware-config
 plugins (``hwconfig``), and the ``Emulator`` front end that runs assembled
 distproc programs on hand-written CDNA4 HIP kernels through the C ABI in
-``include/dpemu.h``; upstream of it, the clean-room compiler scheduling
-stage (``schedule``) and assembler (``assembler``) that turn QubiC circuits
+``include/dpemu.h``; upstream of it, the restated compiler scheduling
+stage (``schedule``) and the API-compatible assembler (``assembler``) that turn QubiC circuits
 into that machine code.
 """
 

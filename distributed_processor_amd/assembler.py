@@ -1,6 +1,10 @@
-"""Clean-room distproc assembler: assembly-level program dicts -> machine code.
+"""API-compatible restatement of the distproc assembler: assembly-level
+program dicts -> machine code.
 
-The API surface is the reference's (``python/distproc/assembler.py``):
+The API surface, statement handling and error messages are the reference's
+(``python/distproc/assembler.py``), kept on purpose for drop-in and
+bug-for-bug parity; it is therefore a restatement
+that follows the reference's method structure, not a clean-room design:
 
 * ``SingleCoreAssembler(elem_cfgs)`` (``:62-541``) -- build one core's program
   from a list of statement dicts (``from_list``) or ``add_*`` calls;

@@ -5,25 +5,32 @@
 // one thread = one (shot, core) lane, a shot's C cores adjacent lanes of ONE
 // wavefront, each iteration retires at most one command per lane and
 // advances its next-DECODE cycle by hdl/ctrl.v's closed-form latency
-// (oracle/fast_model.c).  What differs is how a command retires: the general
-// interpreter dispatches on the opcode (a switch -- under divergence every
-// taken case runs -- whose cases write the loop-carried state on different
-// paths, which the register allocator pays for with copies of all of it on
-// every iteration); here every lane evaluates ONE branch-free datapath, like
-// the gateware does:
+// (oracle/fast_model.c).  What differs is how a command retires.  The
+// general interpreter dispatches on the opcode; under divergence every taken
+// case runs, and cases that write the loop-carried state on different paths
+// cost copies of all of it per iteration.  Here:
 //
-//   wait      = cmd_time - qclk(D)                    pulse trigger / idle
-//   alu_out   = alu(in0, reg[rs1] | qclk(D) | fproc)   alu.v:20-50
-//   next ip   = jump ? target : ip + 1                instr_ptr.v, proc.sv:124
-//   next D    = (tT | R | D) + latency(op)            ctrl.v, 4-bit table per opcode
+//   * the commands that need no ALU -- pulse write / trigger, idle, pulse
+//     reset, jump_i, sync, done, hang: almost every command of a branching
+//     program -- go through ONE branch-free datapath written once through
+//     selects:  wait = cmd_time - qclk(D), qclk(D) = D + qoff;  strobe at
+//     tT + 2;  next decode tT + 3 / D + 4;  next ip ip + 1 / target;
+//   * reg_alu, jump_cond, alu_fproc / jump_fproc, inc_qclk take a second
+//     datapath (alu.v:20-50, instr_ptr.v, proc.sv:124) under a wave-uniform
+//     guard, the fproc_meas lookup under its own;
+//   * the cross-core phases are wave-uniform and run only when needed: the
+//     fproc_meas bound before a read, the sync barrier AFTER the iteration's
+//     commands, so the last arrival releases it in the same iteration;
+//     group min / max are DPP within a row of 16 lanes;
+//   * the reset hold (qclk(0) = qclk(1) = 0, proc.sv:125-136) can only be
+//     seen by a lane's first decode: a peeled first iteration;
+//   * no register file when no command writes one (FEAT_REGS), and the
+//     workgroup's programs staged in LDS when they are short
+//     (FEAT_PROG_LDS: an LDS fetch does not wait behind the lane's event
+//     stores, which share vmcnt with global loads on gfx950).
 //
-// and writes its state once, through selects; branches guard only stores,
-// LDS writes, the measurement draw and the rare reset-hold arithmetic.
-// The cross-core phases are wave-uniform and only run when some lane needs
-// them: the fproc_meas bound before an fproc read, the sync barrier after
-// the iteration's commands (so the last arrival releases the barrier in the
-// same iteration).  The meas_lut back end (FEAT_LUT) and LDS-staged programs
-// stay on interp_kernel.
+// Branches guard only stores, LDS writes and the measurement draw.  The
+// meas_lut back end (FEAT_LUT) stays on interp_kernel.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>

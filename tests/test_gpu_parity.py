@@ -164,7 +164,7 @@ def test_config1_golden_program(emu, golden_dir):
 @pytest.mark.parametrize('name', ['test_fproc_hold', 'test_hw_virtualz_out', 'test_linear_compile_out',
                                   'test_multirst_cfg', 'test_multirst_fproc_res_cfg', 'test_pulse_compile_out',
                                   'test_simple_loop'])
-def test_clean_room_assembled_goldens(emu, name):
+def test_restated_assembler_goldens(emu, name):
     """the reference's compiler golden programs, assembled by this framework's
     clean-room GlobalAssembler (byte-identical to the reference's, see
     tests/test_assembler.py), run on the GPU against oracle_fast"""
