@@ -646,8 +646,8 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
         if (d[0] >= ch->n_lanes) return fail(ctx, DPEMU_E_INVALID, "channel %u: lane %u >= n_lanes", i, d[0]);
         if (d[2] < 1 || d[2] > 16) return fail(ctx, DPEMU_E_INVALID, "channel %u: spc %u not in [1, 16]", i, d[2]);
         if (d[3] < 1) return fail(ctx, DPEMU_E_INVALID, "channel %u: interp must be >= 1", i);
-        // staged words: (E, E') pairs for interp 1, (R, R') pairs of the freq entries
-        const uint32_t ew = d[3] == 1 ? 2 * d[5] : d[5], fw = 2 * d[7];
+        // staged words: (E, E') pairs for interp 1 (swizzled chunks), (R, R') pairs of the freq entries
+        const uint32_t ew = d[3] == 1 ? dds_env_pairs_words(d[5]) : d[5], fw = 2 * d[7];
         if (ew <= DDS_ENV_LDS_MAX) env_max = std::max(env_max, ew);
         if (fw <= DDS_FREQ_LDS_MAX) freq_max = std::max(freq_max, fw);
     }

@@ -11,17 +11,19 @@
 //     of the channel's element and its pulse_resets (time-sorted: a core emits
 //     them in time order) once, channel-contiguous, and writes every sample
 //     tile's window of them (the records a tile's samples can see);
-//   * dds_tile_kernel, grid (stripes, channels).  A channel's tiles (1,024
-//     samples: 4 per thread, one 16-B store each) go round-robin to its
-//     stripe workgroups, so at any time the stripes of a channel write
-//     ADJACENT tiles: the chip's store front is a few contiguous runs, as in
-//     a fill, rather than one run per workgroup (the store probe of round 1:
-//     fill-shaped writes 6.5-7.0 TB/s, 64-128 KiB per-workgroup chunks
-//     5.6-6.0).  A workgroup stages the half sine table, the channel's env /
-//     freq tables -- as (E, E') / (R, R') pairs for the Y-form products --
-//     its strobes and its tiles' windows in LDS, then sweeps with no global
-//     loads in the loop: on gfx950 stores count in vmcnt, so a load there
-//     would wait for the previous tile's stores.
+//   * dds_tile_kernel, grid (stripes, channels).  A channel's 1,024-sample
+//     tiles go round-robin to its stripe workgroups, so at any time the
+//     stripes of a channel write ADJACENT tiles.  A workgroup stages the
+//     quarter-wave sine table, the channel's env / freq tables -- as
+//     (E, E') / (R, R') pairs for the Y-form products, the env pairs in
+//     bank-swizzled chunks -- its strobes and its tiles' windows in LDS, then
+//     sweeps with no global loads in the loop (on gfx950 stores count in
+//     vmcnt, so a load there would wait for the previous tile's stores).
+//     At 16 samples per clock (the RFSoC rate) a lane makes one whole cycle
+//     per tile -- window search, record decode, theta and carrier once per
+//     16 samples -- and the wave's 4 KiB goes out through a 1-KiB LDS
+//     transpose as 1-KiB dense store instructions; at other rates a lane
+//     makes 4 consecutive samples (one 16-B store).
 // Channels whose sample rate or tables do not fit the quad sweep take the
 // generic per-sample sweep (the definition, sample by sample).
 
@@ -77,18 +79,20 @@ __device__ __forceinline__ Carrier carrier(const int16_t *lut, uint32_t theta, i
     return carrier_cs(lut[(idx + 1024) & 4095], lut[idx], amp);
 }
 
-// the Q15 table is exactly antisymmetric (sin[i + 2048] = -sin[i]: built from
-// the first quadrant, dpemu_dds_sin_lut), so the lean kernel stages half of it
-__device__ __forceinline__ int32_t lut_half(const int16_t *lut, uint32_t i)
+// the Q15 table is built from its first quadrant with exact symmetry
+// (dpemu_dds_sin_lut): sin[2048 - i] = sin[i], sin[i + 2048] = -sin[i], so
+// the tile kernel stages the quarter wave, entries 0..1024 (2 KiB of LDS)
+__device__ __forceinline__ int32_t lut_quarter(const int16_t *lut, uint32_t i)
 {
-    const int32_t v = lut[i & 2047u];
+    const uint32_t r = i & 1023u;
+    const int32_t v = lut[(i & 1024u) ? 1024u - r : r];
     return (i & 2048u) ? -v : v;
 }
 
-__device__ __forceinline__ Carrier carrier_half(const int16_t *lut, uint32_t theta, int32_t amp)
+__device__ __forceinline__ Carrier carrier_quarter(const int16_t *lut, uint32_t theta, int32_t amp)
 {
     const uint32_t idx = theta >> 20;
-    return carrier_cs(lut_half(lut, (idx + 1024) & 4095), lut_half(lut, idx), amp);
+    return carrier_cs(lut_quarter(lut, (idx + 1024) & 4095), lut_quarter(lut, idx), amp);
 }
 
 // a = symsat((a0 (x) R_k + 2^14) >> 15)
@@ -131,6 +135,15 @@ __device__ __forceinline__ void store4(uint32_t *out, uint32_t j0, uint32_t c_en
         for (int s = 0; s < 4 && j0 + s < c_end; s++) out[j0 + s] = v[s];
     }
 }
+
+// The interp-1 envelope is staged as (E, E') pairs, two pairs per 16-B chunk,
+// chunk c at physical chunk c ^ ((c >> 4) & 7).  The cycle sweep's lanes read
+// chunks 8 apart (16 samples = 8 chunks per cycle); unswizzled, the 16 lanes
+// of a ds_read_b128 pass would hit 2 bank groups (8-way conflicts), swizzled
+// they hit all 16 -- for any pulse start A.
+__device__ __forceinline__ uint32_t env_chunk(uint32_t c) { return c ^ ((c >> 4) & 7u); }
+// word index of pair q's E in that layout (E' at + 1)
+__device__ __forceinline__ uint32_t env_pair(uint32_t q) { return (env_chunk(q >> 1) << 2) | ((q & 1u) << 1); }
 
 // ---------------------------------------------------------------------------
 // Y-form complex products (the segment kernel and the chunk kernel's quad
@@ -236,6 +249,19 @@ __device__ __forceinline__ int window_find(const uint32_t *t, uint32_t lo, uint3
     return r < 0 ? -1 : (int)(lo - base) + r;
 }
 
+// the same over staged strobe records {t, ...} (windows hold 1-3 records)
+__device__ __forceinline__ int window_find_rec(const uint4 *rec, uint32_t lo, uint32_t count, uint32_t base,
+                                               uint32_t n)
+{
+    int a = 0, b = (int)count;                       // first index with t > n
+    const uint4 *r = rec + (lo - base);
+    while (a < b) {
+        const int mid = (a + b) >> 1;
+        if (r[mid].x <= n) a = mid + 1; else b = mid;
+    }
+    return a == 0 ? -1 : (int)(lo - base) + a - 1;
+}
+
 // ===========================================================================
 // Tile sweep.  Workgroup (stripe, ch) synthesises tiles stripe,
 // stripe + stripes, ... of channel ch.  Per tile a thread finds its pulse in
@@ -249,16 +275,16 @@ __device__ __forceinline__ int window_find(const uint32_t *t, uint32_t lo, uint3
 // ===========================================================================
 __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
 {
-    // dynamic LDS (dds_lds_bytes): half sine table | strobe records | strobe
-    // times | reset times | tile windows | env | freq
+    // dynamic LDS (dds_lds_bytes): quarter sine table | strobe records |
+    // reset times | tile windows | env | freq | store transpose
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     int16_t *s_lut = reinterpret_cast<int16_t *>(s_dyn);
-    uint4 *s_st = reinterpret_cast<uint4 *>(s_dyn + 4096);
-    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_st + p.ev_lds);
-    uint32_t *s_rs_t = s_st_t + p.ev_lds;
+    uint4 *s_st = reinterpret_cast<uint4 *>(s_dyn + DDS_LUT_BYTES);
+    uint32_t *s_rs_t = reinterpret_cast<uint32_t *>(s_st + p.ev_lds);
     uint4 *s_win = reinterpret_cast<uint4 *>(s_rs_t + p.ev_lds);
     uint32_t *s_env = reinterpret_cast<uint32_t *>(s_win + DDS_TILES_PER_STRIPE);
     uint32_t *s_freq = s_env + p.env_lds;
+    uint4 *s_xpose = reinterpret_cast<uint4 *>(s_freq + p.freq_lds);   // DDS_XPOSE_BYTES, 16-B aligned
 
     const uint32_t tid = threadIdx.x;
     const uint32_t ch = blockIdx.y, stripe = blockIdx.x, stripes = gridDim.x;
@@ -267,7 +293,7 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
     const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
     const uint32_t spc_sh = __ffs(spc) - 1, int_sh = __ffs(interp) - 1;
-    const bool staged = (interp == 1 ? 2 * env_len : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds;
+    const bool staged = (interp == 1 ? dds_env_pairs_words(env_len) : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds;
     const uint32_t n_t = (p.tiles - stripe + stripes - 1) / stripes;   // this stripe's tiles (<= DDS_TILES_PER_STRIPE)
     const uint4 *gwin = p.win + (uint64_t)ch * p.tiles;
     // the stripe's strobes / resets: from its first tile's window to its last's end
@@ -276,14 +302,15 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
     const uint32_t rs_lo = w_first.z, rs_n = w_last.z + w_last.w - rs_lo;
 
     // prologue: every global load of the workgroup up front
-    reinterpret_cast<uint4 *>(s_lut)[tid] = reinterpret_cast<const uint4 *>(p.sin_lut)[tid];   // 4 KiB = BLOCK x 16 B
+    if (tid < DDS_LUT_BYTES / 16)                                      // entries 0..1031 (1024 needed)
+        reinterpret_cast<uint4 *>(s_lut)[tid] = reinterpret_cast<const uint4 *>(p.sin_lut)[tid];
     bool bad = false;                       // a staged eq or rq is -32768: no Y form
     if (staged) {
         if (interp == 1) {
             for (uint32_t i = tid; i < env_len; i += BLOCK) {
                 const uint32_t e = p.env[env_off + i];
                 bad |= (e & 0xFFFFu) == 0x8000u;
-                reinterpret_cast<uint2 *>(s_env)[i] = make_uint2(e, neg_swap(e));
+                *reinterpret_cast<uint2 *>(s_env + env_pair(i)) = make_uint2(e, neg_swap(e));
             }
         } else {
             for (uint32_t i = tid; i < env_len; i += BLOCK) {
@@ -302,9 +329,7 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
     const uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds + st_lo;
     const uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds + rs_lo;
     for (uint32_t i = tid; i < st_n; i += BLOCK) {
-        const uint4 r = xs[i];
-        s_st[i] = r;
-        s_st_t[i] = r.x;
+        s_st[i] = xs[i];
     }
     for (uint32_t i = tid; i < rs_n; i += BLOCK) s_rs_t[i] = xr[i];
     if (tid < n_t) s_win[tid] = gwin[stripe + tid * stripes];
@@ -312,6 +337,109 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
 
     uint32_t *out = p.iq + (uint64_t)ch * p.n_samples;
     const bool quad = staged && !bad && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
+    if (quad && spc == 16u) {
+        // ---- cycle sweep (16 samples / clk, the RFSoC rate): a lane makes one
+        // whole cycle, so the window search, record decode, theta and carrier
+        // are done once per 16 samples; wave w takes the stripe's tiles w, w + 4, ...
+        const uint32_t wv = tid >> 6, ln = tid & 63u;
+        for (uint32_t i = wv; i < n_t; i += BLOCK / 64) {
+            const uint32_t n = (stripe + i * stripes) * (DDS_TILE / 16) + ln;   // this lane's cycle
+            const uint32_t j0 = 16 * n;
+            const uint4 w = s_win[i];
+            uint32_t v[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) v[q] = 0u;
+            const int si = j0 < p.n_samples ? window_find_rec(s_st, w.x, w.y, st_lo, n) : -1;
+            if (si >= 0) {
+                const uint4 rec = s_st[si];                          // {t, env word, phase | freq << 17, amp}
+                const uint32_t A = rec.y & 0xFFFu, L = (rec.y >> 12) & 0xFFFu, fi = rec.z >> 17;
+                const uint32_t room = env_len > 4 * A ? env_len - 4 * A : 0u;
+                uint32_t lim, emask;
+                if (L) {
+                    emask = 0xFFFFFFFFu;
+                    const uint32_t n_env = min(4 * L, room);
+                    lim = n_env << int_sh;
+                    if ((lim >> int_sh) != n_env) lim = 0xFFFFFFFFu;
+                } else {
+                    emask = 0u;
+                    lim = room ? 0xFFFFFFFFu : 0u;
+                }
+                const uint32_t d0 = 16 * (n - rec.x);                // samples since the strobe's first
+                if (16 * fi + 15 < freq_len && d0 < lim) {
+                    const int ri = window_find(s_rs_t, w.z, w.w, rs_lo, n);
+                    const uint32_t t_ref = ri >= 0 ? s_rs_t[ri] : 0u;
+                    const uint32_t *frp = s_freq + 32 * fi;          // (R, R') pairs; pair 0 = (F0, 0)
+                    const uint32_t idx = (frp[0] * (n - t_ref) + ((rec.z & 0x1FFFFu) << 15)) >> 20;
+                    const int32_t c = lut_quarter(s_lut, (idx + 1024) & 4095), sn = lut_quarter(s_lut, idx);
+                    const int32_t a16 = (int32_t)(rec.w & 0xFFFFu);
+                    const uint32_t y0 = pack16((c * a16 + (1 << 15)) >> 16, (sn * a16 + (1 << 15)) >> 16);
+                    const bool inside = d0 + 15 < lim && emask;
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        uint32_t R[4], Rp[4], E[4], Ep[4];
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            const uint4 rw = *reinterpret_cast<const uint4 *>(frp + 8 * g + 4 * h);
+                            R[2 * h] = rw.x; Rp[2 * h] = rw.y; R[2 * h + 1] = rw.z; Rp[2 * h + 1] = rw.w;
+                        }
+                        if (interp == 1) {
+                            if (inside) {
+#pragma unroll
+                                for (int h = 0; h < 2; h++) {
+                                    const uint4 ew = *reinterpret_cast<const uint4 *>(
+                                        s_env + 4 * env_chunk(2 * A + (d0 >> 1) + 2 * g + h));
+                                    E[2 * h] = ew.x; Ep[2 * h] = ew.y; E[2 * h + 1] = ew.z; Ep[2 * h + 1] = ew.w;
+                                }
+                            } else {
+#pragma unroll
+                                for (int s2 = 0; s2 < 4; s2++) {
+                                    const uint32_t d = d0 + 4 * g + s2;
+                                    const uint32_t wi = env_pair(4 * A + (d & emask));
+                                    E[s2] = d < lim ? s_env[wi] : 0u;
+                                    Ep[s2] = d < lim ? s_env[wi + 1] : 0u;
+                                }
+                            }
+                        } else {                                     // interp >= 4: one env word for 4 samples
+                            const uint32_t e = s_env[4 * A + (((d0 + 4 * g) >> int_sh) & emask)], ep = neg_swap(e);
+#pragma unroll
+                            for (int s2 = 0; s2 < 4; s2++) { E[s2] = e; Ep[s2] = ep; }
+                        }
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; s2++) {
+                            const uint32_t y = (g == 0 && s2 == 0) ? y0 : rot_y(y0, R[s2], Rp[s2]);
+                            v[4 * g + s2] = d0 + 4 * g + s2 < lim ? mix_y(E[s2], Ep[s2], y) : 0u;
+                        }
+                    }
+                }
+            }
+            // transpose through the wave's 1-KiB LDS slice so every store
+            // instruction writes 1 KiB dense (lane-per-cycle stores would be 64 B
+            // apart): round r, lanes 16 r .. 16 r + 15 put their 4 chunks
+            // (lane l's chunk q at slot 4 (l & 15) + (q ^ (l >> 2 & 3)):
+            // conflict-free both ways), every lane takes one chunk and stores
+            uint4 *xp = s_xpose + 64 * wv;
+            const uint32_t tb = (stripe + i * stripes) * DDS_TILE;      // the tile's first sample
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                if ((ln >> 4) == (uint32_t)r) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        xp[4 * (ln & 15u) + (q ^ ((ln >> 2) & 3u))] =
+                            make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t lc = ln >> 2;                            // source lane 16 r + lc
+                const uint4 x = xp[4 * lc + ((ln & 3u) ^ ((lc >> 2) & 3u))];
+                const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+                store4(out, tb + 4 * (64u * r + ln), p.n_samples, w4);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the next writes
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        return;
+    }
     const uint32_t k0 = (4 * tid) & (spc - 1);     // sub-sample slot: fixed (the tile is a multiple of spc)
     for (uint32_t i = 0; i < n_t; i++) {
         const uint32_t j0 = (stripe + i * stripes) * DDS_TILE + 4 * tid;
@@ -320,7 +448,7 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
         uint32_t v[4] = {0u, 0u, 0u, 0u};
         if (quad) {
             const uint32_t n = j0 >> spc_sh;                         // the thread's 4 samples share cycle n
-            const int si = window_find(s_st_t, w.x, w.y, st_lo, n);
+            const int si = window_find_rec(s_st, w.x, w.y, st_lo, n);
             if (si >= 0) {
                 const uint4 rec = s_st[si];                          // {t, env word, phase | freq << 17, amp}
                 const uint32_t A = rec.y & 0xFFFu, L = (rec.y >> 12) & 0xFFFu, fi = rec.z >> 17;
@@ -344,7 +472,7 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                     const uint32_t t_ref = ri >= 0 ? s_rs_t[ri] : 0u;
                     const uint32_t *frp = s_freq + 32 * fi;          // (R, R') pairs; pair 0 = (F0, 0)
                     const uint32_t idx = (frp[0] * (n - t_ref) + ((rec.z & 0x1FFFFu) << 15)) >> 20;
-                    const int32_t c = lut_half(s_lut, (idx + 1024) & 4095), sn = lut_half(s_lut, idx);
+                    const int32_t c = lut_quarter(s_lut, (idx + 1024) & 4095), sn = lut_quarter(s_lut, idx);
                     const int32_t a16 = (int32_t)(rec.w & 0xFFFFu);
                     const uint32_t y0 = pack16((c * a16 + (1 << 15)) >> 16, (sn * a16 + (1 << 15)) >> 16);
                     uint32_t R[4], Rp[4], E[4], Ep[4];
@@ -355,19 +483,20 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                     }
                     const bool inside = d0 + 3 < lim;
                     if (interp == 1) {
-                        const uint32_t *envp = s_env + 8 * A;            // (E, E') pairs
+                        // (E, E') pairs, swizzled chunks (env_pair); pair 4A + d
                         if (inside && emask) {
 #pragma unroll
                             for (int h = 0; h < 2; h++) {
-                                const uint4 ew = *reinterpret_cast<const uint4 *>(envp + 2 * d0 + 4 * h);
+                                const uint4 ew = *reinterpret_cast<const uint4 *>(
+                                    s_env + 4 * env_chunk(2 * A + (d0 >> 1) + h));
                                 E[2 * h] = ew.x; Ep[2 * h] = ew.y; E[2 * h + 1] = ew.z; Ep[2 * h + 1] = ew.w;
                             }
                         } else {
 #pragma unroll
                             for (int s = 0; s < 4; s++) {
-                                const uint32_t wi = (d0 + s) & emask;
-                                E[s] = d0 + s < lim ? envp[2 * wi] : 0u;
-                                Ep[s] = d0 + s < lim ? envp[2 * wi + 1] : 0u;
+                                const uint32_t wi = env_pair(4 * A + ((d0 + s) & emask));
+                                E[s] = d0 + s < lim ? s_env[wi] : 0u;
+                                Ep[s] = d0 + s < lim ? s_env[wi + 1] : 0u;
                             }
                         }
                     } else {                                         // interp >= 4: one env word for the 4
@@ -390,7 +519,7 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                 const uint32_t j = j0 + s;
                 if (j >= p.n_samples) break;
                 const uint32_t n = spc_p2 ? (j >> spc_sh) : j / spc, k = j - n * spc;
-                const int si = window_find(s_st_t, w.x, w.y, st_lo, n);
+                const int si = window_find_rec(s_st, w.x, w.y, st_lo, n);
                 if (si < 0) continue;
                 const uint4 rec = s_st[si];
                 const uint32_t A = rec.y & 0xFFFu, L = (rec.y >> 12) & 0xFFFu;
@@ -402,7 +531,7 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                     const int ri = window_find(s_rs_t, w.z, w.w, rs_lo, n);
                     const uint32_t *fr = p.freq + freq_off + 16 * fi;
                     const uint32_t t_ref = ri >= 0 ? s_rs_t[ri] : 0u;
-                    const Carrier a0 = carrier_half(s_lut, fr[0] * (n - t_ref) + (phase << 15), (int32_t)(rec.w & 0xFFFFu));
+                    const Carrier a0 = carrier_quarter(s_lut, fr[0] * (n - t_ref) + (phase << 15), (int32_t)(rec.w & 0xFFFFu));
                     v[s] = mix(p.env[env_off + widx], k ? rotate(a0, fr[k]) : a0);
                 }
             }

@@ -184,13 +184,20 @@ constexpr uint32_t DDS_TILES_PER_STRIPE = DDS_TPS;   // tiles per workgroup (bui
 constexpr uint32_t DDS_ENV_LDS_MAX = 8192;    // words: tables up to 32 KiB are staged in LDS
 constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;   // words: 64 freq entries as (R, R') pairs
 
-// dynamic LDS bytes of dds_tile_kernel: half sine table | strobe records
-// (16 B) | strobe times | reset times | tile windows | env | freq
+// dynamic LDS bytes of dds_tile_kernel: quarter sine table (entries
+// 0..1031) | strobe records (16 B) | reset times | tile windows | env | freq |
+// the cycle sweep's per-wave store transpose (1 KiB per wave)
+constexpr uint32_t DDS_LUT_BYTES = 1032 * 2;
+constexpr uint32_t DDS_XPOSE_BYTES = (BLOCK / 64) * 1024;
 __host__ __device__ inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t tiles_per_stripe, uint32_t env_lds,
                                                   uint32_t freq_lds)
 {
-    return 4096 + ev_lds * 24 + tiles_per_stripe * 16 + (env_lds + freq_lds) * 4;
+    return DDS_LUT_BYTES + ev_lds * 20 + tiles_per_stripe * 16 + (env_lds + freq_lds) * 4 + DDS_XPOSE_BYTES;
 }
+
+// LDS words of an interp-1 envelope of n words staged as swizzled (E, E')
+// pairs (dds.hip env_pair): whole groups of 8 16-B chunks
+__host__ __device__ inline uint32_t dds_env_pairs_words(uint32_t n) { return (2 * n + 31) & ~31u; }
 
 // bytes of the event index (xs, xr, win)
 inline uint64_t dds_index_bytes(uint32_t n_channels, uint32_t ev_lds, uint32_t tiles)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC counts of one kernel per A/B library: for each lib, rocprofv3 --pmc over
 # scripts/ab.py on one workload, then the per-dispatch mean of each counter.
-#   scripts/pmc_ab.sh <workload> <kernel substring> <lib> [lib ...]
+#   scripts/pmc_ab.sh <workload (scripts/ab.py's, or dds: scripts/ab_dds.py)> <kernel substring> <lib> [lib ...]
 # Counters: SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
@@ -12,7 +12,9 @@ for lib in "$@"; do
     mkdir -p $out
     timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR \
         SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU -d $out -o pmc --output-format csv -- \
-        python3 scripts/ab.py --libs $lib --workload $wl --reps 2 --steps 2 > $out/log 2>&1 || { echo "$name failed"; exit 1; }
+        python3 $([ "$wl" = dds ] && echo "scripts/ab_dds.py --libs $lib --reps 2 --steps 2" \
+                               || echo "scripts/ab.py --libs $lib --workload $wl --reps 2 --steps 2") \
+        > $out/log 2>&1 || { echo "$name failed"; exit 1; }
     python3 - "$out" "$kern" "$name" <<'PY'
 import csv, glob, sys, collections, json
 out, kern, name = sys.argv[1:4]
