@@ -229,15 +229,27 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
     __builtin_amdgcn_wave_barrier();
     const int n_st = (int)ns, n_rs = (int)nr;
     // window of tile c: from the latest record at or before its first cycle
-    // (the first record when none is) to the latest at or before its last
-    for (uint32_t c = wl; c < p.tiles; c += 64) {
-        const uint64_t c0 = (uint64_t)c * DDS_TILE, c1 = min(c0 + DDS_TILE, (uint64_t)p.n_samples) - 1;
-        const uint32_t n0 = (uint32_t)(c0 / spc), n1 = (uint32_t)(c1 / spc);
-        const int s0 = last_le(s_st_t, n_st, n0), s1 = last_le(s_st_t, n_st, n1);
-        const int r0 = last_le(s_rs_t, n_rs, n0), r1 = last_le(s_rs_t, n_rs, n1);
-        const int sl = max(s0, 0), rl = max(r0, 0);
-        p.win[(uint64_t)ch * p.tiles + c] = make_uint4((uint32_t)sl, (uint32_t)(s1 + 1 - sl), (uint32_t)rl,
-                                                      (uint32_t)(r1 + 1 - rl));
+    // (the first record when none is) to the latest at or before its last.
+    // Lane wl takes a contiguous run of tiles: one binary search for its
+    // first tile, then cursors that only move forward (records are sorted)
+    const uint32_t per = (p.tiles + 63u) / 64u;
+    const uint32_t c_beg = min(wl * per, p.tiles), c_end = min(c_beg + per, p.tiles);
+    int a0 = 0, a1 = 0, b0 = 0, b1 = 0;          // records with t <= first / last cycle of the tile
+    for (uint32_t c = c_beg; c < c_end; c++) {
+        const uint64_t j0 = (uint64_t)c * DDS_TILE, j1 = min(j0 + DDS_TILE, (uint64_t)p.n_samples) - 1;
+        const uint32_t n0 = (uint32_t)(j0 / spc), n1 = (uint32_t)(j1 / spc);
+        if (c == c_beg) {
+            a0 = last_le(s_st_t, n_st, n0) + 1; a1 = last_le(s_st_t, n_st, n1) + 1;
+            b0 = last_le(s_rs_t, n_rs, n0) + 1; b1 = last_le(s_rs_t, n_rs, n1) + 1;
+        } else {
+            while (a0 < n_st && s_st_t[a0] <= n0) a0++;
+            while (a1 < n_st && s_st_t[a1] <= n1) a1++;
+            while (b0 < n_rs && s_rs_t[b0] <= n0) b0++;
+            while (b1 < n_rs && s_rs_t[b1] <= n1) b1++;
+        }
+        const int sl = max(a0 - 1, 0), rl = max(b0 - 1, 0);
+        p.win[(uint64_t)ch * p.tiles + c] = make_uint4((uint32_t)sl, (uint32_t)(a1 - sl), (uint32_t)rl,
+                                                      (uint32_t)(b1 - rl));
     }
 }
 
