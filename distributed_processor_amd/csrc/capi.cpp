@@ -679,6 +679,11 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.freq_lds = (freq_max + 3) & ~3u;
     p.tiles = (p.n_samples + DDS_TILE - 1) / DDS_TILE;
     p.stripes = std::max<uint32_t>(1, std::min<uint32_t>(p.tiles, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE));
+    {
+        const uint32_t fixed = dds_lds_bytes(0, DDS_TILES_PER_STRIPE, p.env_lds, p.freq_lds);
+        const uint32_t fit = fixed < DDS_WG_LDS_BUDGET ? (DDS_WG_LDS_BUDGET - fixed) / 20 & ~7u : 0u;
+        p.rec_lds = std::min(p.ev_lds, std::max(fit, DDS_REC_LDS_MIN));
+    }
     const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds, p.tiles);
     if (need > ctx->dds_index_cap) {         // the event index (grown, never shrunk)
         HIPCHK(ctx, hipStreamSynchronize(s));   // an earlier launch may still use it

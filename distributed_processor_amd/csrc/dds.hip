@@ -16,7 +16,8 @@
 //     stripes of a channel write ADJACENT tiles.  A workgroup stages the
 //     quarter-wave sine table, the channel's env / freq tables -- as
 //     (E, E') / (R, R') pairs for the Y-form products, the env pairs in
-//     bank-swizzled chunks -- its strobes and its tiles' windows in LDS, then
+//     bank-swizzled chunks -- its strobes (up to rec_lds; a denser stripe
+//     reads them from the global index) and its tiles' windows in LDS, then
 //     sweeps with no global loads in the loop (on gfx950 stores count in
 //     vmcnt, so a load there would wait for the previous tile's stores).
 //     At 16 samples per clock (the RFSoC rate) a lane makes one whole cycle
@@ -274,102 +275,60 @@ __device__ __forceinline__ int window_find_rec(const uint4 *rec, uint32_t lo, ui
     return a == 0 ? -1 : (int)(lo - base) + a - 1;
 }
 
-// ===========================================================================
-// Tile sweep.  Workgroup (stripe, ch) synthesises tiles stripe,
-// stripe + stripes, ... of channel ch.  Per tile a thread finds its pulse in
-// the tile's window (binary search over a few LDS entries), decodes it and
-// makes its 4 samples:
-//   Y-form quad sweep (spc a power of two >= 4, interp 1 or >= 4 and a power
-//   of two, tables staged, no -32768 in the staged eq / rq): a = symsat(a0 (x)
-//   R_k) as 2 v_dot2_i32_i16 + v_cvt_pk_i16_i32 + v_pk_max_i16, the mix
-//   sat16(E (x) a) as 2 v_dot2_i32_i16 + v_cvt_pk_i16_i32;
-//   else the generic per-sample sweep (X/Y form, tables read where they lie).
-// ===========================================================================
-__global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
+// local tile i of stripe `stripe`: the channel's tiles go round-robin over
+// its stripes, so at any time the stripes of a channel write adjacent tiles
+// (measured against contiguous runs per stripe: 0.317 vs 0.325 ms, config 5)
+__device__ __forceinline__ uint32_t stripe_tile(uint32_t stripe, uint32_t stripes, uint32_t i)
 {
-    // dynamic LDS (dds_lds_bytes): quarter sine table | strobe records |
-    // reset times | tile windows | env | freq | store transpose
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    int16_t *s_lut = reinterpret_cast<int16_t *>(s_dyn);
-    uint4 *s_st = reinterpret_cast<uint4 *>(s_dyn + DDS_LUT_BYTES);
-    uint32_t *s_rs_t = reinterpret_cast<uint32_t *>(s_st + p.ev_lds);
-    uint4 *s_win = reinterpret_cast<uint4 *>(s_rs_t + p.ev_lds);
-    uint32_t *s_env = reinterpret_cast<uint32_t *>(s_win + DDS_TILES_PER_STRIPE);
-    uint32_t *s_freq = s_env + p.env_lds;
-    uint4 *s_xpose = reinterpret_cast<uint4 *>(s_freq + p.freq_lds);   // DDS_XPOSE_BYTES, 16-B aligned
+    return stripe + i * stripes;
+}
 
+// the LDS-resident part of a tile workgroup
+struct TileLds {
+    const int16_t *lut;
+    const uint4 *win;
+    const uint32_t *env, *freq;
+    uint4 *xpose;
+};
+
+// The sweep over a stripe's n_t tiles.  st / rs_t: the strobe records and
+// reset times, staged in LDS (base = the first staged index) or the global
+// index (base 0); inlined at both call sites so each keeps its address space.
+__device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L, const uint32_t *d, uint32_t stripe,
+                                           uint32_t stripes, uint32_t n_t, bool quad, const uint4 *st,
+                                           uint32_t st_lo, const uint32_t *rs_t, uint32_t rs_lo)
+{
     const uint32_t tid = threadIdx.x;
-    const uint32_t ch = blockIdx.y, stripe = blockIdx.x, stripes = gridDim.x;
-    const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
+    const uint32_t ch = blockIdx.y;
     const uint32_t spc = d[2], interp = d[3] ? d[3] : 1u;
     const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
     const uint32_t spc_sh = __ffs(spc) - 1, int_sh = __ffs(interp) - 1;
-    const bool staged = (interp == 1 ? dds_env_pairs_words(env_len) : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds;
-    const uint32_t n_t = (p.tiles - stripe + stripes - 1) / stripes;   // this stripe's tiles (<= DDS_TILES_PER_STRIPE)
-    const uint4 *gwin = p.win + (uint64_t)ch * p.tiles;
-    // the stripe's strobes / resets: from its first tile's window to its last's end
-    const uint4 w_first = gwin[stripe], w_last = gwin[stripe + (n_t - 1) * stripes];
-    const uint32_t st_lo = w_first.x, st_n = w_last.x + w_last.y - st_lo;
-    const uint32_t rs_lo = w_first.z, rs_n = w_last.z + w_last.w - rs_lo;
-
-    // prologue: every global load of the workgroup up front
-    if (tid < DDS_LUT_BYTES / 16)                                      // entries 0..1031 (1024 needed)
-        reinterpret_cast<uint4 *>(s_lut)[tid] = reinterpret_cast<const uint4 *>(p.sin_lut)[tid];
-    bool bad = false;                       // a staged eq or rq is -32768: no Y form
-    if (staged) {
-        if (interp == 1) {
-            for (uint32_t i = tid; i < env_len; i += BLOCK) {
-                const uint32_t e = p.env[env_off + i];
-                bad |= (e & 0xFFFFu) == 0x8000u;
-                *reinterpret_cast<uint2 *>(s_env + env_pair(i)) = make_uint2(e, neg_swap(e));
-            }
-        } else {
-            for (uint32_t i = tid; i < env_len; i += BLOCK) {
-                const uint32_t e = p.env[env_off + i];
-                bad |= (e & 0xFFFFu) == 0x8000u;
-                s_env[i] = e;
-            }
-        }
-        for (uint32_t i = tid; i < freq_len; i += BLOCK) {
-            const uint32_t w = p.freq[freq_off + i];
-            const bool rot = (i & 15u) != 0;
-            bad |= rot && (w & 0xFFFFu) == 0x8000u;
-            reinterpret_cast<uint2 *>(s_freq)[i] = make_uint2(w, rot ? neg_swap(w) : 0u);
-        }
-    }
-    const uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds + st_lo;
-    const uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds + rs_lo;
-    for (uint32_t i = tid; i < st_n; i += BLOCK) {
-        s_st[i] = xs[i];
-    }
-    for (uint32_t i = tid; i < rs_n; i += BLOCK) s_rs_t[i] = xr[i];
-    if (tid < n_t) s_win[tid] = gwin[stripe + tid * stripes];
-    bad = __syncthreads_or(bad);
-
+    const int16_t *s_lut = L.lut;
+    const uint32_t *s_env = L.env, *s_freq = L.freq;
     uint32_t *out = p.iq + (uint64_t)ch * p.n_samples;
-    const bool quad = staged && !bad && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
     if (quad && spc == 16u) {
         // ---- cycle sweep (16 samples / clk, the RFSoC rate): a lane makes one
         // whole cycle, so the window search, record decode, theta and carrier
         // are done once per 16 samples; wave w takes the stripe's tiles w, w + 4, ...
         const uint32_t wv = tid >> 6, ln = tid & 63u;
         for (uint32_t i = wv; i < n_t; i += BLOCK / 64) {
-            const uint32_t n = (stripe + i * stripes) * (DDS_TILE / 16) + ln;   // this lane's cycle
+            const uint32_t tile = stripe_tile(stripe, stripes, i);
+            const uint32_t n = tile * (DDS_TILE / 16) + ln;                  // this lane's cycle
             const uint32_t j0 = 16 * n;
-            const uint4 w = s_win[i];
+            const uint4 w = L.win[i];
             uint32_t v[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) v[q] = 0u;
-            const int si = j0 < p.n_samples ? window_find_rec(s_st, w.x, w.y, st_lo, n) : -1;
+            const int si = j0 < p.n_samples ? window_find_rec(st, w.x, w.y, st_lo, n) : -1;
             if (si >= 0) {
-                const uint4 rec = s_st[si];                          // {t, env word, phase | freq << 17, amp}
-                const uint32_t A = rec.y & 0xFFFu, L = (rec.y >> 12) & 0xFFFu, fi = rec.z >> 17;
+                const uint4 rec = st[si];                            // {t, env word, phase | freq << 17, amp}
+                const uint32_t A = rec.y & 0xFFFu, Lw = (rec.y >> 12) & 0xFFFu, fi = rec.z >> 17;
                 const uint32_t room = env_len > 4 * A ? env_len - 4 * A : 0u;
                 uint32_t lim, emask;
-                if (L) {
+                if (Lw) {
                     emask = 0xFFFFFFFFu;
-                    const uint32_t n_env = min(4 * L, room);
+                    const uint32_t n_env = min(4 * Lw, room);
                     lim = n_env << int_sh;
                     if ((lim >> int_sh) != n_env) lim = 0xFFFFFFFFu;
                 } else {
@@ -378,8 +337,8 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                 }
                 const uint32_t d0 = 16 * (n - rec.x);                // samples since the strobe's first
                 if (16 * fi + 15 < freq_len && d0 < lim) {
-                    const int ri = window_find(s_rs_t, w.z, w.w, rs_lo, n);
-                    const uint32_t t_ref = ri >= 0 ? s_rs_t[ri] : 0u;
+                    const int ri = window_find(rs_t, w.z, w.w, rs_lo, n);
+                    const uint32_t t_ref = ri >= 0 ? rs_t[ri] : 0u;
                     const uint32_t *frp = s_freq + 32 * fi;          // (R, R') pairs; pair 0 = (F0, 0)
                     const uint32_t idx = (frp[0] * (n - t_ref) + ((rec.z & 0x1FFFFu) << 15)) >> 20;
                     const int32_t c = lut_quarter(s_lut, (idx + 1024) & 4095), sn = lut_quarter(s_lut, idx);
@@ -405,21 +364,24 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                             } else {
 #pragma unroll
                                 for (int s2 = 0; s2 < 4; s2++) {
-                                    const uint32_t d = d0 + 4 * g + s2;
-                                    const uint32_t wi = env_pair(4 * A + (d & emask));
-                                    E[s2] = d < lim ? s_env[wi] : 0u;
-                                    Ep[s2] = d < lim ? s_env[wi + 1] : 0u;
+                                    const uint32_t dd = d0 + 4 * g + s2;
+                                    const uint32_t wi = env_pair(4 * A + (dd & emask));
+                                    E[s2] = dd < lim ? s_env[wi] : 0u;
+                                    Ep[s2] = dd < lim ? s_env[wi + 1] : 0u;
                                 }
                             }
                         } else {                                     // interp >= 4: one env word for 4 samples
-                            const uint32_t e = s_env[4 * A + (((d0 + 4 * g) >> int_sh) & emask)], ep = neg_swap(e);
+                            const uint32_t e = d0 + 4 * g < lim ? s_env[4 * A + (((d0 + 4 * g) >> int_sh) & emask)] : 0u;
+                            const uint32_t ep = neg_swap(e);
 #pragma unroll
                             for (int s2 = 0; s2 < 4; s2++) { E[s2] = e; Ep[s2] = ep; }
                         }
 #pragma unroll
                         for (int s2 = 0; s2 < 4; s2++) {
                             const uint32_t y = (g == 0 && s2 == 0) ? y0 : rot_y(y0, R[s2], Rp[s2]);
-                            v[4 * g + s2] = d0 + 4 * g + s2 < lim ? mix_y(E[s2], Ep[s2], y) : 0u;
+                            // E = E' = 0 past the pulse end makes the mix 0 (interp 1: the
+                            // loads above; interp >= 4: 4-sample groups lie wholly in or out)
+                            v[4 * g + s2] = mix_y(E[s2], Ep[s2], y);
                         }
                     }
                 }
@@ -429,8 +391,8 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
             // apart): round r, lanes 16 r .. 16 r + 15 put their 4 chunks
             // (lane l's chunk q at slot 4 (l & 15) + (q ^ (l >> 2 & 3)):
             // conflict-free both ways), every lane takes one chunk and stores
-            uint4 *xp = s_xpose + 64 * wv;
-            const uint32_t tb = (stripe + i * stripes) * DDS_TILE;      // the tile's first sample
+            uint4 *xp = L.xpose + 64 * wv;
+            const uint32_t tb = tile * DDS_TILE;                      // the tile's first sample
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 if ((ln >> 4) == (uint32_t)r) {
@@ -454,24 +416,24 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
     }
     const uint32_t k0 = (4 * tid) & (spc - 1);     // sub-sample slot: fixed (the tile is a multiple of spc)
     for (uint32_t i = 0; i < n_t; i++) {
-        const uint32_t j0 = (stripe + i * stripes) * DDS_TILE + 4 * tid;
+        const uint32_t j0 = stripe_tile(stripe, stripes, i) * DDS_TILE + 4 * tid;
         if (j0 >= p.n_samples) continue;
-        const uint4 w = s_win[i];
+        const uint4 w = L.win[i];
         uint32_t v[4] = {0u, 0u, 0u, 0u};
         if (quad) {
             const uint32_t n = j0 >> spc_sh;                         // the thread's 4 samples share cycle n
-            const int si = window_find_rec(s_st, w.x, w.y, st_lo, n);
+            const int si = window_find_rec(st, w.x, w.y, st_lo, n);
             if (si >= 0) {
-                const uint4 rec = s_st[si];                          // {t, env word, phase | freq << 17, amp}
-                const uint32_t A = rec.y & 0xFFFu, L = (rec.y >> 12) & 0xFFFu, fi = rec.z >> 17;
+                const uint4 rec = st[si];                            // {t, env word, phase | freq << 17, amp}
+                const uint32_t A = rec.y & 0xFFFu, Lw = (rec.y >> 12) & 0xFFFu, fi = rec.z >> 17;
                 const uint32_t base = rec.x << spc_sh;               // sample index of the strobe
-                // samples d = j - base with env index (d >> int_sh) & emask inside
-                // the pulse and the table: d < lim
+                // samples dd = j - base with env index (dd >> int_sh) & emask inside
+                // the pulse and the table: dd < lim
                 const uint32_t room = env_len > 4 * A ? env_len - 4 * A : 0u;
                 uint32_t lim, emask;
-                if (L) {
+                if (Lw) {
                     emask = 0xFFFFFFFFu;
-                    const uint32_t n_env = min(4 * L, room);
+                    const uint32_t n_env = min(4 * Lw, room);
                     lim = n_env << int_sh;
                     if ((lim >> int_sh) != n_env) lim = 0xFFFFFFFFu;   // no overflow past 2^32
                 } else {
@@ -480,8 +442,8 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                 }
                 const uint32_t d0 = j0 - base;
                 if (16 * fi + 15 < freq_len && d0 < lim) {           // (a finished pulse plays zeros)
-                    const int ri = window_find(s_rs_t, w.z, w.w, rs_lo, n);
-                    const uint32_t t_ref = ri >= 0 ? s_rs_t[ri] : 0u;
+                    const int ri = window_find(rs_t, w.z, w.w, rs_lo, n);
+                    const uint32_t t_ref = ri >= 0 ? rs_t[ri] : 0u;
                     const uint32_t *frp = s_freq + 32 * fi;          // (R, R') pairs; pair 0 = (F0, 0)
                     const uint32_t idx = (frp[0] * (n - t_ref) + ((rec.z & 0x1FFFFu) << 15)) >> 20;
                     const int32_t c = lut_quarter(s_lut, (idx + 1024) & 4095), sn = lut_quarter(s_lut, idx);
@@ -495,7 +457,7 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                     }
                     const bool inside = d0 + 3 < lim;
                     if (interp == 1) {
-                        // (E, E') pairs, swizzled chunks (env_pair); pair 4A + d
+                        // (E, E') pairs, swizzled chunks (env_pair); pair 4A + dd
                         if (inside && emask) {
 #pragma unroll
                             for (int h = 0; h < 2; h++) {
@@ -531,18 +493,18 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
                 const uint32_t j = j0 + s;
                 if (j >= p.n_samples) break;
                 const uint32_t n = spc_p2 ? (j >> spc_sh) : j / spc, k = j - n * spc;
-                const int si = window_find_rec(s_st, w.x, w.y, st_lo, n);
+                const int si = window_find_rec(st, w.x, w.y, st_lo, n);
                 if (si < 0) continue;
-                const uint4 rec = s_st[si];
-                const uint32_t A = rec.y & 0xFFFu, L = (rec.y >> 12) & 0xFFFu;
+                const uint4 rec = st[si];
+                const uint32_t A = rec.y & 0xFFFu, Lw = (rec.y >> 12) & 0xFFFu;
                 const uint32_t r = j - rec.x * spc;
-                const uint32_t es = L ? (int_p2 ? (r >> int_sh) : r / interp) : 0u;
+                const uint32_t es = Lw ? (int_p2 ? (r >> int_sh) : r / interp) : 0u;
                 const uint32_t widx = 4 * A + es;
                 const uint32_t fi = rec.z >> 17, phase = rec.z & 0x1FFFFu;
-                if ((!L || es < 4 * L) && widx < env_len && 16 * fi + 15 < freq_len) {
-                    const int ri = window_find(s_rs_t, w.z, w.w, rs_lo, n);
+                if ((!Lw || es < 4 * Lw) && widx < env_len && 16 * fi + 15 < freq_len) {
+                    const int ri = window_find(rs_t, w.z, w.w, rs_lo, n);
                     const uint32_t *fr = p.freq + freq_off + 16 * fi;
-                    const uint32_t t_ref = ri >= 0 ? s_rs_t[ri] : 0u;
+                    const uint32_t t_ref = ri >= 0 ? rs_t[ri] : 0u;
                     const Carrier a0 = carrier_quarter(s_lut, fr[0] * (n - t_ref) + (phase << 15), (int32_t)(rec.w & 0xFFFFu));
                     v[s] = mix(p.env[env_off + widx], k ? rotate(a0, fr[k]) : a0);
                 }
@@ -550,6 +512,86 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
         }
         store4(out, j0, p.n_samples, v);
     }
+}
+
+// ===========================================================================
+// Tile sweep.  Workgroup (stripe, ch) synthesises its stripe of channel ch
+// (stripe_tile).  Per tile a thread finds its pulse in the tile's window
+// (binary search over a few LDS entries), decodes it and makes its samples:
+//   Y-form quad / cycle sweep (spc a power of two >= 4, interp 1 or >= 4 and
+//   a power of two, tables staged, no -32768 in the staged eq / rq): a =
+//   symsat(a0 (x) R_k) as 2 v_dot2_i32_i16 + v_cvt_pk_i16_i32 + v_pk_max_i16,
+//   the mix sat16(E (x) a) as 2 v_dot2_i32_i16 + v_cvt_pk_i16_i32;
+//   else the generic per-sample sweep (X/Y form, tables read where they lie).
+// ===========================================================================
+__global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
+{
+    // dynamic LDS (dds_lds_bytes): quarter sine table | strobe records |
+    // reset times | tile windows | env | freq | store transpose
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    int16_t *s_lut = reinterpret_cast<int16_t *>(s_dyn);
+    uint4 *s_st = reinterpret_cast<uint4 *>(s_dyn + DDS_LUT_BYTES);
+    uint32_t *s_rs_t = reinterpret_cast<uint32_t *>(s_st + p.rec_lds);
+    uint4 *s_win = reinterpret_cast<uint4 *>(s_rs_t + p.rec_lds);
+    uint32_t *s_env = reinterpret_cast<uint32_t *>(s_win + DDS_TILES_PER_STRIPE);
+    uint32_t *s_freq = s_env + p.env_lds;
+    uint4 *s_xpose = reinterpret_cast<uint4 *>(s_freq + p.freq_lds);   // DDS_XPOSE_BYTES, 16-B aligned
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t ch = blockIdx.y, stripe = blockIdx.x, stripes = gridDim.x;
+    const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
+    const uint32_t spc = d[2], interp = d[3] ? d[3] : 1u;
+    const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
+    const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
+    const bool staged = (interp == 1 ? dds_env_pairs_words(env_len) : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds;
+    const uint32_t n_t = (p.tiles - stripe + stripes - 1) / stripes;   // this stripe's tiles (<= DDS_TILES_PER_STRIPE)
+    const uint4 *gwin = p.win + (uint64_t)ch * p.tiles;
+    // the stripe's strobes / resets: from its first tile's window to its last's end
+    const uint4 w_first = gwin[stripe_tile(stripe, stripes, 0)], w_last = gwin[stripe_tile(stripe, stripes, n_t - 1)];
+    const uint32_t st_lo = w_first.x, st_n = w_last.x + w_last.y - st_lo;
+    const uint32_t rs_lo = w_first.z, rs_n = w_last.z + w_last.w - rs_lo;
+    const bool fits = st_n <= p.rec_lds && rs_n <= p.rec_lds;    // workgroup-uniform
+
+    // prologue: every global load of the workgroup up front
+    if (tid < DDS_LUT_BYTES / 16)                                      // entries 0..1031 (1024 needed)
+        reinterpret_cast<uint4 *>(s_lut)[tid] = reinterpret_cast<const uint4 *>(p.sin_lut)[tid];
+    bool bad = false;                       // a staged eq or rq is -32768: no Y form
+    if (staged) {
+        if (interp == 1) {
+            for (uint32_t i = tid; i < env_len; i += BLOCK) {
+                const uint32_t e = p.env[env_off + i];
+                bad |= (e & 0xFFFFu) == 0x8000u;
+                *reinterpret_cast<uint2 *>(s_env + env_pair(i)) = make_uint2(e, neg_swap(e));
+            }
+        } else {
+            for (uint32_t i = tid; i < env_len; i += BLOCK) {
+                const uint32_t e = p.env[env_off + i];
+                bad |= (e & 0xFFFFu) == 0x8000u;
+                s_env[i] = e;
+            }
+        }
+        for (uint32_t i = tid; i < freq_len; i += BLOCK) {
+            const uint32_t w = p.freq[freq_off + i];
+            const bool rot = (i & 15u) != 0;
+            bad |= rot && (w & 0xFFFFu) == 0x8000u;
+            reinterpret_cast<uint2 *>(s_freq)[i] = make_uint2(w, rot ? neg_swap(w) : 0u);
+        }
+    }
+    const uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
+    const uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
+    if (fits) {
+        for (uint32_t i = tid; i < st_n; i += BLOCK) s_st[i] = xs[st_lo + i];
+        for (uint32_t i = tid; i < rs_n; i += BLOCK) s_rs_t[i] = xr[rs_lo + i];
+    }
+    if (tid < n_t) s_win[tid] = gwin[stripe_tile(stripe, stripes, tid)];
+    bad = __syncthreads_or(bad);
+
+    const bool quad = staged && !bad && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
+    const TileLds L{s_lut, s_win, s_env, s_freq, s_xpose};
+    if (fits)
+        tile_sweep(p, L, d, stripe, stripes, n_t, quad, s_st, st_lo, s_rs_t, rs_lo);
+    else
+        tile_sweep(p, L, d, stripe, stripes, n_t, quad, xs, 0u, xr, 0u);
 }
 
 // dynamic LDS above 64 KiB needs an opt-in per kernel, raised as requests grow
@@ -576,7 +618,7 @@ hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    const uint32_t lds = dds_lds_bytes(p.ev_lds, DDS_TILES_PER_STRIPE, p.env_lds, p.freq_lds);
+    const uint32_t lds = dds_lds_bytes(p.rec_lds, DDS_TILES_PER_STRIPE, p.env_lds, p.freq_lds);
     static uint32_t granted = 0;
     const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_tile_kernel), lds, &granted);
     if (e != hipSuccess) return e;

@@ -166,6 +166,7 @@ struct DDSParams {
     uint32_t *iq;                  // [n_channels][n_samples] packed {I16 low, Q16 high}
     uint32_t n_channels, n_lanes, n_samples, event_cap;
     uint32_t ev_lds;               // compacted-event slots per channel (>= event_cap, multiple of 8)
+    uint32_t rec_lds;              // strobe records / reset times a tile workgroup stages in LDS (<= ev_lds)
     uint32_t env_lds, freq_lds;    // LDS staging capacity for a channel's env / freq table (words, as staged)
     uint32_t tiles;                // sample tiles per channel (DDS_TILE samples each)
     uint32_t stripes;              // workgroups per channel (gridDim.x)
@@ -189,11 +190,17 @@ constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;   // words: 64 freq entries as (R, R
 // the cycle sweep's per-wave store transpose (1 KiB per wave)
 constexpr uint32_t DDS_LUT_BYTES = 1032 * 2;
 constexpr uint32_t DDS_XPOSE_BYTES = (BLOCK / 64) * 1024;
-__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t ev_lds, uint32_t tiles_per_stripe, uint32_t env_lds,
+__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t rec_lds, uint32_t tiles_per_stripe, uint32_t env_lds,
                                                   uint32_t freq_lds)
 {
-    return DDS_LUT_BYTES + ev_lds * 20 + tiles_per_stripe * 16 + (env_lds + freq_lds) * 4 + DDS_XPOSE_BYTES;
+    return DDS_LUT_BYTES + rec_lds * 20 + tiles_per_stripe * 16 + (env_lds + freq_lds) * 4 + DDS_XPOSE_BYTES;
 }
+// LDS budget of a tile workgroup: 8 workgroups (32 waves, the VGPR-bound
+// occupancy) share a CU's 160 KiB.  The record capacity is what is left of
+// it (at least DDS_REC_LDS_MIN); a stripe whose window holds more strobes or
+// resets than that reads them from the global index instead.
+constexpr uint32_t DDS_WG_LDS_BUDGET = 20 * 1024;
+constexpr uint32_t DDS_REC_LDS_MIN = 64;
 
 // LDS words of an interp-1 envelope of n words staged as swizzled (E, E')
 // pairs (dds.hip env_pair): whole groups of 8 16-B chunks

@@ -74,7 +74,16 @@ def main():
             else:
                 same &= bool(torch.equal(ref, snap))
     gb = plan.n_channels * n_samples * 4 / 1e9
-    print(json.dumps({'same_iq': same, 'GB': gb,
+    fills = []                       # the same buffer written by a fill (hipMemsetAsync): the store ceiling
+    for _ in range(a.reps):
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(a.steps):
+            iq.fill_(1)
+        t1.record()
+        torch.cuda.synchronize()
+        fills.append(t0.elapsed_time(t1) / a.steps)
+    print(json.dumps({'same_iq': same, 'GB': gb, 'fill_ms': float(np.median(fills)),
                       'kernel_ms': {os.path.basename(l): float(np.median(k)) for l, k in zip(libs, kern)},
                       'kernel_min_ms': {os.path.basename(l): float(np.min(k)) for l, k in zip(libs, kern)},
                       'step_ms': {os.path.basename(l): float(np.median(k)) for l, k in zip(libs, step)}}))

@@ -102,6 +102,52 @@ __global__ void __launch_bounds__(BLOCK) fillU_k(uint32_t *iq, uint64_t total)
     }
 }
 
+// the dds_tile_kernel store shape: grid (stripes, channels), 1024-sample tiles
+// (4 KiB, four 1-KiB row stores per wave), wave w of stripe s takes local
+// tiles w, w + 4, ... of its stripe; RR: local tile i = tile s + i * stripes,
+// else the stripe's contiguous run s * TPS + i
+template <bool RR>
+__global__ void __launch_bounds__(BLOCK) ddsshape_k(uint32_t *iq, uint32_t n_samples, uint32_t tps)
+{
+    const uint32_t tiles = (n_samples + 1023) / 1024, stripes = gridDim.x, s = blockIdx.x;
+    uint32_t *out = iq + (uint64_t)blockIdx.y * n_samples;
+    const uint32_t n_t = RR ? (tiles - s + stripes - 1) / stripes : min(tps, tiles - s * tps);
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    for (uint32_t i = wv; i < n_t; i += 4) {
+        const uint32_t t = RR ? s + i * stripes : s * tps + i;
+        for (int r = 0; r < 4; r++) {
+            const uint32_t j = t * 1024 + 4 * (64 * r + ln);
+            if (j + 3 < n_samples) st<false>(out + j, j);
+        }
+    }
+}
+
+// flattened buffer, 1024-sample tiles; WG b writes T consecutive tiles, wave w tiles w, w + 4, ...
+__global__ void __launch_bounds__(BLOCK) wgtiles_k(uint32_t *iq, uint64_t total, uint32_t T)
+{
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    for (uint32_t i = wv; i < T; i += 4) {
+        const uint64_t t = (uint64_t)blockIdx.x * T + i;
+        for (int r = 0; r < 4; r++) {
+            const uint64_t j = t * 1024 + 4 * (64 * r + ln);
+            if (j + 3 < total) st<false>(iq + j, (uint32_t)j);
+        }
+    }
+}
+
+// WG b = tiles 4b .. 4b + 3 of channel b / tpc (tpc = WGs per channel), one tile per wave
+__global__ void __launch_bounds__(BLOCK) wavetile_k(uint32_t *iq, uint32_t n_samples, uint32_t tpc)
+{
+    const uint32_t ch = blockIdx.x / tpc, tw = blockIdx.x % tpc;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    uint32_t *out = iq + (uint64_t)ch * n_samples;
+    const uint32_t t = 4 * tw + wv;
+    for (int r = 0; r < 4; r++) {
+        const uint32_t j = t * 1024 + 4 * (64 * r + ln);
+        if (j + 3 < n_samples) st<false>(out + j, j);
+    }
+}
+
 static double timeit(void (*launch)(void *), void *a, uint64_t bytes)
 {
     hipEvent_t e0, e1;
@@ -136,6 +182,23 @@ int main(int argc, char **argv)
         printf("{\"variant\": \"%s\", \"TB_s\": %.3f, \"ms\": %.4f}\n", name, tbs, bytes / (tbs * 1e12) * 1e3);
         fflush(stdout);
     };
+    {
+        const uint32_t tiles = (g.ns + 1023) / 1024;
+        static const uint32_t TPSs[] = {4, 2, 8, 16};
+        for (uint32_t T : TPSs) {
+            char nm[64];
+            g.p = T;
+            snprintf(nm, sizeof nm, "ddsshape_rr_%u", T);
+            report(nm, [](void *) { const uint32_t tl = (g.ns + 1023) / 1024; ddsshape_k<true><<<dim3((tl + g.p - 1) / g.p, g.nch), BLOCK>>>(g.iq, g.ns, g.p); });
+            snprintf(nm, sizeof nm, "ddsshape_cont_%u", T);
+            report(nm, [](void *) { const uint32_t tl = (g.ns + 1023) / 1024; ddsshape_k<false><<<dim3((tl + g.p - 1) / g.p, g.nch), BLOCK>>>(g.iq, g.ns, g.p); });
+            snprintf(nm, sizeof nm, "wgtiles_%u", T);
+            report(nm, [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; wgtiles_k<<<(uint32_t)((t / 1024 + g.p - 1) / g.p), BLOCK>>>(g.iq, t, g.p); });
+        }
+        report("wavetile", [](void *) { const uint32_t tl = (g.ns + 1023) / 1024, tpc = (tl + 3) / 4; wavetile_k<<<g.nch * tpc, BLOCK>>>(g.iq, g.ns, tpc); });
+        report("fill1_256_again", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fill1_k<256><<<(uint32_t)((t / 4 + 255) / 256), 256>>>(g.iq, t); });
+        (void)tiles;
+    }
     const uint32_t chunks = (g.ns + 32767) / 32768;
     {
         const uint64_t tot = (uint64_t)g.nch * g.ns;

@@ -244,3 +244,31 @@ def test_config5_slice(emu):
     ref = oracle.dds(plan.desc, host(out['summary']), host(out['events']), plan.env, plan.freq, n_samples,
                      cfg.event_cap, threads=8)
     check_equal(host(iq), ref, 'config5 slice')
+
+
+def test_global_record_fallback(emu):
+    """a staged 32-KiB envelope leaves room for only DDS_REC_LDS_MIN records in
+    a tile workgroup's LDS: stripes with denser windows read their strobes and
+    resets from the global index, the sparse lanes of the same launch stage
+    them; both against oracle_dds"""
+    import torch
+    rng = np.random.default_rng(23)
+    cap, n_lanes, n_cycles = 320, 5, 2500
+    env_tab = pack_iq16(np.exp(1j * rng.uniform(0, 2 * np.pi, 4000)) * rng.uniform(0, 1, 4000))
+    freq_tab = np.concatenate([DDSElementConfig(samples_per_clk=16).get_freq_buffer([f])
+                               for f in (91.7e6, -13.1e6, 250e6)])
+    summary, ev = synthetic_timelines(rng, n_lanes, cap, n_cycles, 4000, 3)
+    summary[4, 2] = 20                                     # a sparse lane: its stripes fit in LDS
+    desc = []
+    for L in range(n_lanes):
+        for e, (spc, interp) in enumerate(((16, 1), (16, 4), (8, 1), (16, 3))):
+            desc.append((L, e, spc, interp, 0, 4000, 0, len(freq_tab)))
+    desc = np.array(desc, np.uint32)
+    n_samples = 16 * n_cycles + 4 * 5
+    ref = oracle.dds(desc, summary, ev, env_tab, freq_tab, n_samples, cap)
+    dev = {'summary': torch.from_numpy(summary.view(np.int32)).cuda(),
+           'events': torch.from_numpy(ev.view(np.int32)).cuda()}
+    iq = emu.synthesize(plan_from(desc, env_tab, freq_tab, n_lanes, cap), dev, n_samples)
+    torch.cuda.synchronize()
+    check_equal(host(iq), ref, 'global record fallback')
+    assert (ref != 0).sum() > 10000
