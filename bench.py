@@ -150,11 +150,30 @@ def bytes_per_lane(summary_np, cfg):
     return 32.0 + 16.0 * n_ev + 8.0 * n_me
 
 
+SETTLE_S = 0.3
+
+
+def settle(step, drain, seconds=SETTLE_S):
+    """untimed steps for `seconds` of wall time, synchronised every 10 steps:
+    the GPU's clocks ramp up under load, and a leg that starts after an idle
+    host-side phase would otherwise time its first milliseconds at low clocks
+    (config 2 measured 0.202 ms per step cold against 0.176-0.179 warm,
+    scripts/step_probe.py)"""
+    import torch
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        for _ in range(10):
+            step()
+        drain()
+        torch.cuda.synchronize()
+
+
 def timed(step, drain, steps, warmup, world):
-    """warm-up, then exactly `steps` steps between barrier + synchronize;
-    returns the max over ranks of the wall time"""
+    """clock settle, warm-up, then exactly `steps` steps between barrier +
+    synchronize; returns the max over ranks of the wall time"""
     import torch
     from distributed_processor_amd import sharding
+    settle(step, drain)
     for _ in range(warmup):
         step()
     drain()
@@ -245,10 +264,10 @@ def leg_ramsey(emu, args, world, rank, stream):
     ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
     emu.load(ps)
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, trace_cap=0, meas_cap=2,
-                           meas_latency=64, seed=0x5EED, p1=0.5)
+                           meas_latency=64, seed=0x5EED, p1=0.5, hist_assign=True)
     shot0, n = sharding.weak_shard(args.shots, rank)
     out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
-    pipe = sharding.HistogramPipeline(out['hist'])
+    pipe = sharding.HistogramPipeline(out['hist'], zero=False)     # each run assigns its histogram
 
     def launch(h):
         out['hist'] = h
@@ -356,10 +375,10 @@ def leg_active_reset(emu, args, world, rank, stream):
     ps = ProgramSet(workloads.config3_active_reset(8))
     emu.load(ps)
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
-                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5)
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, hist_assign=True)
     shot0, n = sharding.weak_shard(args.ar_shots, rank)
     out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
-    pipe = sharding.HistogramPipeline(out['hist'])
+    pipe = sharding.HistogramPipeline(out['hist'], zero=False)     # each run assigns its histogram
 
     def launch(h):
         out['hist'] = h

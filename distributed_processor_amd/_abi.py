@@ -4,7 +4,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_CORES = 64
 MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
 
@@ -36,7 +36,7 @@ class Config(C.Structure):
                 ('lut_mask', C.c_uint32), ('meas_model', C.c_uint32),
                 ('p1_threshold', C.c_uint32 * MAX_CORES), ('lut_table', C.c_uint64 * 256),
                 ('ro_sep', C.c_int32), ('ro_sigma', C.c_uint32), ('ro_thr', C.c_int32),
-                ('ro_win', C.c_uint32)]
+                ('ro_win', C.c_uint32), ('hist_assign', C.c_uint32), ('reserved', C.c_uint32)]
 
 
 class Outputs(C.Structure):
@@ -57,10 +57,12 @@ DEFAULT_LUT_TABLE = (0b00000, 0b00100, 0b10000, 0b01000)   # meas_lut.sv:17-20
 def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 20,
                 event_cap=64, trace_cap=0, meas_cap=8, fproc_mode=FPROC_MEAS, meas_elem=2,
                 meas_latency=64, sync_latency=1, sync_mask=0, seed=0x5EED, p1=0.5,
-                lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE, exec_flags=0, readout=None):
+                lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE, exec_flags=0, readout=None,
+                hist_assign=False):
     """Validated Config.  p1: float or per-core list of P(state = 1).
     readout: None (outcome = prepared state) or dict(sep=, sigma=, thr=) for the
-    readout model of include/dpemu.h (sigma a float noise scale, stored Q16)."""
+    readout model of include/dpemu.h (sigma a float noise scale, stored Q16).
+    hist_assign: a run writes its outcome histogram instead of adding to it."""
     C_ = int(cores_per_shot)
     if C_ < 1 or C_ > MAX_CORES or (C_ & (C_ - 1)):
         raise ValueError('cores_per_shot must be a power of two in [1, 64]')
@@ -90,6 +92,7 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
     cfg.seed = int(seed) & (2 ** 64 - 1)
     cfg.lut_mask = int(lut_mask)
     cfg.exec_flags = int(exec_flags)
+    cfg.hist_assign = 1 if hist_assign else 0
     ps = list(p1) if isinstance(p1, (list, tuple, np.ndarray)) else [p1] * C_
     for c, p in enumerate(ps):
         cfg.p1_threshold[c] = prob_to_threshold(p)

@@ -53,6 +53,7 @@ struct dpemu_ctx {
     // privatised outcome histograms (R replicas, reduced after the interpreter)
     uint32_t *d_hist_rep = nullptr;
     uint64_t hist_rep_bytes = 0;
+    bool hist_rep_dirty = true;     // replicas not known to be zero
     // call ordering across streams: the last call's stream and an event after its work
     hipEvent_t ord_ev = nullptr;
     hipStream_t ord_stream = nullptr;
@@ -343,6 +344,8 @@ static int validate(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t n_shots, b
         return fail(ctx, DPEMU_E_INVALID, "meas_latency / sync_latency must be in [1, 2^20]");
     if (cfg->meas_model != DPEMU_MEAS_STATE && cfg->meas_model != DPEMU_MEAS_READOUT)
         return fail(ctx, DPEMU_E_INVALID, "meas_model must be DPEMU_MEAS_STATE or DPEMU_MEAS_READOUT");
+    if (cfg->hist_assign > 1 || cfg->reserved)
+        return fail(ctx, DPEMU_E_INVALID, "hist_assign must be 0 or 1 and reserved 0");
     if (cfg->ro_win >= 4096)
         return fail(ctx, DPEMU_E_INVALID, "ro_win %u must fit the 12-bit envelope-length field", cfg->ro_win);
     if ((uint64_t)cfg->max_cycles + cfg->meas_latency + 16 >= 0x80000000ull)
@@ -498,8 +501,14 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
                 ctx->d_hist_rep = nullptr; ctx->hist_rep_bytes = 0;
                 HIPCHK(ctx, hipMalloc(&ctx->d_hist_rep, need));
                 ctx->hist_rep_bytes = need;
+                ctx->hist_rep_dirty = true;
             }
-            HIPCHK(ctx, hipMemsetAsync(ctx->d_hist_rep, 0, need, stream));
+            // the reduce kernel leaves every replica word it read zero, so the
+            // replicas are zeroed once per allocation (or after a failed run)
+            if (ctx->hist_rep_dirty) {
+                HIPCHK(ctx, hipMemsetAsync(ctx->d_hist_rep, 0, ctx->hist_rep_bytes, stream));
+                ctx->hist_rep_dirty = false;
+            }
             p.hist = nullptr;
             p.hist_rep = ctx->d_hist_rep;
             p.hist_reps = R;
@@ -524,6 +533,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             p.prog_lds_words = (uint32_t)std::max<uint64_t>(16, (footprint + 15) & ~15ull);
         }
     }
+    if (out->hist && !p.hist_rep && cfg->hist_assign)      // direct atomics: assign = zero, then add
+        HIPCHK(ctx, hipMemsetAsync(out->hist, 0, bins * sizeof(uint64_t), stream));
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
@@ -544,9 +555,12 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             snprintf(name, sizeof name, "interp_kernel<feat=0x%x>", feat);
         ctx->last_kernel = name;
     }
-    if (out->hist && p.hist_rep)
-        HIPCHK(ctx, launch_hist_reduce(ctx->d_hist_rep, R, hist_stride, bins,
+    if (out->hist && p.hist_rep) {
+        ctx->hist_rep_dirty = true;          // until the reduce is enqueued
+        HIPCHK(ctx, launch_hist_reduce(ctx->d_hist_rep, R, hist_stride, bins, cfg->hist_assign != 0,
                                        reinterpret_cast<unsigned long long *>(out->hist), stream));
+        ctx->hist_rep_dirty = false;
+    }
     HIPCHK(ctx, order_end(ctx, stream));
     return DPEMU_OK;
 }

@@ -136,7 +136,7 @@ struct KParams {
 };
 constexpr uint32_t HIST_LDS_MAX = 1024;
 
-hipError_t launch_hist_reduce(const uint32_t *rep, uint32_t R, uint64_t stride, uint64_t bins,
+hipError_t launch_hist_reduce(uint32_t *rep, uint32_t R, uint64_t stride, uint64_t bins, bool assign,
                               unsigned long long *hist, hipStream_t stream);
 
 hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);

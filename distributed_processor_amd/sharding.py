@@ -76,19 +76,22 @@ class HistogramPipeline:
     Batch k's kernel writes its outcome histogram into buffer k % n_buffers;
     the buffer's all-reduce is enqueued asynchronously right after the launch
     (on RCCL's stream, ordered after the kernel), so batch k's exchange runs
-    while batch k + 1's kernel does.  Before a buffer is zeroed for reuse, the
-    exchange that last used it is waited for.  ``drain()`` waits for every
+    while batch k + 1's kernel does.  Before a buffer is reused, the exchange
+    that last used it is waited for; it is then zeroed, unless ``zero`` is
+    False because the launch assigns the histogram (dpemu_config.hist_assign:
+    the library's reduce kernel stores the counts, one launch fewer per batch).  ``drain()`` waits for every
     pending exchange; ``result()`` is then the histogram of the last batch,
     summed over ranks.  One rank: no collectives, the same call sequence.
     """
 
-    def __init__(self, hist, n_buffers=2, group=None):
+    def __init__(self, hist, n_buffers=2, group=None, zero=True):
         import torch
         if n_buffers < 1:
             raise ValueError('n_buffers must be >= 1')
         self.bufs = [hist] + [torch.zeros_like(hist) for _ in range(n_buffers - 1)]
         self.pending = [None] * n_buffers
         self.group = group
+        self.zero = zero
         self.k = 0
 
     def step(self, launch):
@@ -99,7 +102,8 @@ class HistogramPipeline:
             self.pending[b].wait()                    # this buffer's previous exchange is done
             self.pending[b] = None
         h = self.bufs[b]
-        h.zero_()
+        if self.zero:
+            h.zero_()
         launch(h)
         self.pending[b] = allreduce_histogram(h, group=self.group, async_op=True)
         return h

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DPEMU_ABI_VERSION 4
+#define DPEMU_ABI_VERSION 5
 
 /* ---- error codes ---------------------------------------------------- */
 #define DPEMU_OK            0
@@ -127,6 +127,9 @@ typedef struct dpemu_config {
     uint32_t ro_sigma;         /* noise scale, Q16 (noise sigma = ro_sigma / 2^16 * 37837.6) */
     int32_t  ro_thr;           /* discriminator threshold                                */
     uint32_t ro_win;           /* reference readout window (env words, < 4096); 0 = amplitude only */
+    uint32_t hist_assign;      /* 0: out->hist += this run's counts; 1: out->hist = this run's
+                                  counts (no separate zeroing launch before each run)        */
+    uint32_t reserved;         /* 0 */
 } dpemu_config;
 
 #define DPEMU_MEAS_STATE   0
@@ -164,7 +167,7 @@ typedef struct dpemu_outputs {
     uint32_t *trace;      /* [trace_cap][n_lanes][4]           */
     uint32_t *meas;       /* [meas_cap][n_lanes][2]            */
     uint32_t *regs;       /* [16][n_lanes] final register file */
-    uint64_t *hist;       /* [n_groups][2^C], accumulated      */
+    uint64_t *hist;       /* [n_groups][2^C], accumulated (or assigned: hist_assign) */
 } dpemu_outputs;
 
 typedef struct dpemu_ctx dpemu_ctx;

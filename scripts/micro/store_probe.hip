@@ -148,6 +148,22 @@ __global__ void __launch_bounds__(BLOCK) wavetile_k(uint32_t *iq, uint32_t n_sam
     }
 }
 
+// the dds_tile_kernel stripes, but the workgroup writes each tile together:
+// for the stripe's local tiles 4m .. 4m + 3, round r stores tile 4m + r with
+// wave w writing its row w (1 KiB), so every round is one dense 4 KiB
+template <bool RR>
+__global__ void __launch_bounds__(BLOCK) ddswg_k(uint32_t *iq, uint32_t n_samples, uint32_t tps)
+{
+    const uint32_t tiles = (n_samples + 1023) / 1024, stripes = gridDim.x, s = blockIdx.x;
+    uint32_t *out = iq + (uint64_t)blockIdx.y * n_samples;
+    const uint32_t n_t = RR ? (tiles - s + stripes - 1) / stripes : min(tps, tiles - s * tps);
+    for (uint32_t i = 0; i < n_t; i++) {
+        const uint32_t t = RR ? s + i * stripes : s * tps + i;
+        const uint32_t j = t * 1024 + 4 * threadIdx.x;
+        if (j + 3 < n_samples) st<false>(out + j, j);
+    }
+}
+
 static double timeit(void (*launch)(void *), void *a, uint64_t bytes)
 {
     hipEvent_t e0, e1;
@@ -184,7 +200,7 @@ int main(int argc, char **argv)
     };
     {
         const uint32_t tiles = (g.ns + 1023) / 1024;
-        static const uint32_t TPSs[] = {4, 2, 8, 16};
+        static const uint32_t TPSs[] = {16, 8, 32};
         for (uint32_t T : TPSs) {
             char nm[64];
             g.p = T;
@@ -192,6 +208,10 @@ int main(int argc, char **argv)
             report(nm, [](void *) { const uint32_t tl = (g.ns + 1023) / 1024; ddsshape_k<true><<<dim3((tl + g.p - 1) / g.p, g.nch), BLOCK>>>(g.iq, g.ns, g.p); });
             snprintf(nm, sizeof nm, "ddsshape_cont_%u", T);
             report(nm, [](void *) { const uint32_t tl = (g.ns + 1023) / 1024; ddsshape_k<false><<<dim3((tl + g.p - 1) / g.p, g.nch), BLOCK>>>(g.iq, g.ns, g.p); });
+            snprintf(nm, sizeof nm, "ddswg_rr_%u", T);
+            report(nm, [](void *) { const uint32_t tl = (g.ns + 1023) / 1024; ddswg_k<true><<<dim3((tl + g.p - 1) / g.p, g.nch), BLOCK>>>(g.iq, g.ns, g.p); });
+            snprintf(nm, sizeof nm, "ddswg_cont_%u", T);
+            report(nm, [](void *) { const uint32_t tl = (g.ns + 1023) / 1024; ddswg_k<false><<<dim3((tl + g.p - 1) / g.p, g.nch), BLOCK>>>(g.iq, g.ns, g.p); });
             snprintf(nm, sizeof nm, "wgtiles_%u", T);
             report(nm, [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; wgtiles_k<<<(uint32_t)((t / 1024 + g.p - 1) / g.p), BLOCK>>>(g.iq, t, g.p); });
         }

@@ -31,7 +31,8 @@ def test_abi_version_and_struct_sizes():
     L = _native.load_library()
     assert L.dpemu_abi_version() == _abi.ABI_VERSION
     # dpemu_config: 12 u32 + 2 u64 + 2 u32 + 64 u32 + 256 u64 + the readout model's 4 x 32 bit
-    assert C.sizeof(_abi.Config) == 12 * 4 + 16 + 8 + 64 * 4 + 256 * 8 + 16
+    # + hist_assign, reserved
+    assert C.sizeof(_abi.Config) == 12 * 4 + 16 + 8 + 64 * 4 + 256 * 8 + 16 + 8
     assert C.sizeof(_abi.Outputs) == 6 * 8
     assert C.sizeof(_abi.DDSChannels) == 4 * 4 + 8 * 8
 

@@ -63,15 +63,16 @@ def _rank_main(rank, world, port, out_dir):
         slowest = sharding.max_over_ranks(float(rank + 1))
         # bench.py's batch loop: batch b = global shots [b * N_BATCH, (b + 1) * N_BATCH),
         # this rank's share of it emulated by the stand-in "kernel" (oracle_fast
-        # accumulating into the pipeline's buffer, as the GPU kernel does)
-        pipe = sharding.HistogramPipeline(torch.zeros_like(hist))
+        # assigning the pipeline's buffer, as the GPU kernel does with hist_assign:
+        # no zeroing between batches)
+        pipe = sharding.HistogramPipeline(torch.zeros_like(hist), zero=False)
         for b in range(N_BATCHES):
             b0, bn = sharding.shard_range(N_BATCH, rank, world)
 
             def launch(h, b=b, b0=b0, bn=bn):
                 o = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, b * N_BATCH + b0, bn,
                                     threads=1, want=('hist',))
-                h += torch.from_numpy(o['hist'].astype(np.int64))
+                h.copy_(torch.from_numpy(o['hist'].astype(np.int64)))
             pipe.step(launch)
         pipe.drain()
         last_two = torch.stack([pipe.bufs[(N_BATCHES - 2) % 2], pipe.result()])
@@ -155,3 +156,17 @@ def test_pipeline_single_rank_and_buffer_reuse():
     assert pipe.result().tolist() == [5] * 4 and pipe.bufs[1 - (5 - 1) % 2].tolist() == [4] * 4
     with pytest.raises(RuntimeError):
         sharding.HistogramPipeline(h).result()
+
+
+def test_pipeline_assigning_launch_skips_zeroing():
+    """zero=False: the launch assigns the buffer (hist_assign), the pipeline
+    launches nothing else; an accumulating launch would then see old counts"""
+    h = torch.full((4,), 99, dtype=torch.int64)
+    pipe = sharding.HistogramPipeline(h, n_buffers=2, zero=False)
+    for b in range(5):
+        pipe.step(lambda t, b=b: t.fill_(b + 1))
+    pipe.drain()
+    assert pipe.result().tolist() == [5] * 4 and pipe.bufs[1 - (5 - 1) % 2].tolist() == [4] * 4
+    acc = sharding.HistogramPipeline(torch.full((2,), 7, dtype=torch.int64), n_buffers=1, zero=False)
+    acc.step(lambda t: t.add_(1))
+    assert acc.result().tolist() == [8, 8]
