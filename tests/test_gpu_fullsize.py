@@ -1,0 +1,115 @@
+"""BASELINE configs at their stated per-GPU sizes, the whole launch against
+the oracle (config 4 at full size: tests/test_gpu_rb.py).
+
+* config 2 (BASELINE configs[1]): 8-core Ramsey, 100 delay points, 10^6
+  shots on one GPU -- every output array of the bench's launch (summaries,
+  events, measurements, histogram) equal to oracle_fast over the same 10^6
+  shots, bit for bit;
+* config 3 (configs[2]): active reset, 10^7 shots over 8 GPUs = 1.25 * 10^6
+  shots per GPU -- rank 0's and rank 7's shards (global shot offsets, the
+  RNG keyed by global shot index) each equal to oracle_fast in full, and the
+  eight shards' histograms (two of them run) consistent with the outcome law;
+* config 5 (configs[4]): DDS of 128 RB timelines x 16 channels at 16
+  samples / clock, the bench's full-size launch (2048 channels x 209,952
+  samples); 256 channels spread over the launch (128 qdrv, 128 rdrv), whole
+  length, equal to oracle_dds.
+
+oracle_fast / oracle_dds run with the job's CPU share (OMP_NUM_THREADS, 16
+on the GPU box)."""
+
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from distributed_processor_amd import _abi, workloads
+from distributed_processor_amd.dds import ChannelPlan
+from distributed_processor_amd.emulator import Emulator, ProgramSet, alloc_device_outputs
+
+pytestmark = pytest.mark.gpu
+
+THREADS = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope='module')
+def emu():
+    e = Emulator(0)
+    yield e
+    e.close()
+
+
+def run_full(emu, ps, cfg, n, shot0, want):
+    import torch
+    emu.load(ps)
+    out = alloc_device_outputs(cfg, n, want=want)
+    for t in out.values():
+        t.zero_()                     # slots past a lane's count stay 0, as in the oracle's arrays
+    emu.run_device(cfg, n, shot0, out)
+    torch.cuda.synchronize()
+    g = {k: v.cpu().numpy() for k, v in out.items()}
+    del out
+    torch.cuda.empty_cache()
+    f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n, threads=THREADS, want=want)
+    for k in want:
+        a = g[k].view(f[k].dtype).reshape(f[k].shape)
+        if not np.array_equal(a, f[k]):
+            bad = np.argwhere(a != f[k])
+            raise AssertionError('{}: {} mismatches, first at {}'.format(k, len(bad), bad[0].tolist()))
+    return g
+
+
+def test_config2_full_launch_bit_exact(emu):
+    ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, trace_cap=0, meas_cap=2,
+                           meas_latency=64, seed=0x5EED, p1=0.5)
+    n = 10 ** 6
+    g = run_full(emu, ps, cfg, n, 0, ('summary', 'events', 'meas', 'hist'))
+    s = _abi.unpack_summary(g['summary'].view(np.uint32))
+    assert (s['status'] == _abi.ST_DONE).all() and (s['flags'] == 0).all()
+    assert int(g['hist'].sum()) == n
+
+
+@pytest.mark.parametrize('rank', [0, 7])
+def test_config3_shard_bit_exact(emu, rank):
+    ps = ProgramSet(workloads.config3_active_reset(8))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5)
+    n = 1250000
+    g = run_full(emu, ps, cfg, n, rank * n, ('summary', 'events', 'meas', 'hist'))
+    s = _abi.unpack_summary(g['summary'].view(np.uint32))
+    assert (s['status'] == _abi.ST_DONE).all()
+    assert int(g['hist'].sum()) == n
+    # the conditional X180 pair ran exactly where the first outcome was 1
+    flip = (s['meas_bits'] & 1).astype(bool)
+    assert (s['n_events'][flip] == s['n_events'][~flip].min() + 2).all()
+    assert abs(flip.mean() - 0.5) < 0.01
+
+
+def test_config5_full_launch_sampled_channels(emu):
+    import torch
+    n_seq = 128
+    ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=512, meas_cap=4,
+                           meas_latency=64, seed=0x5EED)
+    emu.load(ps)
+    ev = alloc_device_outputs(cfg, n_seq, want=('summary', 'events'))
+    ev['events'].zero_()
+    emu.run_device(cfg, n_seq, 0, ev)
+    torch.cuda.synchronize()
+    n_samples = ((int(ev['summary'][:, 0].max().item()) + 8) * 16 + 3) // 4 * 4
+    params = {i: (e['samples_per_clk'], e['interp_ratio']) for i, e in enumerate(workloads.ELEMS)}
+    chans = [(q, c, e) for q in range(n_seq) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
+    plan = ChannelPlan(ps, cfg, 0, n_seq, chans, params)
+    assert plan.n_channels == 2048 and n_samples > 200000
+    iq = emu.synthesize(plan, ev, n_samples)
+    torch.cuda.synchronize()
+    pick = np.sort(np.concatenate([np.arange(0, plan.n_channels, 16), np.arange(1, plan.n_channels, 16)]))
+    got = iq[torch.from_numpy(pick).cuda()].cpu().numpy().view(np.uint32)
+    ref = oracle.dds(plan.desc[pick], ev['summary'].cpu().numpy(), ev['events'].cpu().numpy(), plan.env, plan.freq,
+                     n_samples, cfg.event_cap, threads=THREADS)
+    if not np.array_equal(got, ref):
+        bad = np.argwhere(got != ref)
+        raise AssertionError('{} mismatching samples, first at channel {} sample {}'.format(
+            len(bad), int(pick[bad[0][0]]), int(bad[0][1])))
+    assert (ref[0::2] != 0).any(axis=1).all() and (ref[1::2] != 0).any(axis=1).all()   # qdrv and rdrv play
