@@ -22,6 +22,7 @@ def main():
     ap.add_argument('--seqs', type=int, default=128)
     ap.add_argument('--reps', type=int, default=4)
     ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--align', type=int, default=4, help='round n_samples up to a multiple of this')
     a = ap.parse_args()
     import torch
     from distributed_processor_amd import _abi, workloads
@@ -37,7 +38,7 @@ def main():
     emus[0].run_device(cfg, a.seqs, 0, ev)
     torch.cuda.synchronize()
     s = _abi.unpack_summary(ev['summary'].cpu().numpy().view(np.uint32))
-    n_samples = ((int(s['t_end'].max()) + 8) * 16 + 3) // 4 * 4
+    n_samples = ((int(s['t_end'].max()) + 8) * 16 + a.align - 1) // a.align * a.align
     params = {i: (e['samples_per_clk'], e['interp_ratio']) for i, e in enumerate(workloads.ELEMS)}
     chans = [(q, c, e) for q in range(a.seqs) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
     plan = ChannelPlan(ps, cfg, 0, a.seqs, chans, params)
@@ -83,7 +84,7 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         fills.append(t0.elapsed_time(t1) / a.steps)
-    print(json.dumps({'same_iq': same, 'GB': gb, 'fill_ms': float(np.median(fills)),
+    print(json.dumps({'same_iq': same, 'GB': gb, 'n_samples': n_samples, 'fill_ms': float(np.median(fills)),
                       'kernel_ms': {os.path.basename(l): float(np.median(k)) for l, k in zip(libs, kern)},
                       'kernel_min_ms': {os.path.basename(l): float(np.min(k)) for l, k in zip(libs, kern)},
                       'step_ms': {os.path.basename(l): float(np.median(k)) for l, k in zip(libs, step)}}))
