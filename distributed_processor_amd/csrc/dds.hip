@@ -7,7 +7,7 @@
 // sample, nothing else leaves the chip.
 //
 // Two launches per synthesis:
-//   * dds_index_kernel (one wave per channel) compacts the lane's strobes
+//   * dds_index_kernel (one workgroup per channel) compacts the lane's strobes
 //     of the channel's element and its pulse_resets (time-sorted: a core emits
 //     them in time order) once, channel-contiguous, and writes every sample
 //     tile's window of them (the records a tile's samples can see);
@@ -176,78 +176,79 @@ __device__ __forceinline__ uint32_t mix_y(uint32_t e, uint32_t ep, uint32_t y)
 }
 
 // ===========================================================================
-// Event index: one wave per channel, BLOCK / 64 channels per workgroup, no
-// workgroup barrier.  Each lane issues its event loads (one 16-B record per
-// event of the slot-major array) before the wave compacts them with ballot /
-// popc straight into the global index; the strobe / reset times also go to
-// the wave's LDS slice for the window searches.
+// Event index: one workgroup per channel.  Wave w owns events
+// [256 w, 256 w + 256) (4 per lane, all loaded up front), the four waves'
+// strobe / reset counts are scanned in LDS, each wave writes its records at its
+// offset in event order, then the 256 threads find the tile windows, one tile
+// each per pass (binary searches over the channel's LDS time arrays).  (One
+// wave per channel with per-lane tile cursors measured 1 % slower per step.)
 // ===========================================================================
 __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    const uint32_t wl = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t ch = blockIdx.x * (BLOCK / 64) + wv;
-    if (ch >= p.n_channels) return;                         // the whole wave
-    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn) + (uint64_t)wv * 2 * p.ev_lds;
+    __shared__ uint32_t s_cnt[2][BLOCK / 64];
+    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn);
     uint32_t *s_rs_t = s_st_t + p.ev_lds;
+    const uint32_t tid = threadIdx.x, wl = tid & 63u, wv = tid >> 6;
+    const uint32_t ch = blockIdx.x;
     const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
     const uint32_t lane = d[0], elem = d[1] & 3u, spc = d[2];
     const uint32_t n_ev = min(p.summary[8ull * lane + 2], p.event_cap);
     uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
     uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
     const uint64_t below = wl ? (~0ull >> (64 - wl)) : 0ull;
+    constexpr int K = DDS_MAX_EVENTS / BLOCK;           // events per lane
+    uint4 ev[K];
+    bool is_st[K], is_rs[K];
     uint32_t ns = 0, nr = 0;
-    constexpr int K = 8;
-    for (uint32_t e0 = 0; e0 < n_ev; e0 += 64 * K) {
-        uint4 ev[K];
 #pragma unroll
-        for (int k = 0; k < K; k++) {
-            const uint32_t e = e0 + 64 * k + wl;
-            ev[k] = e < n_ev ? p.events[(uint64_t)e * p.n_lanes + lane] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            const uint32_t e = e0 + 64 * k + wl;
-            const uint32_t kind = ev[k].y >> 28;
-            const bool is_st = e < n_ev && kind == 0u && ((ev[k].y >> 24) & 3u) == elem;
-            const bool is_rs = e < n_ev && kind == 1u;
-            const uint64_t bs = __ballot(is_st), br = __ballot(is_rs);
-            if (is_st) {
-                const uint32_t i = ns + (uint32_t)__popcll(bs & below);
-                xs[i] = make_uint4(ev[k].x, ev[k].y & 0xFFFFFFu, ev[k].z, ev[k].w & 0xFFFFu);
-                s_st_t[i] = ev[k].x;
-            }
-            if (is_rs) {
-                const uint32_t i = nr + (uint32_t)__popcll(br & below);
-                xr[i] = ev[k].x;
-                s_rs_t[i] = ev[k].x;
-            }
-            ns += (uint32_t)__popcll(bs);
-            nr += (uint32_t)__popcll(br);
-        }
+    for (int k = 0; k < K; k++) {
+        const uint32_t e = (wv * K + k) * 64u + wl;
+        ev[k] = e < n_ev ? p.events[(uint64_t)e * p.n_lanes + lane] : make_uint4(0, 0, 0, 0);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the wave's LDS writes before its reads
-    __builtin_amdgcn_wave_barrier();
-    const int n_st = (int)ns, n_rs = (int)nr;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t e = (wv * K + k) * 64u + wl;
+        const uint32_t kind = ev[k].y >> 28;
+        is_st[k] = e < n_ev && kind == 0u && ((ev[k].y >> 24) & 3u) == elem;
+        is_rs[k] = e < n_ev && kind == 1u;
+        ns += (uint32_t)__popcll(__ballot(is_st[k]));
+        nr += (uint32_t)__popcll(__ballot(is_rs[k]));
+    }
+    if (wl == 0) { s_cnt[0][wv] = ns; s_cnt[1][wv] = nr; }
+    __syncthreads();
+    uint32_t os = 0, orr = 0, n_st = 0, n_rs = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < BLOCK / 64; w++) {
+        os += w < wv ? s_cnt[0][w] : 0u;
+        orr += w < wv ? s_cnt[1][w] : 0u;
+        n_st += s_cnt[0][w];
+        n_rs += s_cnt[1][w];
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t bs = __ballot(is_st[k]), br = __ballot(is_rs[k]);
+        if (is_st[k]) {
+            const uint32_t i = os + (uint32_t)__popcll(bs & below);
+            xs[i] = make_uint4(ev[k].x, ev[k].y & 0xFFFFFFu, ev[k].z, ev[k].w & 0xFFFFu);
+            s_st_t[i] = ev[k].x;
+        }
+        if (is_rs[k]) {
+            const uint32_t i = orr + (uint32_t)__popcll(br & below);
+            xr[i] = ev[k].x;
+            s_rs_t[i] = ev[k].x;
+        }
+        os += (uint32_t)__popcll(bs);
+        orr += (uint32_t)__popcll(br);
+    }
+    __syncthreads();
     // window of tile c: from the latest record at or before its first cycle
-    // (the first record when none is) to the latest at or before its last.
-    // Lane wl takes a contiguous run of tiles: one binary search for its
-    // first tile, then cursors that only move forward (records are sorted)
-    const uint32_t per = (p.tiles + 63u) / 64u;
-    const uint32_t c_beg = min(wl * per, p.tiles), c_end = min(c_beg + per, p.tiles);
-    int a0 = 0, a1 = 0, b0 = 0, b1 = 0;          // records with t <= first / last cycle of the tile
-    for (uint32_t c = c_beg; c < c_end; c++) {
+    // (the first record when none is) to the latest at or before its last
+    for (uint32_t c = tid; c < p.tiles; c += BLOCK) {
         const uint64_t j0 = (uint64_t)c * DDS_TILE, j1 = min(j0 + DDS_TILE, (uint64_t)p.n_samples) - 1;
         const uint32_t n0 = (uint32_t)(j0 / spc), n1 = (uint32_t)(j1 / spc);
-        if (c == c_beg) {
-            a0 = last_le(s_st_t, n_st, n0) + 1; a1 = last_le(s_st_t, n_st, n1) + 1;
-            b0 = last_le(s_rs_t, n_rs, n0) + 1; b1 = last_le(s_rs_t, n_rs, n1) + 1;
-        } else {
-            while (a0 < n_st && s_st_t[a0] <= n0) a0++;
-            while (a1 < n_st && s_st_t[a1] <= n1) a1++;
-            while (b0 < n_rs && s_rs_t[b0] <= n0) b0++;
-            while (b1 < n_rs && s_rs_t[b1] <= n1) b1++;
-        }
+        const int a0 = last_le(s_st_t, (int)n_st, n0) + 1, a1 = last_le(s_st_t, (int)n_st, n1) + 1;
+        const int b0 = last_le(s_rs_t, (int)n_rs, n0) + 1, b1 = last_le(s_rs_t, (int)n_rs, n1) + 1;
         const int sl = max(a0 - 1, 0), rl = max(b0 - 1, 0);
         p.win[(uint64_t)ch * p.tiles + c] = make_uint4((uint32_t)sl, (uint32_t)(a1 - sl), (uint32_t)rl,
                                                       (uint32_t)(b1 - rl));
@@ -606,12 +607,8 @@ static hipError_t opt_in_lds(const void *fn, uint32_t bytes, uint32_t *granted)
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    const uint32_t ilds = (BLOCK / 64) * 2 * p.ev_lds * 4;   // per wave: strobe and reset times
-    static uint32_t granted = 0;
-    const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_index_kernel), ilds, &granted);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(dds_index_kernel, dim3((p.n_channels + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), ilds,
-                       stream, p);
+    // the channel's strobe and reset times: 2 * ev_lds words <= 8 KiB
+    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), 2 * p.ev_lds * 4, stream, p);
     return hipGetLastError();
 }
 
