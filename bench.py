@@ -129,13 +129,15 @@ def hbm_roofline(alg_bytes, kernel_ms, ms_per_step, kernel, prof, rocprof_key):
     """HBM roofline of a kernel: algorithmic bytes / kernel time.  The kernel
     time is the median HIP-event duration of the launches, capped at the
     step's own time (the event pair cannot make the kernel longer than the
-    whole step); the committed rocprof average gives a second fraction"""
+    whole step); the committed rocprofv3 kernel-trace average of this leg's
+    launch shape (profiles/<tag>_<leg>_pmc.json duration_ns; else the
+    kernel's --stats row) gives a second fraction"""
     k_ms = min(kernel_ms, ms_per_step)
     gbs = alg_bytes / (k_ms * 1e-3) / 1e9
     r = {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS,
          'traffic': prof.get('hbm_bytes_per_launch') if prof else None, 'bytes_per_launch': alg_bytes,
          'kernel_ms': k_ms, 'kernel_ms_events': kernel_ms, 'kernel': kernel}
-    rp = rocprof_avg_ms(rocprof_key)
+    rp = prof['duration_ns'] * 1e-6 if prof and prof.get('duration_ns') else rocprof_avg_ms(rocprof_key)
     if rp:
         r['kernel_ms_rocprof'] = rp
         r['frac_rocprof'] = alg_bytes / (rp * 1e-3) / 1e9 / HBM_PEAK_GBS
@@ -228,13 +230,14 @@ def block_pass(launch, k):
 
 
 def interp_kernel_ms(emu, cfg, n, shot0, out, stream, steps, step, drain):
-    """the interpreter kernel's time per launch: a block of back-to-back
-    launches without the histogram (whose zeroing / reduction are separate
-    launches of the step), beside the per-launch event median"""
+    """the interpreter kernel's time per launch: the median of the library's
+    HIP-event pairs around the kernel inside `steps` real steps (the same
+    launch as the timed ones; it agrees with rocprofv3's average), beside a
+    block of back-to-back launches without the histogram output"""
     nohist = {k: v for k, v in out.items() if k != 'hist'}
     ev = kernel_pass(emu, steps, step, drain)
     blk = block_pass(lambda: emu.run_device(cfg, n, shot0, nohist, stream), max(steps, 10))
-    return blk, ev
+    return ev, blk
 
 
 def fill_gbps(device='cuda'):
@@ -274,7 +277,7 @@ def leg_ramsey(emu, args, world, rank, stream):
         emu.run_device(cfg, n, shot0, out, stream)
     step = lambda: pipe.step(launch)
     dt = timed(step, pipe.drain, args.steps, args.warmup, world)
-    kernel_ms, kernel_ms_ev = interp_kernel_ms(emu, cfg, n, shot0, out, stream, args.steps, step, pipe.drain)
+    kernel_ms, kernel_ms_blk = interp_kernel_ms(emu, cfg, n, shot0, out, stream, args.steps, step, pipe.drain)
     kernel = emu.last_kernel()
     # accounting from the last step's outputs (identical every step)
     summ = out['summary'].cpu().numpy().view(np.uint32)
@@ -291,7 +294,7 @@ def leg_ramsey(emu, args, world, rank, stream):
     alg = float(bytes_per_lane(summ, cfg).sum())
     prof = pmc('ramsey')
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'straight_kernel')
-    roof['kernel_ms_events'] = kernel_ms_ev
+    roof['kernel_ms_block'] = kernel_ms_blk
     roof['valu'] = valu_view(prof)
     res = {'value': n * 8 * world * args.steps / dt, 'ms_per_step': ms_step,
            'shots_per_s': n * world * args.steps / dt,
@@ -386,7 +389,7 @@ def leg_active_reset(emu, args, world, rank, stream):
     step = lambda: pipe.step(launch)
     dt = timed(step, pipe.drain, args.steps, args.warmup, world)
     kernel = emu.last_kernel()
-    kernel_ms, kernel_ms_ev = interp_kernel_ms(emu, cfg, n, shot0, out, stream, args.steps, step, pipe.drain)
+    kernel_ms, kernel_ms_blk = interp_kernel_ms(emu, cfg, n, shot0, out, stream, args.steps, step, pipe.drain)
     summ = out['summary'].cpu().numpy().view(np.uint32)
     s = _abi.unpack_summary(summ)
     assert (s['status'] == _abi.ST_DONE).all(), 'config 3: not every lane reached DONE'
@@ -395,7 +398,7 @@ def leg_active_reset(emu, args, world, rank, stream):
     prof = pmc('active_reset')
     ms_step = dt / args.steps * 1e3
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'branch_kernel')
-    roof['kernel_ms_events'] = kernel_ms_ev
+    roof['kernel_ms_block'] = kernel_ms_blk
     roof['valu'] = valu_view(prof)
     res = {'metric': 'emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
                      '1.25e6 shots/GPU)',
@@ -445,7 +448,7 @@ def leg_rb(emu, args, world, rank, stream):
     steps = max(1, args.steps // 4)
     dt = timed(step, pipe.drain, steps, min(args.warmup, 2), world)
     kernel = emu.last_kernel()
-    kernel_ms, kernel_ms_ev = interp_kernel_ms(emu, cfg, n, shot0, out, stream, steps, step, pipe.drain)
+    kernel_ms, kernel_ms_blk = interp_kernel_ms(emu, cfg, n, shot0, out, stream, steps, step, pipe.drain)
     summ = out['summary'].cpu().numpy().view(np.uint32)
     s = _abi.unpack_summary(summ)
     assert (s['status'] == _abi.ST_DONE).all(), 'config 4: not every lane reached DONE'
@@ -456,7 +459,7 @@ def leg_rb(emu, args, world, rank, stream):
     prof = pmc('rb')
     alg = float(bytes_per_lane(summ, cfg).sum())
     hbm = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'macro_kernel')
-    hbm['kernel_ms_events'] = kernel_ms_ev
+    hbm['kernel_ms_block'] = kernel_ms_blk
     if prof and prof.get('SQ_INSTS_VALU'):
         valu_per_launch = float(prof['SQ_INSTS_VALU'])
         achieved = valu_per_launch / (k_ms * 1e-3)

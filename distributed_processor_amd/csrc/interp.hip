@@ -571,39 +571,54 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
 
 // out[i] += sum of the R replicas; thread = (bin, slice of 8 replicas), loads independent
 // hist[i] (+)= the sum of the R replicas' bin i; every replica word read is
-// left zero for the next run.  Adding: slices of 8 replicas per thread and a
-// u64 atomic each; storing (hist_assign): one thread per bin sums all R
+// left zero for the next run.  A thread sums one slice of 8 replicas of one
+// bin.  Adding: a u64 atomic per slice.  Storing (hist_assign): the G >=
+// slices lanes of a bin are adjacent, their sums are combined with
+// cross-lane shuffles and the group's first lane stores the bin.
 __global__ void __launch_bounds__(BLOCK) hist_reduce_kernel(uint32_t *rep, uint32_t R, uint64_t stride,
-                                                           uint64_t bins, bool store, unsigned long long *hist)
+                                                           uint64_t bins, uint32_t G, unsigned long long *hist)
 {
-    const uint32_t per = store ? R : 8u;
-    const uint32_t slices = (R + per - 1) / per;
-    const uint64_t n = bins * slices;
-    for (uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; x < n; x += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t i = x % bins;
-        const uint32_t r0 = (uint32_t)(x / bins) * per, r1 = min(r0 + per, R);
+    const uint32_t slices = (R + 7) / 8;
+    const uint32_t per = G ? G : slices;                     // threads per bin
+    const uint64_t n = bins * per;
+    for (uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; x - threadIdx.x < n; x += (uint64_t)gridDim.x * BLOCK) {
+        const bool in = x < n;
+        const uint64_t i = G ? x / G : x % bins;
+        const uint32_t sl = G ? (uint32_t)(x % G) : (uint32_t)(x / bins);
+        const uint32_t r0 = sl * 8;
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = (in && r0 + k < R) ? rep[(uint64_t)(r0 + k) * stride + i] : 0u;
         unsigned long long acc = 0;
-        for (uint32_t rb = r0; rb < r1; rb += 8) {
-            uint32_t v[8];
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = (rb + k < r1) ? rep[(uint64_t)(rb + k) * stride + i] : 0u;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                acc += v[k];
-                if (v[k]) rep[(uint64_t)(rb + k) * stride + i] = 0u;
-            }
+        for (int k = 0; k < 8; k++) {
+            acc += v[k];
+            if (v[k]) rep[(uint64_t)(r0 + k) * stride + i] = 0u;
         }
-        if (store) hist[i] = acc;
-        else if (acc) atomicAdd(&hist[i], acc);
+        if (G) {                                             // uniform: every lane of the wave shuffles
+            for (uint32_t m = 1; m < G; m <<= 1) {
+                const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)acc, (int)m, 64);
+                const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), (int)m, 64);
+                acc += ((unsigned long long)hi << 32) | lo;
+            }
+            if (in && sl == 0) hist[i] = acc;
+        } else if (in && acc) {
+            atomicAdd(&hist[i], acc);
+        }
     }
 }
 
 hipError_t launch_hist_reduce(uint32_t *rep, uint32_t R, uint64_t stride, uint64_t bins, bool assign,
                               unsigned long long *hist, hipStream_t stream)
 {
-    const uint64_t n = bins * (assign ? 1u : (R + 7) / 8);
+    uint32_t G = 0;                                          // storing: lanes per bin, a power of two >= slices
+    if (assign) {
+        G = 1;
+        while (G < (R + 7) / 8) G <<= 1;                     // R <= 64: G <= 8
+    }
+    const uint64_t n = bins * (assign ? G : (R + 7) / 8);
     const uint64_t blocks = std::min<uint64_t>((n + BLOCK - 1) / BLOCK, 8192);
-    hipLaunchKernelGGL(hist_reduce_kernel, dim3((uint32_t)blocks), dim3(BLOCK), 0, stream, rep, R, stride, bins, assign,
+    hipLaunchKernelGGL(hist_reduce_kernel, dim3((uint32_t)blocks), dim3(BLOCK), 0, stream, rep, R, stride, bins, G,
                        hist);
     return hipGetLastError();
 }
