@@ -137,7 +137,7 @@ def hbm_roofline(alg_bytes, kernel_ms, ms_per_step, kernel, prof, rocprof_key):
     r = {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS,
          'traffic': prof.get('hbm_bytes_per_launch') if prof else None, 'bytes_per_launch': alg_bytes,
          'kernel_ms': k_ms, 'kernel_ms_events': kernel_ms, 'kernel': kernel}
-    rp = prof['duration_ns'] * 1e-6 if prof and prof.get('duration_ns') else rocprof_avg_ms(rocprof_key)
+    rp = (prof['duration_ns'] * 1e-6 if prof.get('duration_ns') else rocprof_avg_ms(rocprof_key)) if prof else None
     if rp:
         r['kernel_ms_rocprof'] = rp
         r['frac_rocprof'] = alg_bytes / (rp * 1e-3) / 1e9 / HBM_PEAK_GBS
@@ -155,19 +155,33 @@ def bytes_per_lane(summary_np, cfg):
 SETTLE_S = 0.3
 
 
-def settle(step, drain, seconds=SETTLE_S):
-    """untimed steps for `seconds` of wall time, synchronised every 10 steps:
-    the GPU's clocks ramp up under load, and a leg that starts after an idle
-    host-side phase would otherwise time its first milliseconds at low clocks
-    (config 2 measured 0.202 ms per step cold against 0.176-0.179 warm,
-    scripts/step_probe.py)"""
-    import torch
-    t_end = time.perf_counter() + seconds
-    while time.perf_counter() < t_end:
-        for _ in range(10):
-            step()
-        drain()
-        torch.cuda.synchronize()
+def settle(step, drain, seconds=SETTLE_S, sync=None, device='cuda'):
+    """untimed steps for about `seconds` of wall time: the GPU's clocks ramp
+    up under load, and a leg that starts after an idle host-side phase would
+    otherwise time its first milliseconds at low clocks (config 2 measured
+    0.202 ms per step cold against 0.176-0.179 warm, scripts/step_probe.py).
+    Every rank runs the SAME number of steps (a step may enqueue a
+    collective): the count comes from 3 timed steps, maxed over ranks."""
+    from distributed_processor_amd import sharding
+    if sync is None:
+        import torch
+        sync = torch.cuda.synchronize
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        step()
+    drain()
+    sync()
+    per = (time.perf_counter() - t0) / 3
+    n = int(sharding.max_over_ranks(float(int(seconds / max(per, 1e-6))), device=device))
+    for i in range(n):
+        step()
+        if i % 10 == 9:
+            drain()
+            sync()
+    drain()
+    sync()
+    return n + 3
 
 
 def timed(step, drain, steps, warmup, world):
@@ -292,7 +306,7 @@ def leg_ramsey(emu, args, world, rank, stream):
     assert gathered.shape[0] == world and torch.equal(gathered[rank], sample)
     ms_step = dt / args.steps * 1e3
     alg = float(bytes_per_lane(summ, cfg).sum())
-    prof = pmc('ramsey')
+    prof = pmc('ramsey') if args.shots == 10 ** 6 else None         # profiled at the default size only
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'straight_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
     roof['valu'] = valu_view(prof)
@@ -339,7 +353,7 @@ def leg_dds(emu, args, world, rank, stream):
     kernel_ms = kernel_pass(emu, args.steps, step, lambda: None)
     samples = plan.n_channels * n_samples
     ms_step = dt / args.steps * 1e3
-    prof = pmc('dds')
+    prof = pmc('dds') if args.dds_seqs == 128 else None
     roof = hbm_roofline(samples * 4, kernel_ms, ms_step, 'dpemu::dds_tile_kernel', prof, 'dds_tile_kernel')
     res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
            'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s', 'ms_per_step': ms_step,
@@ -395,7 +409,7 @@ def leg_active_reset(emu, args, world, rank, stream):
     assert (s['status'] == _abi.ST_DONE).all(), 'config 3: not every lane reached DONE'
     assert int(pipe.result().sum().item()) == n * world
     alg = float(bytes_per_lane(summ, cfg).sum())
-    prof = pmc('active_reset')
+    prof = pmc('active_reset') if args.ar_shots == 1250000 else None
     ms_step = dt / args.steps * 1e3
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'branch_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
@@ -456,7 +470,7 @@ def leg_rb(emu, args, world, rank, stream):
     instrs = float(s['n_instr'].astype(np.float64).sum())
     ms_step = dt / steps * 1e3
     k_ms = min(kernel_ms, ms_step)
-    prof = pmc('rb')
+    prof = pmc('rb') if (args.rb_seqs, args.rb_spg) == (100000, 10) else None
     alg = float(bytes_per_lane(summ, cfg).sum())
     hbm = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'macro_kernel')
     hbm['kernel_ms_block'] = kernel_ms_blk

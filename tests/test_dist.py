@@ -170,3 +170,37 @@ def test_pipeline_assigning_launch_skips_zeroing():
     acc = sharding.HistogramPipeline(torch.full((2,), 7, dtype=torch.int64), n_buffers=1, zero=False)
     acc.step(lambda t: t.add_(1))
     assert acc.result().tolist() == [8, 8]
+
+
+def _settle_main(rank, world, port, out_dir):
+    """bench.settle on both ranks with a step that enqueues a collective and
+    runs at a different speed per rank: the ranks must agree on the step count
+    (a mismatch deadlocks the collectives, as an uneven wall-time loop did)"""
+    import sys
+    import time
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        t = torch.zeros(1)
+        count = [0]
+
+        def step():
+            time.sleep(0.002 * (rank + 1))
+            dist.all_reduce(t)
+            count[0] += 1
+        n = bench.settle(step, lambda: None, seconds=0.1, sync=lambda: None, device='cpu')
+        dist.barrier()
+        np.save(os.path.join(out_dir, 'settle{}.npy'.format(rank)), np.array([n, count[0]]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_settle_same_step_count_on_every_rank(tmp_path):
+    world = 2
+    mp.start_processes(_settle_main, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method='spawn')
+    got = [np.load(tmp_path / 'settle{}.npy'.format(r)) for r in range(world)]
+    assert got[0][0] == got[1][0] == got[0][1] == got[1][1] > 3
