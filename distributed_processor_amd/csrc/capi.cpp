@@ -535,6 +535,9 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     }
     if (out->hist && !p.hist_rep && cfg->hist_assign)      // direct atomics: assign = zero, then add
         HIPCHK(ctx, hipMemsetAsync(out->hist, 0, bins * sizeof(uint64_t), stream));
+    // from the main launch until the reduce is enqueued the replicas may hold
+    // counts: a failure in between leaves them to the next run's memset
+    if (p.hist_rep) ctx->hist_rep_dirty = true;
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
@@ -556,7 +559,6 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
         ctx->last_kernel = name;
     }
     if (out->hist && p.hist_rep) {
-        ctx->hist_rep_dirty = true;          // until the reduce is enqueued
         HIPCHK(ctx, launch_hist_reduce(ctx->d_hist_rep, R, hist_stride, bins, cfg->hist_assign != 0,
                                        reinterpret_cast<unsigned long long *>(out->hist), stream));
         ctx->hist_rep_dirty = false;
