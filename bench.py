@@ -47,6 +47,9 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s
 VALU_PEAK = 7.7e11             # wave64 integer-VALU instructions/s, measured (profiles/r01_valu_peak.jsonl)
 PROFILE_TAG = 'r02'            # profiles/<tag>_*: rocprofv3 kernel stats and PMC passes of this bench
+# where they are read from: the committed profiles/, or (DPEMU_BENCH_PROFILES)
+# the summaries of a profile pass just taken on the same box
+PROFILE_DIR = os.environ.get('DPEMU_BENCH_PROFILES') or os.path.join(REPO, 'profiles')
 
 
 # ---------------------------------------------------------------------------- helpers
@@ -101,7 +104,7 @@ def cpu_baselines(ps, cfg, horizon, what):
 
 def pmc(name):
     """per-launch PMC summary of a kernel from profiles/<tag>_<name>_pmc.json (scripts/pmc_summary.py)"""
-    path = os.path.join(REPO, 'profiles', '{}_{}_pmc.json'.format(PROFILE_TAG, name))
+    path = os.path.join(PROFILE_DIR, '{}_{}_pmc.json'.format(PROFILE_TAG, name))
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -110,7 +113,7 @@ def pmc(name):
 
 def rocprof_avg_ms(kernel_substr):
     """the committed rocprofv3 --stats average of a kernel (profiles/<tag>_*kernel_stats.csv)"""
-    for path in sorted(glob.glob(os.path.join(REPO, 'profiles', PROFILE_TAG + '*kernel_stats.csv'))):
+    for path in sorted(glob.glob(os.path.join(PROFILE_DIR, PROFILE_TAG + '*kernel_stats.csv'))):
         with open(path) as f:
             for r in csv.DictReader(f):
                 if kernel_substr in r.get('Name', ''):
