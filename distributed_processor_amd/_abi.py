@@ -4,7 +4,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_CORES = 64
 MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
 
@@ -12,6 +12,7 @@ ST_DONE, ST_MAX_CYCLES, ST_HUNG_OPCODE, ST_DEADLOCK = 1, 2, 3, 4
 F_LATE, F_EVENT_OVF, F_TRACE_OVF, F_MEAS_OVF, F_DOUBLE_STROBE, F_GUARD = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 FPROC_MEAS, FPROC_LUT = 0, 1
 MEAS_STATE, MEAS_READOUT = 0, 1
+LANES_CORE_MAJOR, LANES_SHOT_MAJOR = 0, 1
 EV_STROBE, EV_PULSE_RESET = 0, 1
 TRACE_QCLK_LOAD, TRACE_QCLK_RST = 16, 17
 MAX_CYCLES_LIMIT = 2 ** 31 - 64
@@ -36,7 +37,7 @@ class Config(C.Structure):
                 ('lut_mask', C.c_uint32), ('meas_model', C.c_uint32),
                 ('p1_threshold', C.c_uint32 * MAX_CORES), ('lut_table', C.c_uint64 * 256),
                 ('ro_sep', C.c_int32), ('ro_sigma', C.c_uint32), ('ro_thr', C.c_int32),
-                ('ro_win', C.c_uint32), ('hist_assign', C.c_uint32), ('reserved', C.c_uint32)]
+                ('ro_win', C.c_uint32), ('hist_assign', C.c_uint32), ('lane_order', C.c_uint32)]
 
 
 class Outputs(C.Structure):
@@ -58,11 +59,13 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
                 event_cap=64, trace_cap=0, meas_cap=8, fproc_mode=FPROC_MEAS, meas_elem=2,
                 meas_latency=64, sync_latency=1, sync_mask=0, seed=0x5EED, p1=0.5,
                 lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE, exec_flags=0, readout=None,
-                hist_assign=False):
+                hist_assign=False, lane_order=LANES_CORE_MAJOR):
     """Validated Config.  p1: float or per-core list of P(state = 1).
     readout: None (outcome = prepared state) or dict(sep=, sigma=, thr=) for the
     readout model of include/dpemu.h (sigma a float noise scale, stored Q16).
-    hist_assign: a run writes its outcome histogram instead of adding to it."""
+    hist_assign: a run writes its outcome histogram instead of adding to it.
+    lane_order: LANES_CORE_MAJOR (lane = core * n_shots + shot) or
+    LANES_SHOT_MAJOR (lane = shot * C + core)."""
     C_ = int(cores_per_shot)
     if C_ < 1 or C_ > MAX_CORES or (C_ & (C_ - 1)):
         raise ValueError('cores_per_shot must be a power of two in [1, 64]')
@@ -93,6 +96,9 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
     cfg.lut_mask = int(lut_mask)
     cfg.exec_flags = int(exec_flags)
     cfg.hist_assign = 1 if hist_assign else 0
+    if lane_order not in (LANES_CORE_MAJOR, LANES_SHOT_MAJOR):
+        raise ValueError('lane_order must be LANES_CORE_MAJOR or LANES_SHOT_MAJOR')
+    cfg.lane_order = int(lane_order)
     ps = list(p1) if isinstance(p1, (list, tuple, np.ndarray)) else [p1] * C_
     for c, p in enumerate(ps):
         cfg.p1_threshold[c] = prob_to_threshold(p)
@@ -124,16 +130,24 @@ def prob_to_threshold(p):
 OUTPUT_NAMES = ('summary', 'events', 'trace', 'meas', 'regs', 'hist')
 
 
-def lane_index(shot_local, core, n_shots):
-    """output lane of (shot - shot_begin, core) in a run of n_shots shots:
-    core-major, L = core * n_shots + shot_local (include/dpemu.h)"""
+def lane_index(shot_local, core, n_shots, cores_per_shot=None, lane_order=LANES_CORE_MAJOR):
+    """output lane of (shot - shot_begin, core) in a run of n_shots shots
+    (include/dpemu.h): core-major L = core * n_shots + shot_local, or
+    shot-major L = shot_local * C + core"""
+    if lane_order == LANES_SHOT_MAJOR:
+        return np.asarray(shot_local) * int(cores_per_shot) + np.asarray(core)
     return np.asarray(core) * int(n_shots) + np.asarray(shot_local)
 
 
-def by_shot(arr, cores_per_shot, axis=0):
-    """view of a per-lane array with the lane axis split into (core, shot)"""
+def by_shot(arr, cores_per_shot, axis=0, lane_order=LANES_CORE_MAJOR):
+    """per-lane array with the lane axis split into (core, shot), whatever
+    the lane order (a view for core-major lanes)"""
     a = np.asarray(arr)
-    shp = a.shape[:axis] + (cores_per_shot, a.shape[axis] // cores_per_shot) + a.shape[axis + 1:]
+    n = a.shape[axis] // cores_per_shot
+    if lane_order == LANES_SHOT_MAJOR:
+        shp = a.shape[:axis] + (n, cores_per_shot) + a.shape[axis + 1:]
+        return np.swapaxes(a.reshape(shp), axis, axis + 1)
+    shp = a.shape[:axis] + (cores_per_shot, n) + a.shape[axis + 1:]
     return a.reshape(shp)
 
 

@@ -344,8 +344,9 @@ static int validate(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t n_shots, b
         return fail(ctx, DPEMU_E_INVALID, "meas_latency / sync_latency must be in [1, 2^20]");
     if (cfg->meas_model != DPEMU_MEAS_STATE && cfg->meas_model != DPEMU_MEAS_READOUT)
         return fail(ctx, DPEMU_E_INVALID, "meas_model must be DPEMU_MEAS_STATE or DPEMU_MEAS_READOUT");
-    if (cfg->hist_assign > 1 || cfg->reserved)
-        return fail(ctx, DPEMU_E_INVALID, "hist_assign must be 0 or 1 and reserved 0");
+    if (cfg->hist_assign > 1) return fail(ctx, DPEMU_E_INVALID, "hist_assign must be 0 or 1");
+    if (cfg->lane_order > DPEMU_LANES_SHOT_MAJOR)
+        return fail(ctx, DPEMU_E_INVALID, "lane_order %u is not DPEMU_LANES_CORE_MAJOR / SHOT_MAJOR", cfg->lane_order);
     if (cfg->ro_win >= 4096)
         return fail(ctx, DPEMU_E_INVALID, "ro_win %u must fit the 12-bit envelope-length field", cfg->ro_win);
     if ((uint64_t)cfg->max_cycles + cfg->meas_latency + 16 >= 0x80000000ull)
@@ -398,6 +399,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.shot_begin = shot_begin;
     p.n_lanes = (uint32_t)(n_shots * C);
     p.n_shots = (uint32_t)n_shots;
+    p.shot_major = cfg->lane_order == DPEMU_LANES_SHOT_MAJOR;
     p.C = C;
     p.log2C = 0;
     while ((1u << p.log2C) < C) p.log2C++;

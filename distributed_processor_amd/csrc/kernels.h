@@ -120,6 +120,7 @@ struct KParams {
     // run
     uint64_t shot_begin;
     uint32_t n_lanes, n_shots, C, log2C, n_groups, shots_per_group;
+    uint32_t shot_major;          // dpemu_config.lane_order: lane = shot * C + core (else core * n_shots + shot)
     uint32_t grp_g0, grp_r0;      // (shot_begin / spg) % n_groups, shot_begin % spg
     uint32_t max_cycles, event_cap, trace_cap, meas_cap;
     uint32_t fproc_mode, meas_elem, meas_latency, sync_latency;

@@ -103,10 +103,11 @@ __device__ __forceinline__ uint32_t group_step(const KParams &p, uint32_t sp, ui
     return (uint32_t)(a - b);
 }
 
-// output lane of (run shot sl, core): core-major (include/dpemu.h)
+// output lane of (run shot sl, core) (include/dpemu.h): core-major, or
+// shot-major with lane_order DPEMU_LANES_SHOT_MAJOR
 __device__ __forceinline__ uint32_t out_lane(const KParams &p, uint32_t sl, uint32_t core)
 {
-    return core * p.n_shots + sl;
+    return p.shot_major ? (sl << p.log2C) + core : core * p.n_shots + sl;
 }
 
 // the 16-B event record (include/dpemu.h): pulse_iface snapshot at cycle te
@@ -158,15 +159,27 @@ __device__ __forceinline__ uint32_t stage_programs(const KParams &p, uint4 *s_pr
 
 // Thread -> (shot, core) of the branch-free kernels (straight.hip, macro.hip):
 // workgroup b covers the run's shots [b S, (b + 1) S), S = BLOCK / C, all C
-// cores, CORE-major inside the workgroup (thread = core * S + shot), so a
-// wave's lanes are consecutive shots of one core -- consecutive output lanes:
-// every event / summary store of a wave is one contiguous run (the
-// interpreter with fproc / sync keeps a shot's cores in one wave instead).
+// cores, in the output's lane order inside the workgroup: core-major lanes
+// (thread = core * S + shot) put consecutive shots of one core in a wave,
+// shot-major lanes (thread = shot * C + core) whole shots -- either way a
+// wave's lanes are consecutive output lanes, so every event / summary store
+// of a wave is one contiguous run.  The slot of the thread's shot in the
+// workgroup (count_outcome_block) is shot_slot.
 __device__ __forceinline__ void block_core_major(const KParams &p, uint32_t &sl, uint32_t &core)
 {
     const uint32_t S_log2 = 8u - p.log2C;                // BLOCK = 256
-    core = threadIdx.x >> S_log2;
-    sl = (blockIdx.x << S_log2) + (threadIdx.x & ((1u << S_log2) - 1u));
+    if (p.shot_major) {
+        core = threadIdx.x & (p.C - 1u);
+        sl = (blockIdx.x << S_log2) + (threadIdx.x >> p.log2C);
+    } else {
+        core = threadIdx.x >> S_log2;
+        sl = (blockIdx.x << S_log2) + (threadIdx.x & ((1u << S_log2) - 1u));
+    }
+}
+
+__device__ __forceinline__ uint32_t shot_slot(const KParams &p)
+{
+    return p.shot_major ? threadIdx.x >> p.log2C : threadIdx.x & ((1u << (8u - p.log2C)) - 1u);
 }
 
 // the outcome histogram for block_core_major workgroups: each lane ORs its
@@ -177,12 +190,13 @@ __device__ __forceinline__ void count_outcome_block(const KParams &p, uint32_t *
 {
     if (!p.hist && !p.hist_rep) return;                  // uniform
     const uint32_t tid = threadIdx.x, S_log2 = 8u - p.log2C, S = 1u << S_log2;
+    const uint32_t slot = shot_slot(p);
     if (tid < S) s_key[tid] = 0u;
     __syncthreads();
-    if (valid && last_bit) atomicOr(&s_key[tid & (S - 1u)], 1u << core);
+    if (valid && last_bit) atomicOr(&s_key[slot], 1u << core);
     __syncthreads();
     const bool mine = valid && core == 0u;               // thread (core 0, shot): the shot's count
-    const uint32_t key = mine ? s_key[tid] : 0u;
+    const uint32_t key = mine ? s_key[slot] : 0u;
     const uint64_t bin = (uint64_t)grp * (1ull << p.C) + key;
     if (p.hist_rep) {
         uint32_t *rep = p.hist_rep + (uint64_t)(blockIdx.x % p.hist_reps) * p.hist_stride;

@@ -71,7 +71,8 @@ class ChannelPlan:
             (eo, el), n_env = place(np.ascontiguousarray(env, np.uint32), envs, env_at, n_env)
             (fo, fl), n_freq = place(np.ascontiguousarray(frq, np.uint32), freqs, freq_at, n_freq)
             spc, interp = elem_params[elem]
-            rows.append((core * int(n_shots) + (shot - shot_begin), elem, spc, interp, eo, el, fo, fl))
+            lane = int(_abi.lane_index(shot - shot_begin, core, n_shots, C_, cfg.lane_order))
+            rows.append((lane, elem, spc, interp, eo, el, fo, fl))
         self.desc = np.array(rows, np.uint32).reshape(-1, 8)
         self.env = np.concatenate(envs).astype(np.uint32) if n_env else np.zeros(1, np.uint32)
         self.freq = np.concatenate(freqs).astype(np.uint32) if n_freq else np.zeros(1, np.uint32)

@@ -146,8 +146,9 @@ class EmulationResult:
         return self.n_shots * self.cfg.cores_per_shot
 
     def lane(self, shot, core):
-        """output lane of (absolute shot, core): core-major (include/dpemu.h)"""
-        return int(_abi.lane_index(shot - self.shot_begin, core, self.n_shots))
+        """output lane of (absolute shot, core) in the run's lane order (include/dpemu.h)"""
+        return int(_abi.lane_index(shot - self.shot_begin, core, self.n_shots, self.cfg.cores_per_shot,
+                                   self.cfg.lane_order))
 
     def events(self, shot, core) -> np.ndarray:
         """structured events of one lane: t, env_word, cfg, kind, phase, freq, amp"""

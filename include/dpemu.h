@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DPEMU_ABI_VERSION 5
+#define DPEMU_ABI_VERSION 6
 
 /* ---- error codes ---------------------------------------------------- */
 #define DPEMU_OK            0
@@ -129,18 +129,25 @@ typedef struct dpemu_config {
     uint32_t ro_win;           /* reference readout window (env words, < 4096); 0 = amplitude only */
     uint32_t hist_assign;      /* 0: out->hist += this run's counts; 1: out->hist = this run's
                                   counts (no separate zeroing launch before each run)        */
-    uint32_t reserved;         /* 0 */
+    uint32_t lane_order;       /* DPEMU_LANES_CORE_MAJOR (0) or DPEMU_LANES_SHOT_MAJOR (1), below */
 } dpemu_config;
 
 #define DPEMU_MEAS_STATE   0
 #define DPEMU_MEAS_READOUT 1
+
+/* lane order of every per-lane output (dpemu_config.lane_order) */
+#define DPEMU_LANES_CORE_MAJOR 0  /* lane = core * n_shots + (shot - shot_begin)                  */
+#define DPEMU_LANES_SHOT_MAJOR 1  /* lane = (shot - shot_begin) * C + core: a shot's cores adjacent */
 
 #define DPEMU_MAX_EVENT_CAP (1u << 20)   /* event / trace slots per lane (validate)  */
 
 /*
  * Lanes: lane L = core * n_shots + (shot - shot_begin) -- core-major, so the
  * lanes of one core's shots are adjacent (the lanes that run one program in
- * lockstep write whole cache lines).
+ * lockstep write whole cache lines) -- or, with lane_order SHOT_MAJOR,
+ * L = (shot - shot_begin) * C + core (a shot's cores adjacent: the layout the
+ * fproc / sync interpreter writes as whole lines, since a wave holds whole
+ * shots).
  *
  * Per-lane summary, 8 x u32:
  *   w0 t_end      decode cycle of DONE (done_gate from t_end+1) or of the stop

@@ -46,7 +46,7 @@ typedef struct {
     uint32_t status, flags, n_instr_exec, n_events, n_trace, n_meas, meas_bits, last_bit;
     uint32_t t_end, ip_end, qclk_end;
     uint32_t mt[MEAS_LOOKUP]; uint8_t mb[MEAS_LOOKUP];   /* measurement (valid cycle, bit) */
-    uint32_t lane;                   /* output lane index (core-major) */
+    uint32_t lane;                   /* output lane index (cfg->lane_order) */
     uint32_t core;
 } flane;
 
@@ -457,7 +457,8 @@ int fast_run(const dpemu_config *cfg, const uint32_t *words, const uint32_t *off
             l->prog = words + 4 * (uint64_t)offsets[p];
             l->n_instr = n_instr[p];
             l->qa_t = 1; l->qa_q = 0;
-            l->lane = (uint32_t)((uint64_t)c * n_shots + (uint64_t)si);   /* core-major lanes */
+            l->lane = cfg->lane_order == DPEMU_LANES_SHOT_MAJOR      /* include/dpemu.h lane order */
+                          ? (uint32_t)((uint64_t)si * C + c) : (uint32_t)((uint64_t)c * n_shots + (uint64_t)si);
             l->core = c;
         }
         run_shot(s);

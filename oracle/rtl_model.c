@@ -636,7 +636,9 @@ int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint
             done += rtl_run_shot(&sc, progs, ni, shot, horizon, cfg->event_cap, cfg->trace_cap, cfg->meas_cap, lo);
             if (summary)
                 for (uint32_t c = 0; c < C; c++) {
-                    uint32_t *sm = summary + 8 * ((uint64_t)c * n_shots + (uint64_t)si);   /* core-major */
+                    const uint64_t L = cfg->lane_order == DPEMU_LANES_SHOT_MAJOR ? (uint64_t)si * C + c
+                                                                                 : (uint64_t)c * n_shots + (uint64_t)si;
+                    uint32_t *sm = summary + 8 * L;                          /* include/dpemu.h lane order */
                     sm[0] = lo[c].t_end;
                     sm[1] = (lo[c].ip & 0xFFFF) | ((lo[c].status & 0xFF) << 16) | ((lo[c].flags & 0xFF) << 24);
                     sm[2] = lo[c].n_events; sm[3] = lo[c].n_instr; sm[4] = lo[c].qclk_end;
