@@ -283,8 +283,12 @@ def leg_ramsey(emu, args, world, rank, stream):
     from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
     ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
     emu.load(ps)
+    # shot-major lanes: a wave (8 shots x 8 cores) writes each event slot as
+    # one 1-KiB run (core-major: two 512-B runs), 0.180 -> 0.159 ms per kernel
+    # (scripts/lane_order_ab.py, profiles/r02_lane_order_ab.json)
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, trace_cap=0, meas_cap=2,
-                           meas_latency=64, seed=0x5EED, p1=0.5, hist_assign=True)
+                           meas_latency=64, seed=0x5EED, p1=0.5, hist_assign=True,
+                           lane_order=_abi.LANES_SHOT_MAJOR)
     shot0, n = sharding.weak_shard(args.shots, rank)
     out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
     pipe = sharding.HistogramPipeline(out['hist'], zero=False)     # each run assigns its histogram
@@ -303,7 +307,7 @@ def leg_ramsey(emu, args, world, rank, stream):
     assert int(pipe.result().sum().item()) == n * world
     # the north star's timeline gather: a fixed sample of lanes (summaries and
     # their event records) from every rank, after the timed region
-    lanes = torch.from_numpy(sharding.sample_lanes(n, 8, 16)).to('cuda')
+    lanes = torch.from_numpy(sharding.sample_lanes(n, 8, 16, cfg.lane_order)).to('cuda')
     sample = torch.cat([out['summary'][lanes], out['events'][:, lanes].permute(1, 0, 2).reshape(len(lanes), -1)], 1)
     gathered = sharding.gather_sample(sample)
     assert gathered.shape[0] == world and torch.equal(gathered[rank], sample)
@@ -395,7 +399,8 @@ def leg_active_reset(emu, args, world, rank, stream):
     ps = ProgramSet(workloads.config3_active_reset(8))
     emu.load(ps)
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
-                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, hist_assign=True)
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, hist_assign=True,
+                           lane_order=_abi.LANES_SHOT_MAJOR)       # whole-line event stores
     shot0, n = sharding.weak_shard(args.ar_shots, rank)
     out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
     pipe = sharding.HistogramPipeline(out['hist'], zero=False)     # each run assigns its histogram

@@ -146,13 +146,17 @@ def max_over_ranks(value: float, device=None, group=None) -> float:
     return float(t.item())
 
 
-def sample_lanes(n_shots: int, cores_per_shot: int, n_sample: int) -> np.ndarray:
+def sample_lanes(n_shots: int, cores_per_shot: int, n_sample: int, lane_order: int = 0) -> np.ndarray:
     """Local lane indices of ``n_sample`` whole shots spread evenly over a
-    shard of ``n_shots`` (every core of each chosen shot; lanes are core-major,
-    L = core * n_shots + shot), ordered shot by shot.  The same count on every
+    shard of ``n_shots`` (every core of each chosen shot, in the run's lane
+    order: core-major L = core * n_shots + shot, or shot-major
+    L = shot * C + core), ordered shot by shot.  The same count on every
     rank keeps gather_sample's tensors equal-shaped."""
     if n_shots <= 0 or n_sample <= 0:
         return np.zeros(0, np.int64)
     k = min(int(n_sample), int(n_shots))
     shots = (np.arange(k, dtype=np.int64) * n_shots) // k
-    return (np.arange(cores_per_shot, dtype=np.int64)[None, :] * int(n_shots) + shots[:, None]).reshape(-1)
+    cores = np.arange(cores_per_shot, dtype=np.int64)[None, :]
+    if lane_order == 1:                                  # _abi.LANES_SHOT_MAJOR
+        return (shots[:, None] * int(cores_per_shot) + cores).reshape(-1)
+    return (cores * int(n_shots) + shots[:, None]).reshape(-1)

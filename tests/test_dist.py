@@ -107,6 +107,9 @@ def test_sample_lanes_whole_shots():
     assert (shots == shots[:, :1]).all() and len(set(shots[:, 0])) == 5
     assert (lanes.reshape(5, 8) // 100 == np.arange(8)).all()
     assert len(sharding.sample_lanes(0, 8, 5)) == 0
+    sm = sharding.sample_lanes(100, 8, 5, lane_order=1)     # shot-major lanes: L = shot * 8 + core
+    np.testing.assert_array_equal(sm % 8, lanes // 100)
+    np.testing.assert_array_equal(sm // 8, lanes % 100)
 
 
 def test_single_rank_collectives_are_identity():
