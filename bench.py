@@ -156,6 +156,7 @@ def bytes_per_lane(summary_np, cfg):
 
 
 SETTLE_S = 0.3
+LANE_ORDER_NAMES = ('core-major', 'shot-major')   # dpemu_config.lane_order
 
 
 def settle(step, drain, seconds=SETTLE_S, sync=None, device='cuda'):
@@ -325,6 +326,7 @@ def leg_ramsey(emu, args, world, rank, stream):
            'timeline_gather': {'ranks': int(gathered.shape[0]), 'lanes_per_rank': int(len(lanes)),
                                'bytes': int(gathered.numel() * gathered.element_size())},
            'config': {'workload': 'config2_ramsey_8core_100pt', 'shots_per_gpu': n, 'cores_per_shot': 8,
+                      'lane_order': LANE_ORDER_NAMES[cfg.lane_order],
                       'global_shots_per_step': n * world, 'parallelism': 'shots sharded, {} GPU(s)'.format(world)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baselines(ps, cfg, 4096, 'config 2 Ramsey')
@@ -427,7 +429,8 @@ def leg_active_reset(emu, args, world, rank, stream):
            'value': n * 8 * world * args.steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * args.steps / dt,
            'ms_per_step': ms_step, 'kernel_ms': kernel_ms,
            'instructions_per_s': float(s['n_instr'].astype(np.float64).sum()) * world * args.steps / dt,
-           'config': {'workload': 'config3_active_reset_8core', 'shots_per_gpu': n, 'global_shots_per_step': n * world},
+           'config': {'workload': 'config3_active_reset_8core', 'shots_per_gpu': n, 'global_shots_per_step': n * world,
+                      'lane_order': LANE_ORDER_NAMES[cfg.lane_order]},
            'roofline': roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baselines(ps, cfg, 8192, 'config 3 active reset')
@@ -498,6 +501,7 @@ def leg_rb(emu, args, world, rank, stream):
            'instructions_per_s': instrs * world * steps / dt,
            'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * steps / dt,
            'config': {'workload': 'config4_rb_2core_1e5seq_depth200', 'sequences': args.rb_seqs,
+                      'lane_order': LANE_ORDER_NAMES[cfg.lane_order],
                       'shots_per_sequence': args.rb_spg, 'shots_per_gpu': n, 'commands': int(ps.words.shape[0]),
                       'program_image_bytes': int(ps.words.nbytes), 'event_cap': cfg.event_cap,
                       'generate_s': gen_s, 'load_s': load_s},
