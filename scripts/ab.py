@@ -31,11 +31,12 @@ def workload(name):
         ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
         cfg = _abi.make_config(8, n_groups=100, max_cycles=1 << 20, event_cap=8, meas_cap=2, seed=0x5EED)
         return ps, cfg, 10 ** 6
-    if name in ('ar', 'ar0', 'ar1', 'ar0x32'):   # config 3; ar0 / ar1: every outcome 0 / 1 (no divergence)
+    if name in ('ar', 'ar0', 'ar1', 'ar0x32', 'ar_sm'):   # config 3; ar0 / ar1: every outcome 0 / 1 (no divergence)
         ps = ProgramSet(workloads.config3_active_reset(8, extra_pulses=32 if name.endswith('x32') else 0))
         cfg = _abi.make_config(8, max_cycles=50000, event_cap=48, meas_cap=4,
                                meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED,
-                               p1={'ar': 0.5, 'ar0': 0.0, 'ar1': 1.0, 'ar0x32': 0.0}[name])
+                               p1={'ar': 0.5, 'ar0': 0.0, 'ar1': 1.0, 'ar0x32': 0.0, 'ar_sm': 0.5}[name],
+                               lane_order=_abi.LANES_SHOT_MAJOR if name == 'ar_sm' else _abi.LANES_CORE_MAJOR)
         return ps, cfg, 1250000
     raise ValueError(name)
 
