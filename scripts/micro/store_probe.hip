@@ -164,6 +164,22 @@ __global__ void __launch_bounds__(BLOCK) ddswg_k(uint32_t *iq, uint32_t n_sample
     }
 }
 
+// balanced contiguous stripes: channel tiles split into `ns` near-equal runs,
+// wave w of stripe s takes local tiles w, w + 4, ...
+__global__ void __launch_bounds__(BLOCK) ddsbal_k(uint32_t *iq, uint32_t n_samples, uint32_t ns)
+{
+    const uint32_t tiles = (n_samples + 1023) / 1024, s = blockIdx.x;
+    uint32_t *out = iq + (uint64_t)blockIdx.y * n_samples;
+    const uint32_t t0 = (uint32_t)((uint64_t)tiles * s / ns), t1 = (uint32_t)((uint64_t)tiles * (s + 1) / ns);
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    for (uint32_t t = t0 + wv; t < t1; t += 4) {
+        for (int r = 0; r < 4; r++) {
+            const uint32_t j = t * 1024 + 4 * (64 * r + ln);
+            if (j + 3 < n_samples) st<false>(out + j, j);
+        }
+    }
+}
+
 static double timeit(void (*launch)(void *), void *a, uint64_t bytes)
 {
     hipEvent_t e0, e1;
@@ -217,6 +233,13 @@ int main(int argc, char **argv)
         }
         report("wavetile", [](void *) { const uint32_t tl = (g.ns + 1023) / 1024, tpc = (tl + 3) / 4; wavetile_k<<<g.nch * tpc, BLOCK>>>(g.iq, g.ns, tpc); });
         report("fill1_256_again", [](void *) { const uint64_t t = (uint64_t)g.nch * g.ns; fill1_k<256><<<(uint32_t)((t / 4 + 255) / 256), 256>>>(g.iq, t); });
+        static const uint32_t NSs[] = {2, 3, 4, 6, 13};
+        for (uint32_t NS : NSs) {
+            char nm[64];
+            g.p = NS;
+            snprintf(nm, sizeof nm, "ddsbal_%u", NS);
+            report(nm, [](void *) { ddsbal_k<<<dim3(g.p, g.nch), BLOCK>>>(g.iq, g.ns, g.p); });
+        }
         (void)tiles;
     }
     const uint32_t chunks = (g.ns + 32767) / 32768;
