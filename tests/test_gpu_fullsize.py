@@ -9,6 +9,8 @@ the oracle (config 4 at full size: tests/test_gpu_rb.py).
   shots per GPU -- rank 0's and rank 7's shards (global shot offsets, the
   RNG keyed by global shot index) each equal to oracle_fast in full, and the
   eight shards' histograms (two of them run) consistent with the outcome law;
+* configs 2 and 3 also in the bench's own launch shape: shot-major lanes
+  (DPEMU_LANES_SHOT_MAJOR) with hist_assign;
 * config 5 (configs[4]): DDS of 128 RB timelines x 16 channels at 16
   samples / clock, the bench's full-size launch (2048 channels x 209,952
   samples); 256 channels spread over the launch (128 qdrv, 128 rdrv), whole
@@ -43,8 +45,11 @@ def run_full(emu, ps, cfg, n, shot0, want):
     import torch
     emu.load(ps)
     out = alloc_device_outputs(cfg, n, want=want)
-    for t in out.values():
-        t.zero_()                     # slots past a lane's count stay 0, as in the oracle's arrays
+    for k, t in out.items():
+        if k == 'hist' and cfg.hist_assign:
+            t.fill_(0x5A5A5A5A)   # hist_assign overwrites: stale counts must not survive
+        else:
+            t.zero_()                 # slots past a lane's count stay 0, as in the oracle's arrays
     emu.run_device(cfg, n, shot0, out)
     torch.cuda.synchronize()
     g = {k: v.cpu().numpy() for k, v in out.items()}
@@ -59,10 +64,14 @@ def run_full(emu, ps, cfg, n, shot0, want):
     return g
 
 
-def test_config2_full_launch_bit_exact(emu):
+BENCH_SHAPE = dict(lane_order=_abi.LANES_SHOT_MAJOR, hist_assign=True)
+
+
+@pytest.mark.parametrize('shape', [{}, BENCH_SHAPE], ids=['core_major', 'bench_shape'])
+def test_config2_full_launch_bit_exact(emu, shape):
     ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, trace_cap=0, meas_cap=2,
-                           meas_latency=64, seed=0x5EED, p1=0.5)
+                           meas_latency=64, seed=0x5EED, p1=0.5, **shape)
     n = 10 ** 6
     g = run_full(emu, ps, cfg, n, 0, ('summary', 'events', 'meas', 'hist'))
     s = _abi.unpack_summary(g['summary'].view(np.uint32))
@@ -70,11 +79,11 @@ def test_config2_full_launch_bit_exact(emu):
     assert int(g['hist'].sum()) == n
 
 
-@pytest.mark.parametrize('rank', [0, 7])
-def test_config3_shard_bit_exact(emu, rank):
+@pytest.mark.parametrize('rank,shape', [(0, {}), (7, BENCH_SHAPE)], ids=['rank0_core_major', 'rank7_bench_shape'])
+def test_config3_shard_bit_exact(emu, rank, shape):
     ps = ProgramSet(workloads.config3_active_reset(8))
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
-                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5)
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, **shape)
     n = 1250000
     g = run_full(emu, ps, cfg, n, rank * n, ('summary', 'events', 'meas', 'hist'))
     s = _abi.unpack_summary(g['summary'].view(np.uint32))
