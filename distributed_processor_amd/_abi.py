@@ -4,7 +4,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_CORES = 64
 MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
 
@@ -43,7 +43,7 @@ class Config(C.Structure):
 class Outputs(C.Structure):
     _fields_ = [('summary', C.c_void_p), ('events', C.c_void_p),
                 ('trace', C.c_void_p), ('meas', C.c_void_p), ('regs', C.c_void_p),
-                ('hist', C.c_void_p)]
+                ('hist', C.c_void_p), ('hist_next', C.c_void_p)]
 
 
 class DDSChannels(C.Structure):
@@ -127,7 +127,7 @@ def prob_to_threshold(p):
     return min(int(round(p * 2 ** 32)), 0xFFFFFFFE)
 
 
-OUTPUT_NAMES = ('summary', 'events', 'trace', 'meas', 'regs', 'hist')
+OUTPUT_NAMES = ('summary', 'events', 'trace', 'meas', 'regs', 'hist', 'hist_next')
 
 
 def lane_index(shot_local, core, n_shots, cores_per_shot=None, lane_order=LANES_CORE_MAJOR):

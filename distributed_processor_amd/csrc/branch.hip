@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     uint4 *const s_prog = s_dyn;
     uint32_t *const s_hist = reinterpret_cast<uint32_t *>(s_dyn + (PLDS ? p.prog_lds_words : 0u));
 
+    clear_hist_next(p);
     const uint32_t tid = threadIdx.x;
     const uint32_t C = p.C;
     const uint32_t pos = blockIdx.x * BLOCK + tid;   // thread position; a shot's cores are adjacent

@@ -396,6 +396,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.meas = reinterpret_cast<uint2 *>(out->meas);
     p.regs_out = out->regs;
     p.hist = reinterpret_cast<unsigned long long *>(out->hist);
+    p.hist_next = reinterpret_cast<unsigned long long *>(out->hist_next);
+    p.hist_bins = (uint64_t)cfg->n_groups << C;
     p.shot_begin = shot_begin;
     p.n_lanes = (uint32_t)(n_shots * C);
     p.n_shots = (uint32_t)n_shots;
@@ -574,9 +576,24 @@ int dpemu_run(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin, uint
 {
     if (!ctx) return DPEMU_E_INVALID;
     if (!out) return fail(ctx, DPEMU_E_INVALID, "null outputs");
-    int rc = validate(ctx, cfg, n_shots, out->hist != nullptr);
+    int rc = validate(ctx, cfg, n_shots, out->hist != nullptr || out->hist_next != nullptr);
     if (rc) return rc;
-    if (n_shots == 0) return DPEMU_OK;
+    if (out->hist_next) {
+        const uint64_t bytes = ((uint64_t)cfg->n_groups << cfg->cores_per_shot) * sizeof(uint64_t);
+        const uintptr_t a = (uintptr_t)out->hist, b = (uintptr_t)out->hist_next;
+        if (out->hist && a < b + bytes && b < a + bytes)
+            return fail(ctx, DPEMU_E_INVALID, "hist_next overlaps hist");
+        if (b % sizeof(uint64_t)) return fail(ctx, DPEMU_E_INVALID, "hist_next is not 8-byte aligned");
+    }
+    if (n_shots == 0) {
+        if (out->hist_next) {                                // the contract holds for an empty run too
+            HIPCHK(ctx, hipSetDevice(ctx->device));
+            HIPCHK(ctx, hipMemsetAsync(out->hist_next, 0,
+                                       ((size_t)cfg->n_groups << cfg->cores_per_shot) * sizeof(uint64_t),
+                                       (hipStream_t)stream));
+        }
+        return DPEMU_OK;
+    }
     return run_impl(ctx, cfg, shot_begin, n_shots, out, (hipStream_t)stream);
 }
 
@@ -585,6 +602,7 @@ int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
 {
     if (!ctx) return DPEMU_E_INVALID;
     if (!host_out) return fail(ctx, DPEMU_E_INVALID, "null outputs");
+    if (host_out->hist_next) return fail(ctx, DPEMU_E_INVALID, "hist_next: device runs (dpemu_run) only");
     int rc = validate(ctx, cfg, n_shots, host_out->hist != nullptr);
     if (rc) return rc;
     if (n_shots == 0) return DPEMU_OK;

@@ -92,6 +92,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     __shared__ uint32_t s_scan[BLOCK / 64];
     extern __shared__ uint4 s_prog[];
 
+    clear_hist_next(p);
     const uint32_t tid = threadIdx.x;
     const uint32_t C = p.C;
     const uint32_t pos = blockIdx.x * BLOCK + tid;   // thread position; a shot's cores are adjacent

@@ -134,6 +134,8 @@ struct KParams {
     uint32_t *hist_rep;           // [hist_reps][hist_stride] u32 replicas (128-B aligned rows)
     uint32_t hist_reps, hist_lds; // hist_lds: n_groups << C <= HIST_LDS_MAX, aggregate in LDS
     uint64_t hist_stride;
+    unsigned long long *hist_next;  // dpemu_outputs.hist_next (nullable): zeroed by the kernel
+    uint64_t hist_bins;             // n_groups << C (hist_next's words)
 };
 constexpr uint32_t HIST_LDS_MAX = 1024;
 

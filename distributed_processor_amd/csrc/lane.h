@@ -182,6 +182,16 @@ __device__ __forceinline__ uint32_t shot_slot(const KParams &p)
     return p.shot_major ? threadIdx.x >> p.log2C : threadIdx.x & ((1u << (8u - p.log2C)) - 1u);
 }
 
+// dpemu_outputs.hist_next: the caller's next histogram buffer set to zero in
+// passing (vector stores, one u64 per thread of the first workgroups; it is
+// disjoint from this run's hist, so no ordering with the counting is needed)
+__device__ __forceinline__ void clear_hist_next(const KParams &p)
+{
+    if (!p.hist_next) return;
+    const uint64_t n = (uint64_t)gridDim.x * BLOCK;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < p.hist_bins; i += n) p.hist_next[i] = 0ull;
+}
+
 // the outcome histogram for block_core_major workgroups: each lane ORs its
 // last measurement into its shot's key in LDS, then one thread per shot
 // counts the key (every thread of the workgroup calls it: barriers)

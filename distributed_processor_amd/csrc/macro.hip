@@ -60,6 +60,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
     const uint32_t tid = threadIdx.x;
     const uint32_t C = p.C;
     uint32_t sl, core;                                // shot within the run, core (core-major workgroup)
+    clear_hist_next(p);
     block_core_major(p, sl, core);
     const bool valid = sl < p.n_shots;
     const uint32_t lane = out_lane(p, sl, core);      // output lane index (core-major)

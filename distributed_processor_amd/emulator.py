@@ -316,7 +316,8 @@ def device_output_specs(cfg: _abi.Config, n_shots: int):
     return {'summary': ((n_lanes, 8), torch.int32), 'events': ((cfg.event_cap, n_lanes, 4), torch.int32),
             'trace': ((cfg.trace_cap, n_lanes, 4), torch.int32),
             'meas': ((cfg.meas_cap, n_lanes, 2), torch.int32), 'regs': ((16, n_lanes), torch.int32),
-            'hist': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64)}
+            'hist': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64),
+            'hist_next': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64)}   # zeroed by the run
 
 
 def _check_tensor(name, t, spec, device):
@@ -326,8 +327,8 @@ def _check_tensor(name, t, spec, device):
     shape, dtype = spec
     if not isinstance(t, torch.Tensor):
         raise DpemuError('{}: expected a torch tensor'.format(name))
-    if name == 'hist' and len(shape) == 2 and shape[1] > 4096:
-        raise DpemuError('hist needs cores_per_shot <= 12')
+    if name in ('hist', 'hist_next') and len(shape) == 2 and shape[1] > 4096:
+        raise DpemuError('{} needs cores_per_shot <= 12'.format(name))
     if t.device.type != 'cuda' or (t.device.index if t.device.index is not None else 0) != device:
         raise DpemuError('{}: tensor on {} but the emulator runs on cuda:{}'.format(name, t.device, device))
     if t.element_size() != torch.empty((), dtype=dtype).element_size() or t.is_floating_point():
@@ -347,7 +348,7 @@ def alloc_device_outputs(cfg: _abi.Config, n_shots: int, want=('summary', 'event
     out = {}
     for k in want:
         shp, dt = shapes[k]
-        if k == 'hist':
+        if k in ('hist', 'hist_next'):
             if cfg.cores_per_shot > 12:
                 continue
             out[k] = torch.zeros(shp, dtype=dt, device=device)

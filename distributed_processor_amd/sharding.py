@@ -79,32 +79,54 @@ class HistogramPipeline:
     while batch k + 1's kernel does.  Before a buffer is reused, the exchange
     that last used it is waited for; it is then zeroed, unless ``zero`` is
     False because the launch assigns the histogram (dpemu_config.hist_assign:
-    the library's reduce kernel stores the counts, one launch fewer per batch).  ``drain()`` waits for every
-    pending exchange; ``result()`` is then the histogram of the last batch,
-    summed over ranks.  One rank: no collectives, the same call sequence.
+    the library's reduce kernel stores the counts, one launch fewer per batch).
+    ``clear_next``: the launch is ``launch(hist, hist_next)`` and its kernel
+    zeroes ``hist_next`` (dpemu_outputs.hist_next), the buffer of batch k + 1,
+    in passing -- accumulating runs with no zeroing launch at all.  That needs
+    three buffers: batch k's kernel clears the buffer batch k - 2 exchanged
+    (waited for first), while batch k - 1's exchange may still run.
+    ``drain()`` waits for every pending exchange; ``result()`` is then the
+    histogram of the last batch, summed over ranks.  One rank: no
+    collectives, the same call sequence.
     """
 
-    def __init__(self, hist, n_buffers=2, group=None, zero=True):
+    def __init__(self, hist, n_buffers=2, group=None, zero=True, clear_next=False):
         import torch
         if n_buffers < 1:
             raise ValueError('n_buffers must be >= 1')
+        if clear_next:
+            if zero:
+                raise ValueError('clear_next: the kernels zero the buffers (zero=False)')
+            n_buffers = max(n_buffers, 3)
+            hist.zero_()                              # batch 0's buffer; later ones the kernels clear
         self.bufs = [hist] + [torch.zeros_like(hist) for _ in range(n_buffers - 1)]
         self.pending = [None] * n_buffers
         self.group = group
         self.zero = zero
+        self.clear_next = clear_next
         self.k = 0
 
-    def step(self, launch):
-        """launch(hist): enqueue one batch writing into (accumulating on) hist"""
-        b = self.k % len(self.bufs)
-        self.k += 1
+    def _wait(self, b):
         if self.pending[b] is not None:
             self.pending[b].wait()                    # this buffer's previous exchange is done
             self.pending[b] = None
+
+    def step(self, launch):
+        """launch(hist) (clear_next: launch(hist, hist_next)): enqueue one
+        batch writing into (accumulating on) hist"""
+        n = len(self.bufs)
+        b = self.k % n
+        self.k += 1
+        self._wait(b)
         h = self.bufs[b]
-        if self.zero:
-            h.zero_()
-        launch(h)
+        if self.clear_next:
+            nb = (b + 1) % n
+            self._wait(nb)                            # the kernel is about to zero it
+            launch(h, self.bufs[nb])
+        else:
+            if self.zero:
+                h.zero_()
+            launch(h)
         self.pending[b] = allreduce_histogram(h, group=self.group, async_op=True)
         return h
 

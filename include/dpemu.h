@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DPEMU_ABI_VERSION 6
+#define DPEMU_ABI_VERSION 7
 
 /* ---- error codes ---------------------------------------------------- */
 #define DPEMU_OK            0
@@ -175,6 +175,10 @@ typedef struct dpemu_outputs {
     uint32_t *meas;       /* [meas_cap][n_lanes][2]            */
     uint32_t *regs;       /* [16][n_lanes] final register file */
     uint64_t *hist;       /* [n_groups][2^C], accumulated (or assigned: hist_assign) */
+    uint64_t *hist_next;  /* optional, dpemu_run only: a second [n_groups][2^C] buffer, disjoint
+                             from hist, that this run sets to zero in passing -- the buffer the
+                             caller's next run accumulates into, so a pipeline of runs rotating
+                             over three histogram buffers needs no zeroing launch (ABI 7) */
 } dpemu_outputs;
 
 typedef struct dpemu_ctx dpemu_ctx;

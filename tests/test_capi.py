@@ -33,7 +33,7 @@ def test_abi_version_and_struct_sizes():
     # dpemu_config: 12 u32 + 2 u64 + 2 u32 + 64 u32 + 256 u64 + the readout model's 4 x 32 bit
     # + hist_assign, reserved
     assert C.sizeof(_abi.Config) == 12 * 4 + 16 + 8 + 64 * 4 + 256 * 8 + 16 + 8
-    assert C.sizeof(_abi.Outputs) == 6 * 8
+    assert C.sizeof(_abi.Outputs) == 7 * 8
     assert C.sizeof(_abi.DDSChannels) == 4 * 4 + 8 * 8
 
 

@@ -76,6 +76,21 @@ def _rank_main(rank, world, port, out_dir):
             pipe.step(launch)
         pipe.drain()
         last_two = torch.stack([pipe.bufs[(N_BATCHES - 2) % 2], pipe.result()])
+        # the accumulating form (dpemu_outputs.hist_next): the stand-in kernel
+        # adds into its buffer and zeroes the next batch's
+        cn = sharding.HistogramPipeline(torch.full_like(hist, 3), zero=False, clear_next=True)
+        for b in range(N_BATCHES):
+            b0, bn = sharding.shard_range(N_BATCH, rank, world)
+
+            def launch_cn(h, h_next, b=b, b0=b0, bn=bn):
+                o = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, b * N_BATCH + b0, bn,
+                                    threads=1, want=('hist',))
+                h_next.zero_()
+                h.add_(torch.from_numpy(o['hist'].astype(np.int64)))
+            cn.step(launch_cn)
+        cn.drain()
+        assert torch.equal(cn.result(), last_two[1])
+        assert torch.equal(cn.bufs[(N_BATCHES - 2) % 3], last_two[0])
         if rank == 0:
             np.save(os.path.join(out_dir, 'hist.npy'), hist.numpy())
             np.save(os.path.join(out_dir, 'gathered.npy'), gathered.numpy())
@@ -173,6 +188,30 @@ def test_pipeline_assigning_launch_skips_zeroing():
     acc = sharding.HistogramPipeline(torch.full((2,), 7, dtype=torch.int64), n_buffers=1, zero=False)
     acc.step(lambda t: t.add_(1))
     assert acc.result().tolist() == [8, 8]
+
+
+def test_pipeline_clear_next_rotation():
+    """clear_next: three buffers; batch k's launch gets batch k + 1's buffer
+    to zero and accumulates into its own, which batch k - 1 zeroed (batch 0's
+    the pipeline zeroes once)"""
+    h = torch.full((4,), 99, dtype=torch.int64)
+    pipe = sharding.HistogramPipeline(h, zero=False, clear_next=True)
+    assert len(pipe.bufs) == 3 and h.tolist() == [0] * 4
+    seen = []
+
+    def launch(t, nxt, b):
+        assert t.tolist() == [0] * 4 and nxt is not t
+        seen.append((t.data_ptr(), nxt.data_ptr()))
+        nxt.zero_()                      # as the kernel does (hist_next)
+        t.add_(b + 1)
+    for b in range(7):
+        pipe.step(lambda t, nxt, b=b: launch(t, nxt, b))
+    pipe.drain()
+    assert pipe.result().tolist() == [7] * 4 and pipe.bufs[(7 - 2) % 3].tolist() == [6] * 4
+    ptrs = [x.data_ptr() for x in pipe.bufs]
+    assert seen == [(ptrs[k % 3], ptrs[(k + 1) % 3]) for k in range(7)]
+    with pytest.raises(ValueError):
+        sharding.HistogramPipeline(h, clear_next=True)          # zero=True would add a launch back
 
 
 def _settle_main(rank, world, port, out_dir):

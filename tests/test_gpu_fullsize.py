@@ -10,7 +10,8 @@ the oracle (config 4 at full size: tests/test_gpu_rb.py).
   RNG keyed by global shot index) each equal to oracle_fast in full, and the
   eight shards' histograms (two of them run) consistent with the outcome law;
 * configs 2 and 3 also in the bench's own launch shape: shot-major lanes
-  (DPEMU_LANES_SHOT_MAJOR) with hist_assign;
+  (DPEMU_LANES_SHOT_MAJOR); config 2 accumulating while it clears the next
+  run's histogram (dpemu_outputs.hist_next), config 3 with hist_assign;
 * config 5 (configs[4]): DDS of 128 RB timelines x 16 channels at 16
   samples / clock, the bench's full-size launch (2048 channels x 209,952
   samples); 256 channels spread over the launch (128 qdrv, 128 rdrv), whole
@@ -41,11 +42,15 @@ def emu():
     e.close()
 
 
-def run_full(emu, ps, cfg, n, shot0, want):
+def run_full(emu, ps, cfg, n, shot0, want, clear_next=False):
     import torch
     emu.load(ps)
     out = alloc_device_outputs(cfg, n, want=want)
+    if clear_next:
+        out['hist_next'] = torch.full_like(out['hist'], 0x5A5A5A5A)
     for k, t in out.items():
+        if k == 'hist_next':
+            continue
         if k == 'hist' and cfg.hist_assign:
             t.fill_(0x5A5A5A5A)   # hist_assign overwrites: stale counts must not survive
         else:
@@ -53,6 +58,8 @@ def run_full(emu, ps, cfg, n, shot0, want):
     emu.run_device(cfg, n, shot0, out)
     torch.cuda.synchronize()
     g = {k: v.cpu().numpy() for k, v in out.items()}
+    if clear_next:
+        assert not g.pop('hist_next').any(), 'hist_next not cleared'
     del out
     torch.cuda.empty_cache()
     f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n, threads=THREADS, want=want)
@@ -67,13 +74,14 @@ def run_full(emu, ps, cfg, n, shot0, want):
 BENCH_SHAPE = dict(lane_order=_abi.LANES_SHOT_MAJOR, hist_assign=True)
 
 
-@pytest.mark.parametrize('shape', [{}, BENCH_SHAPE], ids=['core_major', 'bench_shape'])
-def test_config2_full_launch_bit_exact(emu, shape):
+@pytest.mark.parametrize('bench_shape', [False, True], ids=['core_major', 'bench_shape'])
+def test_config2_full_launch_bit_exact(emu, bench_shape):
     ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, trace_cap=0, meas_cap=2,
-                           meas_latency=64, seed=0x5EED, p1=0.5, **shape)
+                           meas_latency=64, seed=0x5EED, p1=0.5,
+                           lane_order=_abi.LANES_SHOT_MAJOR if bench_shape else _abi.LANES_CORE_MAJOR)
     n = 10 ** 6
-    g = run_full(emu, ps, cfg, n, 0, ('summary', 'events', 'meas', 'hist'))
+    g = run_full(emu, ps, cfg, n, 0, ('summary', 'events', 'meas', 'hist'), clear_next=bench_shape)
     s = _abi.unpack_summary(g['summary'].view(np.uint32))
     assert (s['status'] == _abi.ST_DONE).all() and (s['flags'] == 0).all()
     assert int(g['hist'].sum()) == n

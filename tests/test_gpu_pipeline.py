@@ -98,3 +98,99 @@ def test_pipeline_without_zeroing_on_assign():
         got = pipe.result().cpu().numpy()
     ref = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, (batches - 1) * n, n, want=('hist',))['hist']
     np.testing.assert_array_equal(got, ref.astype(np.int64))
+
+
+def _kernel_cases():
+    """one workload per kernel: straight (config 2), macro (config 4),
+    branch (config 3), the general interpreter (config 3, DPEMU_X_GENERAL)"""
+    c3 = dict(max_cycles=50000, event_cap=16, meas_cap=4, meas_latency=workloads.CONFIG3_MEAS_LATENCY, p1=0.5)
+    return {
+        'straight': (ProgramSet(workloads.config2_ramsey(8, 100)), dict(max_cycles=1 << 20, event_cap=8, meas_cap=2)),
+        'macro': (workloads.config4_rb_set(64, 40), dict(shots_per_group=10, max_cycles=1 << 20, event_cap=128,
+                                                         meas_cap=2)),
+        'branch': (ProgramSet(workloads.config3_active_reset(8)), c3),
+        'interp': (ProgramSet(workloads.config3_active_reset(8)), dict(c3, exec_flags=_abi.X_GENERAL)),
+    }
+
+
+@pytest.mark.parametrize('kernel', ['straight', 'macro', 'branch', 'interp'])
+@pytest.mark.parametrize('hist_flags', [_abi.X_HIST_DIRECT, _abi.X_HIST_REPL])
+def test_hist_next_cleared_by_every_kernel(kernel, hist_flags):
+    """dpemu_outputs.hist_next: the run zeroes it whatever it held (every
+    kernel, both histogram strategies, a grid smaller than the buffer) and
+    its own histogram is unchanged"""
+    import torch
+    ps, kw = _kernel_cases()[kernel]
+    kw = dict(kw)
+    kw['exec_flags'] = kw.get('exec_flags', 0) | hist_flags
+    C = ps.cores_per_shot
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, seed=0x5EED, **kw)
+    with Emulator(0) as emu:
+        emu.load(ps)
+        for n in (3, 2000):
+            out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist', 'hist_next'))
+            out['hist_next'].fill_(0x5A5A5A5A)
+            emu.run_device(cfg, n, 7, out)
+            torch.cuda.synchronize()
+            assert not out['hist_next'].any(), (kernel, n)
+            ref = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 7, n, want=('hist',))['hist']
+            np.testing.assert_array_equal(out['hist'].cpu().numpy(), ref.astype(np.int64))
+
+
+def test_hist_next_contract_edges():
+    """an empty run still clears hist_next; an overlapping hist_next and a
+    host run with one are rejected"""
+    import ctypes as C
+    import torch
+    from distributed_processor_amd._native import DpemuError
+    ps = ProgramSet(workloads.config2_ramsey(8, 100))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, event_cap=8, meas_cap=2)
+    with Emulator(0) as emu:
+        emu.load(ps)
+        out = alloc_device_outputs(cfg, 0, want=('hist', 'hist_next'))
+        out['hist_next'].fill_(9)
+        emu.run_device(cfg, 0, 0, out)
+        torch.cuda.synchronize()
+        assert not out['hist_next'].any()
+        big = torch.zeros((2,) + tuple(out['hist'].shape), dtype=torch.int64, device='cuda')
+        flat = big.view(-1)
+        half = out['hist'].numel() // 2
+        with pytest.raises(DpemuError):
+            emu.run_device(cfg, 10, 0, {'hist': big[0], 'hist_next': flat[half:half + out['hist'].numel()]
+                                        .view(out['hist'].shape)})
+        host = _abi.alloc_host_outputs(cfg, 4, ('summary', 'hist'))
+        o = _abi.outputs_struct(host)
+        nxt = np.zeros_like(host['hist'])
+        o.hist_next = nxt.ctypes.data
+        rc = emu._L.dpemu_run_host(emu._h, C.addressof(cfg), 0, 4, C.addressof(o))
+        assert rc != 0
+
+
+@pytest.mark.parametrize('hist_flags', [_abi.X_HIST_DIRECT, _abi.X_HIST_REPL])
+def test_pipeline_clear_next_batches(hist_flags):
+    """bench.py's config-2 loop: three buffers, each run accumulating into
+    the buffer the previous run's kernel zeroed -- no zeroing launch -- and
+    every batch's histogram that batch alone"""
+    import torch
+    ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, meas_cap=2,
+                           meas_latency=64, seed=0x5EED, p1=0.5, exec_flags=hist_flags,
+                           lane_order=_abi.LANES_SHOT_MAJOR)
+    n, batches = 20000, 7
+    with Emulator(0) as emu:
+        emu.load(ps)
+        out = alloc_device_outputs(cfg, n, want=('summary', 'hist'))
+        out['hist'].fill_(77)                               # the pipeline zeroes batch 0's buffer
+        pipe = sharding.HistogramPipeline(out['hist'], zero=False, clear_next=True)
+        for b in range(batches):
+            def launch(h, h_next, b=b):
+                out['hist'], out['hist_next'] = h, h_next
+                emu.run_device(cfg, n, b * n, out)
+            pipe.step(launch)
+        pipe.drain()
+        torch.cuda.synchronize()
+        got = [pipe.bufs[(batches - 1 - j) % 3].cpu().numpy() for j in (1, 0)]
+        assert not pipe.bufs[batches % 3].any()            # the last run cleared the next batch's buffer
+    for j, b in enumerate((batches - 2, batches - 1)):
+        ref = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, b * n, n, want=('hist',))['hist']
+        np.testing.assert_array_equal(got[j], ref.astype(np.int64))
