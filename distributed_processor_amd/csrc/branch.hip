@@ -189,13 +189,21 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         }
     };
 
-    // latest measurement of group lane q with valid cycle <= d (slots in time order, INF = empty)
+    // latest measurement of group lane q with valid cycle <= d.  A lane's
+    // slots fill in time order (valid cycles non-decreasing, INF past the
+    // last; INF >> 1 exceeds any cycle), so the scan stops at the first slot
+    // later than d -- read in pairs (one ds_read2), usually one pair per
+    // lane instead of MT unrolled reads and compares
     auto meas_lookup = [&](uint32_t q_tid, uint32_t d) -> uint32_t {
+        static_assert(MEAS_LOOKUP % 2 == 0, "slots read in pairs");
         uint32_t res = 0;
-#pragma unroll
-        for (int m = 0; m < MT; m++) {
-            const uint32_t e = s_mt[m][q_tid];
-            if (e != INF32 && (e >> 1) <= d) res = e & 1u;
+#pragma unroll 1
+        for (int m = 0; m + 1 < MT; m += 2) {
+            const uint32_t e0 = s_mt[m][q_tid], e1 = s_mt[m + 1][q_tid];
+            if ((e0 >> 1) > d) break;
+            res = e0 & 1u;
+            if ((e1 >> 1) > d) break;
+            res = e1 & 1u;
         }
         return res;
     };
