@@ -52,18 +52,14 @@ constexpr uint64_t LATENCY = 0x0003303304646440ull;
 
 __device__ __forceinline__ uint32_t alu_eval(uint32_t op, uint32_t a, uint32_t b)
 {
-    // alu.v:20-50; le = sub[31] ^ overflow == signed a < b
+    // alu.v:20-50: 0 id0, 1 add, 2 sub, 3 eq, 4 le, 5 ge, 6 id1, 7 zero;
+    // le = sub[31] ^ overflow == signed a < b.  A select tree on op's bits.
     const uint32_t sub = a - b;
     const uint32_t lt = (int32_t)a < (int32_t)b;
-    uint32_t r = a;                 // 0: id0
-    r = (op == 1) ? a + b : r;
-    r = (op == 2) ? sub : r;
-    r = (op == 3) ? (uint32_t)(sub == 0) : r;
-    r = (op == 4) ? lt : r;
-    r = (op == 5) ? (lt ^ 1u) : r;
-    r = (op == 6) ? b : r;
-    r = (op == 7) ? 0u : r;
-    return r;
+    const bool b0 = op & 1u, b1 = op & 2u;
+    const uint32_t lo = b1 ? (b0 ? (uint32_t)(sub == 0u) : sub) : (b0 ? a + b : a);   // 0-3
+    const uint32_t hi = b1 ? (b0 ? 0u : b) : (lt ^ (uint32_t)b0);                     // 4-7
+    return (op & 4u) ? hi : lo;
 }
 
 // group reductions over the C adjacent lanes of a shot (all lanes converged):
@@ -290,18 +286,21 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             const bool cont = pg && (((0x1B04u >> op) & 1u) != 0u) && !over;   // 2, 8, 9, B, C in the budget
             // pulse_reg.sv:59-97 (write enables are zero except for 8 / 9):
             // immediates, then reg[rs0] into register-sourced fields
-            uint32_t pe2 = pe, pp2 = pp, pa2 = pa;
-            pulse_write(u, pe2, pp2, pa2);
-            if (cont && (u.w & UOP_ANY_RS)) {
-                const uint32_t r0 = reg(u.w >> 20);
-                if (u.w & UOP_RS_ENV) pe2 |= r0 & 0xFFFFFFu;
-                if (u.w & UOP_RS_PH) pp2 |= r0 & 0x1FFFFu;
-                if (u.w & UOP_RS_FR) pp2 |= (r0 & 0x1FFu) << 17;
-                if (u.w & UOP_RS_AMP) pa2 = r0 & 0xFFFFu;
+            // (only 8 / 9 write: skipped in iterations where no lane has one)
+            if (__any(cont && ((0x300u >> op) & 1u))) {
+                uint32_t pe2 = pe, pp2 = pp, pa2 = pa;
+                pulse_write(u, pe2, pp2, pa2);
+                if (cont && (u.w & UOP_ANY_RS)) {
+                    const uint32_t r0 = reg(u.w >> 20);
+                    if (u.w & UOP_RS_ENV) pe2 |= r0 & 0xFFFFFFu;
+                    if (u.w & UOP_RS_PH) pp2 |= r0 & 0x1FFFFu;
+                    if (u.w & UOP_RS_FR) pp2 |= (r0 & 0x1FFu) << 17;
+                    if (u.w & UOP_RS_AMP) pa2 = r0 & 0xFFFFu;
+                }
+                pe = cont ? pe2 : pe;
+                pp = cont ? pp2 : pp;
+                pa = cont ? pa2 : pa;
             }
-            pe = cont ? pe2 : pe;
-            pp = cont ? pp2 : pp;
-            pa = cont ? pa2 : pa;
             // strobes: trigger at tT + 2 (cmd_time 0 in the reset hold strobes
             // twice), phase reset at D
             const bool rst = op == 0xBu;
