@@ -1,7 +1,8 @@
 """Where config 3's kernel time goes: the production branch_kernel timed
 (HIP events around the kernel, library side) with fewer outputs requested --
 all of them, without event records, without events and measurements -- so
-the store-side share of a launch shows beside the compute.  One JSON line."""
+the store-side share of a launch shows beside the compute.  One JSON line.
+    python scripts/ar_probe.py [lib.so] [--shot-major]"""
 import json
 import os
 import sys
@@ -16,11 +17,14 @@ def main():
     from distributed_processor_amd import _abi, workloads
     from distributed_processor_amd.emulator import Emulator, ProgramSet, alloc_device_outputs
     ps = ProgramSet(workloads.config3_active_reset(8))
+    order = _abi.LANES_SHOT_MAJOR if '--shot-major' in sys.argv else _abi.LANES_CORE_MAJOR
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
-                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, hist_assign=True)
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, hist_assign=True,
+                           lane_order=order)
     n = 1250000
     res = {}
-    lib = sys.argv[1] if len(sys.argv) > 1 else None
+    args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    lib = args[0] if args else None
     with Emulator(0, lib_path=lib) if lib else Emulator(0) as emu:
         emu.load(ps)
         full = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
@@ -43,6 +47,7 @@ def main():
                     res.setdefault(name, []).append(float(np.median(kt)))
         res = {k: float(np.median(v)) for k, v in res.items()}
         res['kernel'] = emu.last_kernel()
+        res['lane_order'] = 'shot_major' if order else 'core_major'
     print(json.dumps(res))
 
 
