@@ -24,6 +24,8 @@
 //     group min / max are DPP within a row of 16 lanes;
 //   * the reset hold (qclk(0) = qclk(1) = 0, proc.sv:125-136) can only be
 //     seen by a lane's first decode: a peeled first iteration;
+//   * event records are held per lane and stored a whole wave row at a
+//     time (below, pend0 / pend1);
 //   * no register file when no command writes one (FEAT_REGS), and the
 //     workgroup's programs staged in LDS when they are short
 //     (FEAT_PROG_LDS: an LDS fetch does not wait behind the lane's event
@@ -78,6 +80,22 @@ __device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t C)
 #undef DPP
     for (uint32_t m = 16; m < C; m <<= 1) v = comb(v, (uint32_t)__shfl_xor((int)v, (int)m, 64));
     return v;
+}
+
+// per-component select (keeps the pending event records in registers)
+__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b)
+{
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+// minimum over the whole wave (all lanes converged): DPP within each row of
+// 16, then the four rows' minima by readlane
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+    v = group_reduce<0>(v, 16u);
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return min(min(a, b), min(c, d));
 }
 
 }  // namespace
@@ -156,13 +174,32 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     uint32_t n_ev = 0, n_tr = 0, n_meas = 0, n_exec = 0, meas_bits = 0, last_bit = 0;
     const bool is_part = SYNC ? (((p.sync_mask >> core) & 1ull) != 0) : false;
     uint4 *const ev_lane = p.events + lane;          // event slot k of this lane at ev_lane[k * n_lanes]
+    // Event rows written whole.  A record is held (up to two per lane) until
+    // every unfinished lane of the wave has reached its slot, then the wave
+    // stores the row in one instruction: lanes on different branches (config
+    // 3's conditional X90 pair) reach a row in different iterations, and
+    // storing each part as it comes took two store instructions per row
+    // (config 3: 0.480 -> 0.455 ms median, write bytes unchanged,
+    // profiles/r02_ar_rows_ab.json).  Slots [n_st, min(n_ev, cap)) are
+    // pending in pend0, pend1; a third record pushes the oldest out.
+    uint4 pend0 = make_uint4(0u, 0u, 0u, 0u), pend1 = pend0;
+    uint32_t n_st = 0;
 
     // pulse_iface strobe at cycle te (kind 0: trigger, 1: phase reset) with the
     // current pulse registers for lanes with `ok`; readout-element triggers
     // draw the measurement.  Overflow flags come from the final counts.
     auto emit = [&](bool ok, uint32_t te, uint32_t kind) __attribute__((always_inline)) {
         if (ok) {
-            if (n_ev < p.event_cap && p.events) ev_lane[(uint64_t)n_ev * n_lanes] = event_record(te, pe, pp, pa, kind);
+            if (n_ev < p.event_cap && p.events) {
+                const uint4 rec = event_record(te, pe, pp, pa, kind);
+                const bool full = n_ev - n_st == 2u;    // the oldest goes out now
+                if (full) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
+                pend0 = sel4(full, pend1, pend0);
+                n_st += full ? 1u : 0u;
+                const bool first = n_ev == n_st;
+                pend0 = sel4(first, rec, pend0);
+                pend1 = sel4(first, pend1, rec);
+            }
             n_ev++;
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {   // meas_elem 0xFF: none
                 const uint32_t bit = meas_bit(p, shot, core, n_meas, thr_core, pa, pe);
@@ -222,6 +259,21 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         status = stop ? st : status;
         t_end = stop ? at : t_end;
         mode = stop ? B_FIN : mode;
+    };
+
+    // store the pending rows every unfinished lane has passed (all: at the end)
+    auto flush_rows = [&](bool all) __attribute__((always_inline)) {
+        if (!p.events) return;
+        const uint32_t ne = min(n_ev, p.event_cap);
+        if (!__any(ne > n_st)) return;
+        const uint32_t done = all ? INF32 : wave_min(mode == B_FIN ? INF32 : ne);
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const bool f = n_st < ne && n_st < done;
+            if (f) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
+            pend0 = sel4(f, pend1, pend0);
+            n_st += f ? 1u : 0u;
+        }
     };
 
     // One lockstep iteration: every running lane retires at most one command.
@@ -384,6 +436,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
+        flush_rows(false);
         return __any(mode != B_FIN);
     };
 
@@ -398,6 +451,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             }
         }
     }
+    flush_rows(true);
     flags |= (n_ev > p.event_cap ? F_EVENT_OVF : 0u) | (n_meas > min(p.meas_cap, MEAS_LOOKUP) ? F_MEAS_OVF : 0u) |
              ((p.trace_cap && n_tr > p.trace_cap) ? F_TRACE_OVF : 0u);
 

@@ -93,3 +93,22 @@ def test_lane_order_rejected_when_invalid(emu):
     from distributed_processor_amd._native import DpemuError
     with pytest.raises(DpemuError):
         emu.run(4, 0, cfg=cfg, outputs=('summary',))
+
+
+@pytest.mark.parametrize('seed', range(8))
+def test_event_rows_under_divergence(emu, seed):
+    """branch_kernel holds each lane's newest event records and stores whole
+    wave rows: programs whose lanes diverge (jumps on outcomes, syncs, late
+    and hung commands) at small and large event caps, both lane orders, bit
+    for bit against oracle_fast (the record a lane pushes out early, the
+    cap, the final flush)"""
+    C = [2, 4, 8, 8][seed % 4]
+    case = random_case(47000 + seed, ncores=C, mode='meas')
+    groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
+    ps = ProgramSet(groups, cores_per_shot=C)
+    for cap in (1, 2, 3, 64):
+        for order in (_abi.LANES_CORE_MAJOR, SM):
+            cfg = _abi.make_config(C, n_groups=ps.n_groups, max_cycles=6000, event_cap=cap, trace_cap=8, meas_cap=8,
+                                   meas_latency=2 + seed, p1=0.3 + 0.05 * seed, seed=seed, lane_order=order)
+            g, f = run_pair(emu, ps, cfg, 257, seed * 100)
+            compare_all(g, f, 'event_cap {} order {}'.format(cap, order))
