@@ -178,8 +178,8 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // every unfinished lane of the wave has reached its slot, then the wave
     // stores the row in one instruction: lanes on different branches (config
     // 3's conditional X90 pair) reach a row in different iterations, and
-    // storing each part as it comes took two store instructions per row
-    // (config 3: 0.480 -> 0.455 ms median, write bytes unchanged,
+    // storing each part as it comes was slower although it issued fewer
+    // stores and the same bytes (config 3: 0.480 -> 0.447 ms median,
     // profiles/r02_ar_rows_ab.json).  Slots [n_st, min(n_ev, cap)) are
     // pending in pend0, pend1; a third record pushes the oldest out.
     uint4 pend0 = make_uint4(0u, 0u, 0u, 0u), pend1 = pend0;
@@ -270,6 +270,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 #pragma unroll
         for (int r = 0; r < 2; r++) {
             const bool f = n_st < ne && n_st < done;
+            if (!__any(f)) break;                    // most iterations complete no row
             if (f) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
             pend0 = sel4(f, pend1, pend0);
             n_st += f ? 1u : 0u;
