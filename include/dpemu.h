@@ -204,11 +204,14 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words,
                         const uint32_t *prog_table, uint32_t n_groups, uint32_t cores_per_shot);
 
 /* Emulate shots [shot_begin, shot_begin + n_shots) on `stream` (hipStream_t or
- * NULL).  n_lanes = n_shots * C.  Outputs are device pointers. */
+ * NULL).  n_lanes = n_shots * C.  Outputs are device pointers.  out->hist_next,
+ * when set, is zeroed even for n_shots = 0; overlapping out->hist is
+ * DPEMU_E_INVALID. */
 int dpemu_run(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin, uint64_t n_shots,
               const dpemu_outputs *out, void *stream);
 
-/* Same, with host output pointers (the library stages device buffers). */
+/* Same, with host output pointers (the library stages device buffers);
+ * host_out->hist_next must be NULL (DPEMU_E_INVALID otherwise). */
 int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
                    uint64_t n_shots, const dpemu_outputs *host_out);
 
