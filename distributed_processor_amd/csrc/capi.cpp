@@ -231,12 +231,12 @@ int dpemu_kernel_times(dpemu_ctx *ctx, float *ms, int max_n, int *n_out)
     return DPEMU_OK;
 }
 
-int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words, const uint32_t *offsets,
+int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, const uint32_t *offsets,
                         const uint32_t *n_instr, uint32_t n_programs, const uint32_t *prog_table,
                         uint32_t n_groups, uint32_t cores_per_shot)
 {
     if (!ctx) return DPEMU_E_INVALID;
-    if ((!words && n_words) || !offsets || !n_instr || !prog_table || n_programs == 0 || n_groups == 0)
+    if ((!words && n_cmds) || !offsets || !n_instr || !prog_table || n_programs == 0 || n_groups == 0)
         return fail(ctx, DPEMU_E_INVALID, "load_programs: null array or empty program set");
     const uint32_t C = cores_per_shot;
     if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1)))
@@ -246,9 +246,9 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words,
     for (uint32_t i = 0; i < n_programs; i++) {
         if (n_instr[i] > 65536u)
             return fail(ctx, DPEMU_E_INVALID, "program %u: %u commands exceed the 2^16-deep cmd_mem", i, n_instr[i]);
-        if ((uint64_t)offsets[i] + n_instr[i] > n_words)
-            return fail(ctx, DPEMU_E_INVALID, "program %u: offset %u + %u commands run past the %llu words",
-                        i, offsets[i], n_instr[i], (unsigned long long)n_words);
+        if ((uint64_t)offsets[i] + n_instr[i] > n_cmds)
+            return fail(ctx, DPEMU_E_INVALID, "program %u: offset %u + %u commands run past the %llu commands",
+                        i, offsets[i], n_instr[i], (unsigned long long)n_cmds);
     }
     for (uint32_t i = 0; i < n_programs; i++)
         for (uint32_t k = 0; k < n_instr[i]; k++) {
@@ -461,7 +461,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     const bool small = blocks <= 4 * 256;
     const int fetch_batch = small ? 4 : 1;
     const bool uniform = ctx->straight && ctx->max_len < 65536u && !(cfg->exec_flags & DPEMU_X_GENERAL);
-    const bool macro = !uniform && ctx->d_macro && !(cfg->exec_flags & DPEMU_X_GENERAL);
+    const bool macro = !uniform && ctx->d_macro && !(cfg->exec_flags & (DPEMU_X_GENERAL | DPEMU_X_PROG_LDS));
     int src = cmd_major ? STRAIGHT_ROWS : STRAIGHT_PROG;
     if (uniform) {
         const uint64_t per_cu = std::min<uint64_t>(8, std::max<uint64_t>(1, (blocks + 255) / 256));
@@ -586,11 +586,13 @@ int dpemu_run(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin, uint
         if (b % sizeof(uint64_t)) return fail(ctx, DPEMU_E_INVALID, "hist_next is not 8-byte aligned");
     }
     if (n_shots == 0) {
-        if (out->hist_next) {                                // the contract holds for an empty run too
+        if (out->hist_next) {                                // the contract holds for an empty run too,
+            hipStream_t s = (hipStream_t)stream;             // in call order like any other call
             HIPCHK(ctx, hipSetDevice(ctx->device));
+            HIPCHK(ctx, order_begin(ctx, s));
             HIPCHK(ctx, hipMemsetAsync(out->hist_next, 0,
-                                       ((size_t)cfg->n_groups << cfg->cores_per_shot) * sizeof(uint64_t),
-                                       (hipStream_t)stream));
+                                       ((size_t)cfg->n_groups << cfg->cores_per_shot) * sizeof(uint64_t), s));
+            HIPCHK(ctx, order_end(ctx, s));
         }
         return DPEMU_OK;
     }

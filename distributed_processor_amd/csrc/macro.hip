@@ -102,7 +102,11 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
     // come from the final counts.
     auto emit = [&](bool ok, uint32_t te, uint32_t kind, uint32_t reps) __attribute__((always_inline)) {
         for (uint32_t r = 0; r < (ok ? reps : 0u); r++) {
+#ifdef MACRO_PROBE_NOSTORE                              // A/B probe only (scripts/ab_libs.sh): no event stores
+            if (n_ev == 0xFFFFFFFFu)
+#else
             if (n_ev < p.event_cap && p.events)
+#endif
                 p.events[(uint64_t)n_ev * n_lanes + lane] = event_record(te + r, pe, pp, pa, kind);
             n_ev++;
             const bool is_meas = kind == 0u && ((pe >> 24) & 3u) == p.meas_elem;   // meas_elem 0xFF: none
@@ -257,7 +261,11 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
     // macro m of this lane's program (ALU slots, pulse slot); in bounds: the
     // terminal macro repeats
     const uint4 *mbase = p.macros;
+#ifdef MACRO_PROBE_NOFETCH                              // A/B probe only: every fetch hits macro 0..1 (L1)
+    auto addr = [&](uint32_t m) __attribute__((always_inline)) -> const uint4 * { return mbase + 2ull * min(mb + (m & 1u), ml); };
+#else
     auto addr = [&](uint32_t m) __attribute__((always_inline)) -> const uint4 * { return mbase + 2ull * min(mb + m, ml); };
+#endif
 
     // one macro ahead: macro m + 1 is in flight while macro m executes
     uint4 an = addr(0u)[0], un = addr(0u)[1];

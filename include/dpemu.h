@@ -77,7 +77,8 @@ extern "C" {
 
 /* execution knobs (dpemu_config.exec_flags): results never depend on them; the
  * parity tests run every variant against the oracle */
-#define DPEMU_X_PROG_LDS    0x1   /* general interpreter: stage each workgroup's programs in LDS when they fit */
+#define DPEMU_X_PROG_LDS    0x1   /* run non-pulse-only programs on the general interpreter with each
+                                     workgroup's programs staged in LDS when they fit */
 #define DPEMU_X_HIST_DIRECT 0x4   /* outcome histogram: atomics straight into out->hist       */
 #define DPEMU_X_HIST_REPL   0x8   /* outcome histogram: privatised replicas + reduce          */
 #define DPEMU_X_PROG_MAJOR  0x10  /* fetch from the program-major image, not the command-major copy */
@@ -190,16 +191,18 @@ int         dpemu_destroy(dpemu_ctx *ctx);
 const char *dpemu_last_error(dpemu_ctx *ctx);
 
 /*
- * Programs: n_programs cmd_mem images.  `words` holds every program's
- * little-endian u128 commands as u32 quads (word i of the u128 = bits
- * [32i+31:32i], cmd_mem_iface.sv:19-21), program p starting at quad
- * offsets[p] with n_instr[p] commands (assembler cmd_buf bytes reinterpret
- * directly); offsets[p] + n_instr[p] <= n_words for every p.  Fetch beyond
+ * Programs: n_programs cmd_mem images.  `words` holds n_cmds little-endian
+ * u128 commands as u32 quads (word i of the u128 = bits [32i+31:32i],
+ * cmd_mem_iface.sv:19-21), i.e. 4 * n_cmds u32 words; program p starts at
+ * COMMAND offsets[p] with n_instr[p] commands (assembler cmd_buf bytes
+ * reinterpret directly).  n_cmds, offsets and n_instr all count 16-byte
+ * commands; offsets[p] + n_instr[p] <= n_cmds for every p, else
+ * DPEMU_E_INVALID (nothing past the caller's 16 * n_cmds bytes is read).  Fetch beyond
  * n_instr reads 0 (= DONE), as the zero-initialised 2^16-deep cmd_mem of
  * toplevel_sim does.  prog_table[g*C + c] = program run by core c of shots
  * in group g.  Replaces load_commands (cocotb/proc/test_proc.py:29-38).
  */
-int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words, const uint32_t *offsets,
+int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, const uint32_t *offsets,
                         const uint32_t *n_instr, uint32_t n_programs,
                         const uint32_t *prog_table, uint32_t n_groups, uint32_t cores_per_shot);
 

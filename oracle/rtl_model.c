@@ -587,7 +587,8 @@ int rtl_run_shot(const oracle_shot_cfg *cfg, const uint32_t *const *progs, const
  * buffers of the config's caps (the same work as a dpemu run); the summary
  * rows (dpemu layout, include/dpemu.h) go to `summary` when it is non-null.
  * `horizon`: cycles simulated past the first decode at most.  Returns the
- * number of shots whose every core reached DONE.
+ * number of shots whose every core reached DONE, or -1 for a bad config or
+ * a failed scratch allocation (C x event_cap x 16 B per thread).
  */
 int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
                       const uint32_t *n_instr, const uint32_t *prog_table, uint64_t shot_begin,
@@ -607,18 +608,21 @@ int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint
     const uint32_t ev_cap = cfg->event_cap ? cfg->event_cap : 1, tr_cap = cfg->trace_cap ? cfg->trace_cap : 1;
     const uint32_t ms_cap = cfg->meas_cap ? cfg->meas_cap : 1;
     int64_t done = 0;
+    int oom = 0;                 /* any thread's scratch allocation failed */
 #ifdef _OPENMP
     if (n_threads > 0) omp_set_num_threads(n_threads);
 #else
     (void)n_threads;
 #endif
-    #pragma omp parallel reduction(+ : done)
+    #pragma omp parallel reduction(+ : done) reduction(| : oom)
     {
         oracle_lane_out *lo = (oracle_lane_out *)calloc(C, sizeof(oracle_lane_out));
         uint32_t *ev = (uint32_t *)malloc((size_t)C * ev_cap * 16);
         uint32_t *tr = (uint32_t *)malloc((size_t)C * tr_cap * 16);
         uint32_t *ms = (uint32_t *)malloc((size_t)C * ms_cap * 8);
-        for (uint32_t c = 0; c < C; c++) {
+        const int bad = !lo || !ev || !tr || !ms;
+        oom |= bad;
+        for (uint32_t c = 0; c < C && !bad; c++) {
             lo[c].ev = ev + (size_t)c * ev_cap * 4;
             lo[c].tr = tr + (size_t)c * tr_cap * 4; lo[c].meas = ms + (size_t)c * ms_cap * 2;
         }
@@ -626,6 +630,7 @@ int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint
         uint32_t ni[DPEMU_MAX_CORES];
         #pragma omp for schedule(dynamic, 4)
         for (int64_t si = 0; si < (int64_t)n_shots; si++) {
+            if (bad) continue;   /* (no break inside an omp for) */
             const uint64_t shot = shot_begin + (uint64_t)si;
             const uint32_t g = (uint32_t)((shot / cfg->shots_per_group) % cfg->n_groups);
             for (uint32_t c = 0; c < C; c++) {
@@ -647,5 +652,5 @@ int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint
         }
         free(lo); free(ev); free(tr); free(ms);
     }
-    return done;
+    return oom ? -1 : done;
 }

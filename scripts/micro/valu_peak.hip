@@ -1,21 +1,34 @@
-// VALU issue-rate microbenchmark (re-measure the int32 VALU peak).
-// Each lane runs CH independent add/xor chains for ITERS iterations; the VALU
-// instruction count per wave is read from the disassembly (printed by the
-// driver script) and divided by the hipEvent-timed kernel duration.
+// VALU issue-rate microbenchmark (re-measure the int32 VALU
+// peak, VERDICT r02 "next" item 1).  Each lane runs CH independent integer
+// chains (add / shift / xor: the interpreter's instruction mix) for ITERS
+// iterations, at W waves per SIMD (256 * W workgroups of 4 waves).  The
+// instruction count is NOT inferred here: rocprofv3 --pmc SQ_INSTS_VALU
+// GRBM_GUI_ACTIVE (one pass, scripts/valu_peak_summary.py) gives the VALU
+// instructions per launch and the shader clock, and the kernel trace the
+// duration; this program only launches each variant REPS times (and prints
+// its HIP-event time so a run without the profiler is still informative).
+//
+//   ./valu_peak [iters]          kernels valu_kernel<CH, W> for CH in {1,2,4,8}, W in {1,2,4,8}
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
 
-template <int CH>
-__global__ void __launch_bounds__(256) valu_kernel(uint32_t *out, uint32_t iters, uint32_t k) {
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+template <int CH, int W>
+__global__ void __launch_bounds__(256) valu_kernel(uint32_t *out, uint32_t iters, uint32_t k)
+{
     uint32_t a[CH];
 #pragma unroll
     for (int c = 0; c < CH; c++) a[c] = threadIdx.x * (c + 1) + blockIdx.x;
     for (uint32_t i = 0; i < iters; i++) {
 #pragma unroll
-        for (int c = 0; c < CH; c++) {
-            a[c] = (a[c] + k) ^ (a[c] >> 3);
-            a[c] = (a[c] - k) ^ (a[c] << 5);
+        for (int u = 0; u < 4; u++) {
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                a[c] = (a[c] + k) ^ (a[c] >> 3);
+                a[c] = (a[c] - k) ^ (a[c] << 5);
+            }
         }
     }
     uint32_t s = 0;
@@ -24,36 +37,51 @@ __global__ void __launch_bounds__(256) valu_kernel(uint32_t *out, uint32_t iters
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
-template <int CH>
-static void run(const char *name, uint32_t blocks, uint32_t iters, uint32_t *d) {
+template <int CH, int W>
+static void run(uint32_t iters, uint32_t *d, int reps)
+{
+    const uint32_t blocks = 256u * W;          // 256 CUs x 4 SIMDs x W waves = 256 W blocks of 4 waves
+    const uint32_t it = iters / CH;            // about the same instructions per lane for every CH
     hipEvent_t e0, e1;
-    hipEventCreate(&e0); hipEventCreate(&e1);
-    valu_kernel<CH><<<blocks, 256>>>(d, iters, 7u);
-    hipDeviceSynchronize();
-    float best = 1e30f;
-    for (int r = 0; r < 5; r++) {
-        hipEventRecord(e0);
-        valu_kernel<CH><<<blocks, 256>>>(d, iters, 7u);
-        hipEventRecord(e1);
-        hipEventSynchronize(e1);
-        float ms; hipEventElapsedTime(&ms, e0, e1);
-        if (ms < best) best = ms;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    hipLaunchKernelGGL((valu_kernel<CH, W>), dim3(blocks), dim3(256), 0, 0, d, it, 7u);
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f, sum = 0.f;
+    for (int r = 0; r < reps; r++) {
+        CHECK(hipEventRecord(e0));
+        hipLaunchKernelGGL((valu_kernel<CH, W>), dim3(blocks), dim3(256), 0, 0, d, it, 7u);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms < best ? ms : best;
+        sum += ms;
     }
-    const double waves = blocks * 4.0;
-    // each chain step: add, shr, xor, sub, shl, xor = 6 ops (the compiler may fuse to 4: v_add, v_xad/ v_lshl_xor...)
-    printf("{\"kernel\": \"%s\", \"chains\": %d, \"blocks\": %u, \"iters\": %u, \"ms\": %.4f, \"wave_iters_per_s\": %.4e}\n",
-           name, CH, blocks, iters, best, waves * iters * CH / (best * 1e-3));
+    printf("{\"kernel\": \"valu_kernel<%d, %d>\", \"chains\": %d, \"waves_per_simd\": %d, \"blocks\": %u, "
+           "\"iters\": %u, \"ms_min\": %.5f, \"ms_mean\": %.5f}\n", CH, W, CH, W, blocks, it, best, sum / reps);
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
 }
 
-int main() {
+template <int W>
+static void run_w(uint32_t iters, uint32_t *d, int reps)
+{
+    run<1, W>(iters, d, reps);
+    run<2, W>(iters, d, reps);
+    run<4, W>(iters, d, reps);
+    run<8, W>(iters, d, reps);
+}
+
+int main(int argc, char **argv)
+{
+    const uint32_t iters = argc > 1 ? (uint32_t)atoi(argv[1]) : 8192;
     uint32_t *d;
-    hipMalloc(&d, 256u * 65536u * 4u);
-    // 256 CU x 4 SIMD x w waves/SIMD = 256*w blocks of 4 waves
-    for (int w : {1, 2, 4, 8}) {
-        run<8>("ch8", 256 * w, 4096, d);
-        run<2>("ch2", 256 * w, 16384, d);
-        run<1>("ch1", 256 * w, 16384, d);
-    }
-    hipFree(d);
+    CHECK(hipMalloc(&d, 256u * 8u * 256u * 4u));
+    run_w<1>(iters, d, 5);
+    run_w<2>(iters, d, 5);
+    run_w<4>(iters, d, 5);
+    run_w<8>(iters, d, 5);
+    CHECK(hipFree(d));
     return 0;
 }

@@ -1,4 +1,4 @@
-"""Clean-room assembler (distributed_processor_amd.assembler) vs the reference
+"""The API-compatible assembler restatement (distributed_processor_amd.assembler) vs the reference
 GlobalAssembler, byte for byte.
 
 Inputs: the reference's compiler golden programs (python/test/test_outputs/*.txt,

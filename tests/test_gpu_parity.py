@@ -166,7 +166,7 @@ def test_config1_golden_program(emu, golden_dir):
                                   'test_simple_loop'])
 def test_restated_assembler_goldens(emu, name):
     """the reference's compiler golden programs, assembled by this framework's
-    clean-room GlobalAssembler (byte-identical to the reference's, see
+    API-compatible GlobalAssembler restatement (byte-identical to the reference's, see
     tests/test_assembler.py), run on the GPU against oracle_fast"""
     from distributed_processor_amd import hwconfig
     from tests.test_assembler import assemble

@@ -194,3 +194,41 @@ def test_pipeline_clear_next_batches(hist_flags):
     for j, b in enumerate((batches - 2, batches - 1)):
         ref = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, b * n, n, want=('hist',))['hist']
         np.testing.assert_array_equal(got[j], ref.astype(np.int64))
+
+
+def test_empty_run_ordered_across_streams():
+    """an empty run's hist_next clear is in call order like any other call
+    (include/dpemu.h): a 10^6-shot run accumulating into H on one stream,
+    then an empty run on another stream naming H as hist_next, must leave H
+    zero -- the clear waits for the earlier run's counts"""
+    import torch
+    ps = ProgramSet(workloads.config2_ramsey(8, 100))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=8, meas_cap=2, seed=0x5EED, p1=0.5)
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    with Emulator(0) as emu:
+        emu.load(ps)
+        out = alloc_device_outputs(cfg, 10 ** 6, want=('summary', 'events', 'meas', 'hist'))
+        H = out['hist']
+        for _ in range(3):
+            emu.run_device(cfg, 10 ** 6, 0, out, a)
+            emu.run_device(cfg, 0, 0, {'hist_next': H}, b)
+            torch.cuda.synchronize()
+            assert not H.any()
+
+
+@pytest.mark.parametrize('short', [0, 1, 3])
+def test_load_programs_bounds_in_commands(short):
+    """dpemu_load_programs' n_cmds counts 16-byte commands: a caller passing
+    fewer commands than a program spans (e.g. the u32 count / 4 off by a
+    few, or a truncated buffer) gets DPEMU_E_INVALID, never a read past it"""
+    import ctypes as C
+    ps = ProgramSet(workloads.config2_ramsey(8, 4))
+    need = int((ps.offsets.astype(np.int64) + ps.n_instr).max())
+    with Emulator(0) as emu:
+        L = emu._L
+        n = need - short
+        rc = L.dpemu_load_programs(emu._h, ps.words.ctypes.data, n, ps.offsets.ctypes.data, ps.n_instr.ctypes.data,
+                                   ps.n_programs, ps.table.ctypes.data, ps.n_groups, ps.cores_per_shot)
+        assert (rc == 0) == (short == 0), (short, rc)
+        if rc:
+            assert rc == -22 and b'run past' in L.dpemu_last_error(emu._h)
