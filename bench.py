@@ -12,6 +12,9 @@ scaling).  After the timed steps a fixed sample of lane timelines is gathered
 to every rank (sharding.gather_sample).
 
 Sub-objects on the same line, each with its own roofline and CPU baselines:
+  "config1"       config 1: the reference's golden single-core program
+                  (test_linear_compile_globalasm core 0) at 10^6 shots, beside
+                  oracle_rtl (the per-clock stand-in for the Verilator testbench)
   "dds"           config 5: RB timelines (8 cores, depth 200) synthesised to
                   int16 I/Q on 16 channels per sequence at 16 samples/clk
   "active_reset"  config 3: fproc_meas branching + sync barriers, 1.25*10^6
@@ -45,8 +48,20 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s
-VALU_PEAK = 7.7e11             # wave64 integer-VALU instructions/s, measured (profiles/r01_valu_peak.jsonl)
-PROFILE_TAG = 'r02'            # profiles/<tag>_*: rocprofv3 kernel stats and PMC passes of this bench
+PROFILE_TAG = 'r03'            # profiles/<tag>_*: rocprofv3 kernel stats and PMC passes of this bench
+
+
+def _valu_peak():
+    """the measured wave64 integer-VALU issue peak (instructions/s, whole chip)
+    and its cycles per instruction: scripts/micro/valu_peak.hip under
+    rocprofv3 with SQ_INSTS_VALU + GRBM_GUI_ACTIVE in one pass
+    (profiles/r03_valu_peak_pmc.json, scripts/valu_peak_summary.py)"""
+    with open(os.path.join(REPO, 'profiles', 'r03_valu_peak_pmc.json')) as f:
+        v = json.load(f)
+    return v['peak_valu_insts_per_s'], v['peak_cycles_per_inst'], v['peak_variant']
+
+
+VALU_PEAK, VALU_CPI, VALU_PEAK_VARIANT = _valu_peak()
 # where they are read from: the committed profiles/, or (DPEMU_BENCH_PROFILES)
 # the summaries of a profile pass just taken on the same box
 PROFILE_DIR = os.environ.get('DPEMU_BENCH_PROFILES') or os.path.join(REPO, 'profiles')
@@ -121,11 +136,28 @@ def rocprof_avg_ms(kernel_substr):
     return None
 
 
-def valu_view(prof):
-    if not prof:
+def valu_view(prof, kernel_ms=None):
+    """the kernel's VALU roofline beside its HBM one: VALU instructions per
+    launch (rocprof SQ_INSTS_VALU) over the kernel time against the measured
+    integer-VALU issue peak -- at the bench's HIP-event kernel time (`frac`)
+    and at rocprof's trace duration (`frac_rocprof`, = pmc_summary's
+    valu_frac_of_measured_peak) -- plus the same-pass PMC ratios"""
+    if not prof or not prof.get('SQ_INSTS_VALU'):
         return None
-    return {k: prof.get(k) for k in ('valu_insts_per_wave', 'valu_issue_pct', 'valu_busy_pct',
-                                     'valu_lane_util_pct', 'duration_ns', 'kernel', 'SQ_INSTS_VALU')}
+    n = float(prof['SQ_INSTS_VALU'])
+    v = {'bound': 'valu', 'unit': 'wave64 VALU instr/s', 'peak': VALU_PEAK, 'peak_cycles_per_inst': VALU_CPI,
+         'peak_source': 'profiles/r03_valu_peak_pmc.json ({})'.format(VALU_PEAK_VARIANT),
+         'valu_insts_per_launch': n}
+    if kernel_ms:
+        v['achieved'] = n / (kernel_ms * 1e-3)
+        v['frac'] = v['achieved'] / VALU_PEAK
+    if prof.get('duration_ns'):
+        v['frac_rocprof'] = n / (prof['duration_ns'] * 1e-9) / VALU_PEAK
+    for k in ('valu_insts_per_wave', 'valu_issue_pct', 'valu_busy_pct', 'valu_lane_util_pct', 'duration_ns',
+              'kernel', 'warnings'):
+        if prof.get(k) is not None:
+            v[k] = prof.get(k)
+    return v
 
 
 def hbm_roofline(alg_bytes, kernel_ms, ms_per_step, kernel, prof, rocprof_key):
@@ -319,7 +351,7 @@ def leg_ramsey(emu, args, world, rank, stream):
     prof = pmc('ramsey') if args.shots == 10 ** 6 else None         # profiled at the default size only
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'straight_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
-    roof['valu'] = valu_view(prof)
+    roof['valu'] = valu_view(prof, roof['kernel_ms'])
     res = {'value': n * 8 * world * args.steps / dt, 'ms_per_step': ms_step,
            'shots_per_s': n * world * args.steps / dt,
            'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * args.steps / dt,
@@ -332,6 +364,63 @@ def leg_ramsey(emu, args, world, rank, stream):
                       'global_shots_per_step': n * world, 'parallelism': 'shots sharded, {} GPU(s)'.format(world)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baselines(ps, cfg, 4096, 'config 2 Ramsey')
+    del out
+    torch.cuda.empty_cache()
+    return res
+
+
+def leg_config1(emu, args, world, rank, stream):
+    """config 1 (BASELINE configs[0]): the reference's own golden machine
+    code -- core 0 of python/test/test_outputs/test_linear_compile_globalasm.txt
+    (phase reset, X90, readout drive, readout LO, done; the fixture
+    tests/golden/cmd_buf_golden.json holds its bytes) -- at 10^6 shots per GPU.
+    The reference runs this program on the single-core Verilator/cocotb
+    testbench (cocotb/proc/Makefile:1-14), which cannot run here or on the
+    box: oracle_rtl, the per-clock restatement of hdl/, is its stand-in in
+    cpu_baseline (1 thread and every granted thread), oracle_fast beside it."""
+    import torch
+    from distributed_processor_amd import _abi, sharding
+    from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
+    with open(os.path.join(REPO, 'tests', 'golden', 'cmd_buf_golden.json')) as f:
+        gold = json.load(f)
+    ps = ProgramSet([{0: bytes.fromhex(gold['cores']['0']['cmd_buf'])}])
+    emu.load(ps)
+    cfg = _abi.make_config(1, max_cycles=10000, event_cap=8, trace_cap=0, meas_cap=4, seed=0x5EED, p1=0.5)
+    shot0, n = sharding.weak_shard(args.c1_shots, rank)
+    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
+    pipe = sharding.HistogramPipeline(out['hist'], zero=False, clear_next=True)
+
+    def launch(h, h_next):
+        out['hist'], out['hist_next'] = h, h_next
+        emu.run_device(cfg, n, shot0, out, stream)
+    step = lambda: pipe.step(launch)
+    dt = timed(step, pipe.drain, args.steps, args.warmup, world)
+    kernel_ms, kernel_ms_blk = interp_kernel_ms(emu, cfg, n, shot0, out, stream, args.steps, step, pipe.drain)
+    kernel = emu.last_kernel()
+    summ = out['summary'].cpu().numpy().view(np.uint32)
+    s = _abi.unpack_summary(summ)
+    assert (s['status'] == _abi.ST_DONE).all(), 'config 1: not every lane reached DONE'
+    assert int(pipe.result().sum().item()) == n * world
+    ms_step = dt / args.steps * 1e3
+    alg = float(bytes_per_lane(summ, cfg).sum())
+    prof = pmc('config1') if args.c1_shots == 10 ** 6 else None
+    roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'straight_kernel')
+    roof['kernel_ms_block'] = kernel_ms_blk
+    roof['valu'] = valu_view(prof, roof['kernel_ms'])
+    res = {'metric': 'emulated core-shots/s (config 1: the reference\'s golden single-core program, '
+                     'test_linear_compile_globalasm core 0)',
+           'value': n * world * args.steps / dt, 'unit': 'core-shots/s', 'ms_per_step': ms_step, 'kernel_ms': kernel_ms,
+           'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * args.steps / dt,
+           'instructions_per_s': float(s['n_instr'].astype(np.float64).sum()) * world * args.steps / dt,
+           'config': {'workload': 'config1_golden_linear_core0', 'shots_per_gpu': n, 'cores_per_shot': 1,
+                      'program': gold['source'] + ' core 0', 'commands': int(ps.words.shape[0])},
+           'roofline': roof}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baselines(ps, cfg, 2048, 'config 1 golden program')
+        cb['substitute_for'] = ('the reference\'s single-core Verilator/cocotb testbench (cocotb/proc/Makefile:1-14, '
+                                'sim_modules/toplevel_sim.sv), absent from this image: oracle_rtl is the per-clock '
+                                'restatement of the same RTL, timed at 1 thread and at every granted thread')
+        res['cpu_baseline'] = cb
     del out
     torch.cuda.empty_cache()
     return res
@@ -425,7 +514,7 @@ def leg_active_reset(emu, args, world, rank, stream):
     ms_step = dt / args.steps * 1e3
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'branch_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
-    roof['valu'] = valu_view(prof)
+    roof['valu'] = valu_view(prof, roof['kernel_ms'])
     res = {'metric': 'emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
                      '1.25e6 shots/GPU)',
            'value': n * 8 * world * args.steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * args.steps / dt,
@@ -485,16 +574,13 @@ def leg_rb(emu, args, world, rank, stream):
     k_ms = min(kernel_ms, ms_step)
     prof = pmc('rb') if (args.rb_seqs, args.rb_spg) == (100000, 10) else None
     alg = float(bytes_per_lane(summ, cfg).sum())
-    hbm = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'macro_kernel')
+    hbm = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, kernel.split('<')[0])
     hbm['kernel_ms_block'] = kernel_ms_blk
-    if prof and prof.get('SQ_INSTS_VALU'):
-        valu_per_launch = float(prof['SQ_INSTS_VALU'])
-        achieved = valu_per_launch / (k_ms * 1e-3)
-        roof = {'bound': 'valu', 'achieved': achieved, 'peak': VALU_PEAK, 'unit': 'wave64 VALU instr/s',
-                'frac': achieved / VALU_PEAK, 'kernel_ms': k_ms, 'kernel': hbm['kernel'],
-                'valu_ops_per_instruction': valu_per_launch * 64 / instrs,
-                'active_lanes_per_valu_pct': prof.get('valu_lane_util_pct'),
-                'valu_insts_per_launch': valu_per_launch, 'hbm': hbm, 'valu': valu_view(prof)}
+    valu = valu_view(prof, k_ms)
+    if valu:
+        roof = dict(valu, kernel_ms=k_ms, kernel=hbm['kernel'],
+                    valu_ops_per_instruction=valu['valu_insts_per_launch'] * 64 / instrs,
+                    active_lanes_per_valu_pct=prof.get('valu_lane_util_pct'), traffic=hbm['traffic'], hbm=hbm)
     else:
         roof = hbm
     res = {'metric': 'emulated core-shots/s (config 4: 2-qubit RB, 1e5 sequences x depth 200, 10 shots each)',
@@ -526,7 +612,8 @@ def main():
     ap.add_argument('--ar-shots', type=int, default=1250000, help='config-3 shots per GPU per step')
     ap.add_argument('--rb-seqs', type=int, default=100000, help='config-4 RB sequences')
     ap.add_argument('--rb-spg', type=int, default=10, help='config-4 shots per sequence')
-    ap.add_argument('--legs', default='dds,active_reset,rb', help='sub-legs to run (comma list; "" for none)')
+    ap.add_argument('--c1-shots', type=int, default=10 ** 6, help='config-1 shots per GPU per step')
+    ap.add_argument('--legs', default='config1,dds,active_reset,rb', help='sub-legs to run (comma list; "" for none)')
     args = ap.parse_args()
 
     import torch
@@ -567,7 +654,7 @@ def main():
               'cpu_baseline'):
         if k in main_leg:
             result[k] = main_leg[k]
-    fns = {'dds': leg_dds, 'active_reset': leg_active_reset, 'rb': leg_rb}
+    fns = {'config1': leg_config1, 'dds': leg_dds, 'active_reset': leg_active_reset, 'rb': leg_rb}
     for name in [x for x in args.legs.split(',') if x]:
         result[name] = fns[name](emu, args, world, rank, stream)
     result['box'] = {'fill_GBps': fill_gbps(), 'device': torch.cuda.get_device_name(local)}

@@ -22,6 +22,7 @@ X_HIST_DIRECT = 0x4
 X_HIST_REPL = 0x8
 X_PROG_MAJOR = 0x10
 X_GENERAL = 0x20
+X_MACRO_DIRECT = 0x40
 
 STATUS_NAMES = {0: 'running', ST_DONE: 'done', ST_MAX_CYCLES: 'max_cycles',
                 ST_HUNG_OPCODE: 'hung_opcode', ST_DEADLOCK: 'deadlock'}

@@ -32,7 +32,9 @@
 //     stores, which share vmcnt with global loads on gfx950).
 //
 // Branches guard only stores, LDS writes and the measurement draw.  The
-// meas_lut back end (FEAT_LUT) stays on interp_kernel.
+// meas_lut back end (FEAT_LUT: hdl/fproc_lut.sv, core_state_mgr.sv,
+// meas_lut.sv) runs the LUT FSM in each shot's leader lane over the shot's
+// merged measurement stream, as interp_kernel does.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -45,7 +47,7 @@ namespace dpemu {
 
 namespace {
 
-enum : uint32_t { B_RUN = 0, B_SYNC = 1, B_FIN = 3 };
+enum : uint32_t { B_RUN = 0, B_SYNC = 1, B_LUT = 2, B_FIN = 3 };
 
 // decode-to-decode latency per op4 past the command's base cycle (D, the
 // trigger cycle tT for pulse-with-trigger / idle, the fproc ready cycle R):
@@ -104,13 +106,21 @@ template <int FEAT>
 __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 {
     constexpr bool FPROC = (FEAT & FEAT_FPROC) != 0;
+    constexpr bool LUT = (FEAT & FEAT_LUT) != 0;     // fproc_lut back end (exclusive with FPROC)
+    constexpr bool XMEAS = FPROC || LUT;             // measurements readable by the shot
     constexpr bool SYNC = (FEAT & FEAT_SYNC) != 0;
     constexpr bool REGS = (FEAT & FEAT_REGS) != 0;  // some command writes the reg_file (else it reads 0)
     constexpr bool PLDS = (FEAT & FEAT_PROG_LDS) != 0;   // the workgroup's programs staged in LDS
-    constexpr int MT = FPROC ? MEAS_LOOKUP : 1;
+    constexpr int MT = XMEAS ? MEAS_LOOKUP : 1;
+    constexpr int NF = LUT ? LUT_FIRE_CAP : 1;
 
     __shared__ uint32_t s_regs[REGS ? 16 : 1][REGS ? BLOCK : 1];
     __shared__ uint32_t s_mt[MT][BLOCK];              // measurements {valid cycle << 1 | bit}, readable by the shot
+    // meas_lut (hdl/meas_lut.sv, core_state_mgr.sv), per shot: the leader's
+    // merge cursor into each lane's s_mt, and the fires it published, each
+    // as {fire cycle << 1 | this lane's bit of lut_out}
+    __shared__ uint32_t s_cur[LUT ? BLOCK : 1];
+    __shared__ uint32_t s_fire[NF][LUT ? BLOCK : 1];
     __shared__ uint32_t s_pref[PLDS ? BLOCK + 1 : 1];
     __shared__ uint32_t s_scan[BLOCK / 64];
     // dynamic LDS: the staged programs (prog_lds_words commands), then the
@@ -157,10 +167,15 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 #pragma unroll
         for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
     }
-    if constexpr (FPROC) {
+    if constexpr (XMEAS) {
 #pragma unroll
         for (int m = 0; m < MT; m++) s_mt[m][tid] = INF32;
     }
+    if constexpr (LUT) s_cur[tid] = 0;
+    // leader-only meas_lut state (meas_lut.sv:27-56): OR-accumulated valid /
+    // measurement bits of the masked cores, the last fire, fires so far
+    uint64_t lut_valid = 0, lut_addr = 0;
+    uint32_t lut_last_fire = INF32, nfire = 0;
 
     uint32_t mode = valid ? B_RUN : B_FIN;
     // qclk(x) = x + qoff for every decode after the first (hdl/qclk.v: it
@@ -204,7 +219,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {   // meas_elem 0xFF: none
                 const uint32_t bit = meas_bit(p, shot, core, n_meas, thr_core, pa, pe);
                 const uint32_t tv = te + p.meas_latency;
-                if constexpr (FPROC) {
+                if constexpr (XMEAS) {
                     if (n_meas < (uint32_t)MT) s_mt[n_meas < (uint32_t)MT ? n_meas : 0u][tid] = (tv << 1) | bit;
                 }
                 if (p.meas && n_meas < p.meas_cap) p.meas[(uint64_t)n_meas * n_lanes + lane] = make_uint2(tv, bit);
@@ -242,9 +257,12 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     };
 
     // sync barrier keys: a participant's SYNC decode while it waits, its next
-    // decode while it runs (a lower bound of its arrival), INF once finished
+    // decode while it runs (a lower bound of its arrival), the earliest next
+    // decode after a release while it waits on the LUT (>= wait_d + 1 + 4),
+    // INF once finished
     auto sync_maxkey = [&]() -> uint32_t {
         uint32_t key = mode == B_SYNC ? wait_d : t;
+        if constexpr (LUT) key = mode == B_LUT ? wait_d + 5u : key;
         key = mode == B_FIN ? INF32 : key;
         return group_reduce<1>(is_part ? key : 0u, C);
     };
@@ -307,6 +325,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             }
         }
         const bool go = run && !stall;
+        bool sync_rel = false;                           // released from a sync barrier this iteration
         n_exec += go ? 1u : 0u;
         const uint32_t D = t;
         // qclk at this decode (0 in the reset hold)
@@ -378,36 +397,58 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             const uint32_t reg0 = reg(u.w >> 20);
             const uint32_t reg1 = reg(u.y >> 4);
             uint32_t data = 0;
-            const uint32_t R = D + 2u;                   // fproc_meas.sv:18-35: ready two cycles after the read
+            uint32_t R = D + 2u;                         // fproc_meas.sv:18-35: ready two cycles after the read
+            bool lut_wait = false, no_meas = false;
             if constexpr (FPROC) {
                 if (__any(sg && is_fp)) {
                     if (sg && is_fp) data = meas_lookup(leader_tid + (((u.z >> 16) & 0xFFu) & (C - 1u)), D);
                 }
             }
+            if constexpr (LUT) {
+                // core_state_mgr.sv:45-69: id 0 waits for this core's next
+                // meas_valid (>= D + 1: recorded already -- the core's own
+                // strobes precede it -- or never), id != 0 for the LUT
+                if (__any(sg && is_fp)) {
+                    const bool id0 = ((u.z >> 16) & 0xFFu) == 0u;
+                    lut_wait = sg && is_fp && !id0;
+                    if (sg && is_fp && id0) {
+                        uint32_t e = INF32;
+#pragma unroll
+                        for (int m = MT - 1; m >= 0; m--) {
+                            const uint32_t x = s_mt[m][tid];
+                            e = (x != INF32 && (x >> 1) >= D + 1u) ? x : e;
+                        }
+                        no_meas = e == INF32;
+                        R = e >> 1;
+                        data = e & 1u;
+                    }
+                }
+            }
             const uint32_t in0 = (u.y & 8u) ? reg0 : u.x;
             const uint32_t out = alu_eval(u.y & 7u, in0, op == 6u ? qD : is_fp ? data : reg1);
             // not reached (the host picks kernels by opcode): fproc / sync without the feature
-            const bool absent = (!FPROC && is_fp) || (!SYNC && op == 7u);
-            const bool r_over = FPROC && is_fp && R > max_cycles;
-            const bool fin = r_over || absent;
+            const bool absent = (!XMEAS && is_fp) || (!SYNC && op == 7u);
+            const bool r_over = XMEAS && is_fp && !lut_wait && !no_meas && R > max_cycles;
+            const bool fin = r_over || absent || no_meas;
             const bool cont = sg && !fin;
             const bool to_sync = SYNC && cont && op == 7u;
-            const bool adv = cont && !to_sync;
+            const bool to_lut = LUT && cont && lut_wait;
+            const bool adv = cont && !to_sync && !to_lut;
             const uint32_t t_next = (is_fp ? R : D) + (uint32_t)((LATENCY >> (4u * op)) & 15u);
             const bool take = op == 2u || ((op == 3u || op == 5u) && (out & 1u));
             const uint32_t ip_next = take ? (u.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
             // reg_file write (reg_alu, alu_fproc) and the register / qclk trace
-            const bool wr = cont && (op == 1u || op == 4u);
+            const bool wr = adv && (op == 1u || op == 4u);
             if constexpr (REGS) {
                 if (wr) s_regs[(u.y >> 8) & 15u][tid] = out;
             }
-            const bool inc = cont && op == 6u;
+            const bool inc = adv && op == 6u;
             emit_trace(wr || inc, (op == 4u ? R : D) + 3u, inc ? TRACE_QCLK_LOAD : (u.y >> 8) & 15u,
                        inc ? out + 3u : out);
             qoff = inc ? out - D : qoff;                 // qclk(D + 3) = out + 3
             finish(sg && fin, r_over ? ST_MAX_CYCLES : ST_DEADLOCK, D);
-            wait_d = to_sync ? D : wait_d;
-            mode = to_sync ? B_SYNC : mode;
+            wait_d = (to_sync || to_lut) ? D : wait_d;
+            mode = to_sync ? B_SYNC : to_lut ? B_LUT : mode;
             ip = adv ? ip_next : ip;
             t = adv ? t_next : t;
         }
@@ -429,11 +470,127 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
                 t = ok ? S + 3u : t;
                 mode = ok ? B_RUN : mode;
                 finish(rel && !ok, ST_MAX_CYCLES, wait_d);
-                // a shot in which no lane retired or was released can never progress
-                finish(group_bits(__ballot(go || rel), wl, C) == 0ull && mode == B_SYNC, ST_DEADLOCK, wait_d);
+                sync_rel = rel;
+                // a shot in which no lane retired or was released can never
+                // progress (with the LUT: checked after the LUT phase below)
+                if constexpr (!LUT)
+                    finish(group_bits(__ballot(go || rel), wl, C) == 0ull && mode == B_SYNC, ST_DEADLOCK, wait_d);
             }
         }
-        if constexpr (FPROC) {   // this iteration's s_mt writes before the next iteration's reads
+
+        // ---- meas_lut (LUT): the shot's leader merges the group's recorded
+        // measurements in time order up to the horizon before which no
+        // measurement can still appear (the group's bound on its next strobe
+        // + meas_latency), runs the LUT FSM over them (hdl/meas_lut.sv:27-56:
+        // OR-accumulate the masked cores' valid / bits, fire when every masked
+        // core is valid, then clear; the cycle after a fire ignores inputs)
+        // and publishes the fires; a lane waiting on the LUT (core_state_mgr
+        // WAIT_LUT) takes the first fire after its read.  Skipped in
+        // iterations where no lane waits and no measurement is unmerged. ----
+        bool lut_rel = false;
+        if constexpr (LUT) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // this iteration's s_mt writes
+            __builtin_amdgcn_wave_barrier();
+            if (__any(mode == B_LUT || (valid && min(n_meas, (uint32_t)MT) > s_cur[tid]))) {
+                uint32_t bound = mode == B_RUN ? t + 2u : mode == B_LUT ? wait_d + 7u : INF32;
+                if constexpr (SYNC) {
+                    if (__any(mode == B_SYNC)) {
+                        const uint32_t maxkey = sync_maxkey();
+                        if (mode == B_SYNC && is_part && maxkey != INF32) bound = maxkey + p.sync_latency + 5u;
+                    }
+                }
+                const uint32_t gmin = group_reduce<0>(bound, C);
+                const bool any_run_grp = group_bits(__ballot(mode == B_RUN), wl, C) != 0ull;
+                bool fired = false;
+                if (tid == leader_tid && valid) {
+                    uint32_t H = INF32;
+                    if (any_run_grp && gmin != INF32) {
+                        const uint64_t h = (uint64_t)gmin + p.meas_latency - 1u;
+                        H = h > INF32 ? INF32 : (uint32_t)h;
+                    }
+                    // nothing runs: every later measurement follows a release, i.e. a fire
+                    const bool stop_at_fire = !any_run_grp;
+                    for (;;) {
+                        uint32_t tmin = INF32;
+                        for (uint32_t c = 0; c < C; c++) {
+                            const uint32_t cur = s_cur[tid + c];
+                            const uint32_t e = cur < (uint32_t)MT ? s_mt[cur < (uint32_t)MT ? cur : 0u][tid + c] : INF32;
+                            tmin = (e != INF32 && (e >> 1) < tmin) ? e >> 1 : tmin;
+                        }
+                        if (tmin == INF32 || tmin > H) break;
+                        uint64_t v = 0, mv = 0;
+                        for (uint32_t c = 0; c < C; c++) {
+                            const uint32_t cur = s_cur[tid + c];
+                            const uint32_t e = cur < (uint32_t)MT ? s_mt[cur < (uint32_t)MT ? cur : 0u][tid + c] : INF32;
+                            if (e != INF32 && (e >> 1) == tmin) {
+                                v |= 1ull << c;
+                                mv |= (uint64_t)(e & 1u) << c;
+                                s_cur[tid + c] = cur + 1u;
+                            }
+                        }
+                        if (lut_last_fire != INF32 && tmin == lut_last_fire + 1u) continue;
+                        const uint64_t nv = lut_valid | v, na = lut_addr | (v & mv);
+                        if (((uint64_t)p.lut_mask & nv) == (uint64_t)p.lut_mask) {
+                            lut_last_fire = tmin;
+                            if (nfire < (uint32_t)NF) {
+                                const uint64_t o = p.lut_table[na & 0xFFu];
+                                for (uint32_t c = 0; c < C; c++)
+                                    s_fire[nfire < (uint32_t)NF ? nfire : 0u][tid + c] = (tmin << 1) | (uint32_t)((o >> c) & 1ull);
+                            }
+                            nfire++;
+                            lut_valid = 0;
+                            lut_addr = 0;
+                            fired = true;
+                            if (stop_at_fire) break;
+                        } else {
+                            lut_valid = nv;
+                            lut_addr = na;
+                        }
+                    }
+                }
+                const uint32_t nf_grp = (uint32_t)__shfl((int)nfire, (int)(wl & ~(C - 1u)), 64);
+                const bool grp_fired = group_bits(__ballot(fired), wl, C) != 0ull;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (mode == B_LUT) {
+                    const uint32_t n = nf_grp < (uint32_t)NF ? nf_grp : (uint32_t)NF;
+                    for (uint32_t k = 0; k < n; k++) {
+                        const uint32_t f = s_fire[k][tid], tf = f >> 1;
+                        if (tf >= wait_d + 1u) {
+                            // the waiting alu_fproc / jump_fproc (ip has not moved)
+                            const uint4 u2 = PLDS ? s_prog[fetch_off + min(ip, k_max)]
+                                                  : p.fetch[(uint64_t)min(ip, k_max) * p.fetch_stride + fetch_off];
+                            const uint32_t op2 = u2.y >> 28;
+                            const uint32_t in0b = (u2.y & 8u) ? reg(u2.w >> 20) : u2.x;
+                            const uint32_t outb = alu_eval(u2.y & 7u, in0b, f & 1u);
+                            if (tf > max_cycles) {
+                                finish(true, ST_MAX_CYCLES, wait_d);
+                            } else if (op2 == 4u) {
+                                const uint32_t rd = (u2.y >> 8) & 15u;
+                                if constexpr (REGS) s_regs[rd][tid] = outb;
+                                emit_trace(true, tf + 3u, rd, outb);
+                                ip = (ip + 1u) & 0xFFFFu;
+                                t = tf + 4u;
+                                mode = B_RUN;
+                            } else {
+                                ip = (outb & 1u) ? (u2.z & 0xFFFFu) : ((ip + 1u) & 0xFFFFu);
+                                t = tf + 6u;
+                                mode = B_RUN;
+                            }
+                            lut_rel = true;
+                            break;
+                        }
+                    }
+                }
+                lut_rel = lut_rel || (grp_fired && tid == leader_tid);
+            }
+            // a shot in which no lane retired or was released can never progress
+            if (__any(mode == B_SYNC || mode == B_LUT)) {
+                const uint64_t pm = __ballot(go || sync_rel || lut_rel);
+                finish(group_bits(pm, wl, C) == 0ull && (mode == B_SYNC || mode == B_LUT), ST_DEADLOCK, wait_d);
+            }
+        }
+        if constexpr (XMEAS) {   // this iteration's s_mt writes before the next iteration's reads
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
@@ -480,9 +637,10 @@ hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
     if (blocks == 0) return hipSuccess;
-    switch (feat & (FEAT_FPROC | FEAT_SYNC | FEAT_REGS | FEAT_PROG_LDS)) {
+    switch (feat & (FEAT_FPROC | FEAT_LUT | FEAT_SYNC | FEAT_REGS | FEAT_PROG_LDS)) {
 #define CASE(F) case F: return launch_f<F>(p, blocks, stream);
-#define CASES(L) CASE(L) CASE(L | FEAT_FPROC) CASE(L | FEAT_SYNC) CASE(L | FEAT_FPROC | FEAT_SYNC)
+#define CASES(L) CASE(L) CASE(L | FEAT_FPROC) CASE(L | FEAT_SYNC) CASE(L | FEAT_FPROC | FEAT_SYNC) \
+                 CASE(L | FEAT_LUT) CASE(L | FEAT_LUT | FEAT_SYNC)
     CASES(0) CASES(FEAT_REGS) CASES(FEAT_PROG_LDS) CASES(FEAT_REGS | FEAT_PROG_LDS)
 #undef CASES
 #undef CASE

@@ -32,6 +32,10 @@ struct dpemu_ctx {
     uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
     uint32_t n_programs = 0, n_groups = 0, C = 0;
     bool has_fproc = false, has_sync = false, straight = false, linear = false, reg_writes = false;
+    // register slots of the macro image (remap_macro_regs): 2 or 4 in VGPRs, else 16 (identity map)
+    int macro_nr = 16;
+    uint64_t reg_map = 0xFEDCBA9876543210ull, reg_inv = 0xFEDCBA9876543210ull;
+    uint32_t reg_used = 0xFFFFu;
     uint32_t max_len = 0;              // longest program (commands)
     std::vector<uint64_t> group_len;   // instructions of all C programs of each group
     // run constants
@@ -149,6 +153,54 @@ static void build_macros(const uint32_t *u, uint32_t n, std::vector<uint32_t> &o
         out.insert(out.end(), m, m + 8);
         if (op4 == 0x0 || op4 == 0xA || op4 >= 0xD) return;
     }
+}
+
+// The reg_file registers the macro image names (ALU slot ctl: rs0 when
+// in0_reg, rd and rs1 of reg_alu; pulse slot: rs0 when a field is
+// register-sourced; an operand the ALU op ignores -- in1 of id0 / zero, in0
+// of id1 / zero -- names nothing) renumbered to slots 0..n-1 in place when
+// there are at most 2, so macro_staged_kernel keeps them in VGPRs.  Unnamed
+// registers are never written and read as 0 (reg_file.v resets to 0); a
+// field that names no register maps to slot 0 (its value is selected away).
+// Returns the slot count (2, or 16 = left as is) and the maps
+// (KParams::reg_map / reg_inv).
+static int remap_macro_regs(std::vector<uint32_t> &mac, uint64_t &map, uint64_t &inv, uint32_t &used)
+{
+    used = 0;
+    for (size_t i = 0; i < mac.size(); i += 8) {
+        for (int a = 0; a < 2; a++) {
+            const uint32_t ctl = mac[i + 2 * a + 1];
+            if (!(ctl >> 31)) continue;
+            const uint32_t op = ctl & 7u;                       // alu.v: 0 id0, 6 id1, 7 zero
+            if ((ctl & 8u) && op != 6u && op != 7u) used |= 1u << ((ctl >> 12) & 15u);
+            if (!((ctl >> 30) & 1u)) {
+                used |= 1u << ((ctl >> 8) & 15u);
+                if (op != 0u && op != 7u) used |= 1u << ((ctl >> 4) & 15u);
+            }
+        }
+        const uint32_t w = mac[i + 7];
+        if (!(w >> 31) && (w & UOP_ANY_RS)) used |= 1u << ((w >> 20) & 15u);
+    }
+    const int n = __builtin_popcount(used);
+    if (n > 2) {
+        map = inv = 0xFEDCBA9876543210ull;
+        used = 0xFFFFu;
+        return 16;
+    }
+    uint32_t slot[16] = {0};
+    map = inv = 0;
+    for (uint32_t r = 0, k = 0; r < 16; r++)
+        if ((used >> r) & 1u) { slot[r] = k; map |= (uint64_t)k << (4 * r); inv |= (uint64_t)r << (4 * k); k++; }
+    auto re = [&](uint32_t v, int sh) { return (v & ~(15u << sh)) | (slot[(v >> sh) & 15u] << sh); };
+    for (size_t i = 0; i < mac.size(); i += 8) {
+        for (int a = 0; a < 2; a++) {
+            uint32_t &ctl = mac[i + 2 * a + 1];
+            if (ctl >> 31) ctl = re(re(re(ctl, 12), 8), 4);
+        }
+        uint32_t &w = mac[i + 7];
+        if (!(w >> 31) && (w & UOP_ANY_RS)) w = re(w, 20);
+    }
+    return 2;
 }
 
 static void free_programs(dpemu_ctx *ctx)
@@ -304,6 +356,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, 
             if (mac.size() / 8 >= (1ull << 32)) return fail(ctx, DPEMU_E_INVALID, "macro image exceeds 2^32 macros");
         }
         moff[n_programs] = (uint32_t)(mac.size() / 8);
+        ctx->macro_nr = remap_macro_regs(mac, ctx->reg_map, ctx->reg_inv, ctx->reg_used);
         HIPCHK(ctx, hipMalloc(&ctx->d_macro, mac.size() * 4));
         HIPCHK(ctx, hipMemcpy(ctx->d_macro, mac.data(), mac.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(ctx, hipMalloc(&ctx->d_moff, moff.size() * 4));
@@ -389,6 +442,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.offsets = ctx->d_offsets; p.n_instr = ctx->d_ninstr; p.prog_table = ctx->d_table;
     p.max_len = ctx->max_len;
     p.macros = ctx->d_macro; p.macro_off = ctx->d_moff;
+    p.reg_map = ctx->reg_map; p.reg_inv = ctx->reg_inv; p.reg_used = ctx->reg_used;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
     p.summary = out->summary;
     p.events = reinterpret_cast<uint4 *>(out->events);
@@ -462,6 +516,24 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     const int fetch_batch = small ? 4 : 1;
     const bool uniform = ctx->straight && ctx->max_len < 65536u && !(cfg->exec_flags & DPEMU_X_GENERAL);
     const bool macro = !uniform && ctx->d_macro && !(cfg->exec_flags & (DPEMU_X_GENERAL | DPEMU_X_PROG_LDS));
+    // the staged macro kernel needs at most MACRO_SLOTS distinct programs per
+    // wave: (program groups a wave's run of consecutive shots can span) x
+    // (cores in the wave), for the thread mapping of block_core_major
+    bool staged = false;
+    if (macro && !(cfg->exec_flags & DPEMU_X_MACRO_DIRECT)) {
+        uint64_t shots_run, cores_w;
+        if (cfg->lane_order == DPEMU_LANES_SHOT_MAJOR) {
+            shots_run = std::max<uint64_t>(1, 64 / C);
+            cores_w = std::min<uint64_t>(C, 64);
+        } else {
+            const uint64_t Sb = BLOCK / C;
+            shots_run = std::min<uint64_t>(Sb, 64);
+            cores_w = 64 / shots_run;
+        }
+        const uint64_t spg = cfg->shots_per_group;
+        const uint64_t groups = ng == 1 ? 1 : std::min<uint64_t>(ng, (shots_run - 1 + spg - 1) / spg + 1);
+        staged = groups * cores_w <= MACRO_SLOTS;
+    }
     int src = cmd_major ? STRAIGHT_ROWS : STRAIGHT_PROG;
     if (uniform) {
         const uint64_t per_cu = std::min<uint64_t>(8, std::max<uint64_t>(1, (blocks + 255) / 256));
@@ -521,15 +593,14 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             hist_stride = stride;
         }
     }
-    // branch.hip for every other program, except the meas_lut back end, which
-    // the general interpreter runs (and DPEMU_X_GENERAL / DPEMU_X_PROG_LDS:
-    // everything on it).  Its workgroup's programs are staged in LDS when
-    // they are few commands: a fetch from LDS does not wait behind the lane's
-    // event stores, which share vmcnt with global loads on gfx950
+    // branch.hip for every other program, the meas_lut back end included
+    // (DPEMU_X_GENERAL / DPEMU_X_PROG_LDS: everything on the general
+    // interpreter).  Its workgroup's programs are staged in LDS when they are
+    // few commands: a fetch from LDS does not wait behind the lane's event
+    // stores, which share vmcnt with global loads on gfx950
     // (DPEMU_X_PROG_MAJOR keeps the global fetch).
-    const bool branch = !uniform && !macro && !(feat & FEAT_LUT) &&
-                        !(cfg->exec_flags & (DPEMU_X_GENERAL | DPEMU_X_PROG_LDS));
-    int bfeat = (feat & (FEAT_FPROC | FEAT_SYNC)) | (ctx->reg_writes ? FEAT_REGS : 0);
+    const bool branch = !uniform && !macro && !(cfg->exec_flags & (DPEMU_X_GENERAL | DPEMU_X_PROG_LDS));
+    int bfeat = (feat & (FEAT_FPROC | FEAT_LUT | FEAT_SYNC)) | (ctx->reg_writes ? FEAT_REGS : 0);
     if (branch) {
         p.prog_lds_words = 0;
         if (footprint <= BRANCH_LDS_MAX && !(cfg->exec_flags & DPEMU_X_PROG_MAJOR)) {
@@ -545,7 +616,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
-    else if (macro) HIPCHK(ctx, launch_macro(p, stream));
+    else if (macro) HIPCHK(ctx, launch_macro(p, staged, ctx->macro_nr, stream));
     else if (branch) HIPCHK(ctx, launch_branch(p, bfeat, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, stream));
@@ -554,6 +625,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
         if (uniform)
             snprintf(name, sizeof name, "straight_kernel<%s,fb%d>",
                      src == STRAIGHT_ROWS ? "rows" : src == STRAIGHT_PROG ? "prog" : "lds", fetch_batch);
+        else if (macro && staged)
+            snprintf(name, sizeof name, "macro_staged_kernel<%d>", ctx->macro_nr);
         else if (macro)
             snprintf(name, sizeof name, "macro_kernel");
         else if (branch)

@@ -108,6 +108,9 @@ struct KParams {
     uint32_t max_len;             // longest program; the command-major image's guard row
     const uint4 *macros;          // macro.hip image: 2 x uint4 per macro (capi.cpp build_macros)
     const uint32_t *macro_off;    // [n_programs + 1]: program p's macros [macro_off[p], macro_off[p + 1])
+    uint64_t reg_map;             // macro image register slots: reg_file register r is slot (reg_map >> 4 r) & 15
+    uint64_t reg_inv;             //   for r in the reg_used mask (others are never named: they read 0);
+    uint32_t reg_used;            //   slot s holds register (reg_inv >> 4 s) & 15 (trace addresses)
     const uint32_t *p1_thr;
     const uint64_t *lut_table;
     // outputs (device, nullable); lane L = core * n_shots + shot (core-major)
@@ -150,8 +153,13 @@ constexpr uint32_t STRAIGHT_LDS_MAX = 9216;   // commands (144 KiB) of dynamic L
 hipError_t launch_straight(const KParams &p, int src, int fb, hipStream_t stream);
 // programs with jumps / fproc_meas / sync (branch.hip): FEAT_FPROC | FEAT_SYNC | FEAT_REGS | FEAT_PROG_LDS bits of feat
 hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream);
-// branch-free programs with reg_alu / inc_qclk (macro.hip)
-hipError_t launch_macro(const KParams &p, hipStream_t stream);
+// branch-free programs with reg_alu / inc_qclk (macro.hip): macro_staged_kernel
+// when every wave runs at most MACRO_SLOTS distinct programs (nr = the
+// register slots the macro image names: 2, else 16 in LDS), else
+// macro_kernel (staged = false)
+constexpr uint32_t MACRO_SLOTS = 8;     // distinct programs per wave whose macros are staged in LDS
+constexpr uint32_t MACRO_CHUNK = 8;     // macros per program per staged chunk
+hipError_t launch_macro(const KParams &p, bool staged, int nr, hipStream_t stream);
 constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no command; ALU ctl bit 31: present
 
 // ---- DDS ------------------------------------------------------------------

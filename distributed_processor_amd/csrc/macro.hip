@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
         if (ok && !is_q) s_regs[rd][tid] = out;
         if (tr_on && ok && n_tr < p.trace_cap)
             p.trace[(uint64_t)n_tr * n_lanes + lane] =
-                make_uint4(D + 3u, is_q ? TRACE_QCLK_LOAD : rd, is_q ? out + 3u : out, 0u);
+                make_uint4(D + 3u, is_q ? TRACE_QCLK_LOAD : (uint32_t)(p.reg_inv >> (4 * rd)) & 15u, is_q ? out + 3u : out, 0u);
         n_tr += ok ? 1u : 0u;
         const bool load = ok && is_q;
         qa_t = load ? D + 3u : qa_t;
@@ -290,16 +290,382 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
     }
     if (valid && p.regs_out) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) p.regs_out[(uint64_t)r * n_lanes + lane] = s_regs[r][tid];
+        for (int r = 0; r < 16; r++)
+            p.regs_out[(uint64_t)r * n_lanes + lane] = ((p.reg_used >> r) & 1u) ? s_regs[(p.reg_map >> (4 * r)) & 15u][tid] : 0u;
     }
     count_outcome_block(p, s_hist, s_key, valid, core, sl, valid ? shot_group(p, sl) : 0u, last_bit);
 }
 
-hipError_t launch_macro(const KParams &p, hipStream_t stream)
+// ---------------------------------------------------------------------------
+// macro_staged_kernel<NR>: the same macro loop with the program memory STAGED
+// IN LDS per wave (the cmd_mem analogue, sim_modules/toplevel_sim.sv:5) and
+// the register file in VGPRs.
+//
+// A wave's 64 lanes run at most MACRO_SLOTS distinct programs (config 4:
+// 64 consecutive shots of one core, 10 shots per RB sequence -> <= 8; the
+// host checks the bound for the run's lane order and shots_per_group).  The
+// wave assigns each distinct program a slot, and streams the programs'
+// macros through a per-wave LDS chunk of MACRO_SLOTS x MACRO_CHUNK macros
+// (2 KiB): every lane loads two 16-B pieces of the NEXT chunk into VGPRs
+// while the wave executes the current chunk from LDS, and writes them to
+// LDS at the chunk boundary.  A lane's macro fetch is then an LDS read, and
+// the global loads -- which on gfx950 share vmcnt with the event stores, so
+// the wait for a load also waits for every earlier store -- are waited for
+// once per MACRO_CHUNK iterations instead of every iteration (macro_kernel
+// fetches one macro ahead per lane).
+//
+// NR: register slots the macro image names (capi.cpp remaps the reg_file
+// indices of the macro image to slots; RB programs name 2): NR = 2 keeps
+// them in VGPRs (a select instead of an LDS round trip per access), NR = 16
+// the [16][lane] LDS file.  Semantics, outputs and layout are
+// macro_kernel's (hdl/alu.v, ctrl.v latencies; oracle/fast_model.c).
+//
+// The lane state is one struct with inlined member functions rather than
+// nested lambdas: lambdas that call lambdas that capture by reference left
+// their closures (and a copy of the kernel arguments) in scratch memory
+// here -- 848 B per lane, every access a scratch round trip under vmcnt.
+
+template <int NR>
+struct MacroLane {
+    const KParams &p;
+    uint32_t *s_regs_lane;                 // NR == 16: &s_regs[0][tid], stride BLOCK
+    uint32_t lane, sl, core;
+    uint32_t rg[NR == 16 ? 1 : NR];
+    uint32_t t, pe, pp, pa, qa_t, qa_q;
+    uint32_t flags, n_ev, n_meas, meas_bits, last_bit, n_tr, k, st;
+    uint4 *evp;                            // event slot n_ev of this lane
+    bool tr_on, ev_on;
+    static constexpr uint32_t ST_TOP = 0x100u;
+
+    __device__ __forceinline__ MacroLane(const KParams &p_, uint32_t *srl, uint32_t lane_, uint32_t sl_,
+                                         uint32_t core_, bool valid)
+        : p(p_), s_regs_lane(srl), lane(lane_), sl(sl_), core(core_)
+    {
+#pragma unroll
+        for (int r = 0; r < (NR == 16 ? 1 : NR); r++) rg[r] = 0;
+        t = pe = pp = pa = 0;
+        qa_t = 1; qa_q = 0;
+        flags = n_ev = n_meas = meas_bits = last_bit = n_tr = k = 0;
+        st = valid ? 0u : ST_DONE;
+        evp = p.events + lane;
+        tr_on = p.trace != nullptr && p.trace_cap != 0u;
+        ev_on = p.events != nullptr;
+    }
+
+    __device__ __forceinline__ uint32_t reg_rd(uint32_t i) const
+    {
+        if constexpr (NR == 16) {
+            return s_regs_lane[(i & 15u) * BLOCK];
+        } else {
+            uint32_t v = rg[0];
+#pragma unroll
+            for (int r = 1; r < NR; r++) v = (i == (uint32_t)r) ? rg[r] : v;
+            return v;
+        }
+    }
+    __device__ __forceinline__ void reg_wr(bool ok, uint32_t i, uint32_t v)
+    {
+        if constexpr (NR == 16) {
+            if (ok) s_regs_lane[(i & 15u) * BLOCK] = v;
+        } else {
+#pragma unroll
+            for (int r = 0; r < NR; r++) rg[r] = (ok && i == (uint32_t)r) ? v : rg[r];
+        }
+    }
+    // qclk at cycle x: 0 in the reset hold, qa_q + x - qa_t after it
+    __device__ __forceinline__ uint32_t qclk_at(uint32_t x) const { return x < qa_t ? 0u : qa_q + (x - qa_t); }
+
+    // one pulse_iface strobe at te (kind 0 trigger, 1 phase reset); readout
+    // triggers draw the outcome
+    __device__ __forceinline__ void emit1(bool ok, uint32_t te, uint32_t kind)
+    {
+        if (ok) {
+            if (n_ev < p.event_cap && ev_on) *evp = event_record(te, pe, pp, pa, kind);
+            evp += p.n_lanes;
+            n_ev++;
+            if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {        // meas_elem 0xFF: none
+                const uint32_t bit = meas_bit(p, p.shot_begin + sl, core, n_meas, p.p1_thr[core], pa, pe);
+                if (p.meas && n_meas < p.meas_cap)
+                    p.meas[(uint64_t)n_meas * p.n_lanes + lane] = make_uint2(te + p.meas_latency, bit);
+                meas_bits |= (n_meas < 32u ? bit : 0u) << (n_meas & 31u);
+                last_bit = bit;
+                n_meas++;
+            }
+        }
+    }
+    // register-sourced pulse fields (decode_cmd cleared them)
+    __device__ __forceinline__ void pulse_regs(const uint4 u)
+    {
+        if (u.w & UOP_ANY_RS) {
+            const uint32_t reg0 = reg_rd((u.w >> 20) & 15u);
+            pe |= (u.w & UOP_RS_ENV) ? (reg0 & 0xFFFFFFu) : 0u;
+            pp |= (u.w & UOP_RS_PH) ? (reg0 & 0x1FFFFu) : 0u;
+            pp |= (u.w & UOP_RS_FR) ? ((reg0 & 0x1FFu) << 17) : 0u;
+            pa = (u.w & UOP_RS_AMP) ? (reg0 & 0xFFFFu) : pa;
+        }
+    }
+    // ALU slot {imm, ctl}: reg_alu reg[rd] = alu(in0, reg[rs1]) next decode
+    // D + 4; inc_qclk qclk = alu(in0, qclk(D)) + 3 at D + 3 (qclk.v)
+    __device__ __forceinline__ void alu_common(bool ok, uint32_t D, uint32_t ctl, uint32_t out)
+    {
+        const bool is_q = (ctl >> 30) & 1u;
+        const uint32_t rd = (ctl >> 8) & 15u;
+        reg_wr(ok && !is_q, rd, out);
+        if (tr_on && ok && n_tr < p.trace_cap)
+            p.trace[(uint64_t)n_tr * p.n_lanes + lane] =
+                make_uint4(D + 3u, is_q ? TRACE_QCLK_LOAD : (uint32_t)(p.reg_inv >> (4 * rd)) & 15u,
+                           is_q ? out + 3u : out, 0u);
+        n_tr += ok ? 1u : 0u;
+        const bool load = ok && is_q;
+        qa_t = load ? D + 3u : qa_t;
+        qa_q = load ? out + 3u : qa_q;
+        t = ok ? D + 4u : t;
+        k += ok ? 1u : 0u;
+    }
+    __device__ __forceinline__ void alu_general(uint32_t imm, uint32_t ctl)
+    {
+        const bool live = st == 0u && (int32_t)ctl < 0;
+        const uint32_t D = t;
+        const bool top = D > p.max_cycles;
+        st = (live && top) ? (ST_MAX_CYCLES | ST_TOP) : st;
+        const uint32_t reg0 = reg_rd((ctl >> 12) & 15u);
+        const uint32_t reg1 = reg_rd((ctl >> 4) & 15u);
+        const uint32_t in0 = (ctl & 8u) ? reg0 : imm;
+        const uint32_t out = alu_macro(ctl & 7u, in0, ((ctl >> 30) & 1u) ? qclk_at(D) : reg1);
+        alu_common(live && !top, D, ctl, out);
+    }
+    // the wave's ALU slot: skipped when no running lane has it; a scalar
+    // switch when every running lane that has it holds a reg_alu with the
+    // same op and none is past max_cycles; else the general path
+    __device__ __forceinline__ void alu_step(uint32_t imm, uint32_t ctl)
+    {
+        const bool pres = st == 0u && (int32_t)ctl < 0;
+        const uint64_t pm = __ballot(pres);
+        if (!pm) return;
+        const uint32_t key = ctl & 0x40000007u;
+        const uint32_t key_u = __builtin_amdgcn_readlane(key, (int)__builtin_ctzll(pm));
+        if (key_u & 0x40000000u || __ballot(pres && (key != key_u || t > p.max_cycles))) {
+            alu_general(imm, ctl);
+            return;
+        }
+        const uint32_t D = t;
+        const uint32_t in0 = (ctl & 8u) ? reg_rd((ctl >> 12) & 15u) : imm;
+        const uint32_t b = reg_rd((ctl >> 4) & 15u);
+        uint32_t out;
+        switch (key_u) {                                     // alu.v:20-50
+        case 0: out = in0; break;
+        case 1: out = in0 + b; break;
+        case 2: out = in0 - b; break;
+        case 3: out = (uint32_t)(in0 == b); break;
+        case 4: out = (uint32_t)((int32_t)in0 < (int32_t)b); break;
+        case 5: out = (uint32_t)((int32_t)in0 >= (int32_t)b); break;
+        case 6: out = b; break;
+        default: out = 0u; break;
+        }
+        alu_common(pres, D, ctl, out);
+    }
+    // pulse slot (a decode_cmd word, w bit 31 = absent): any command, the
+    // first included (reset hold: qclk(0) = qclk(1) = 0, proc.sv:125-136;
+    // cmd_time 0 there strobes twice)
+    __device__ __forceinline__ void pulse_general(const uint4 u)
+    {
+        const bool live = st == 0u && (int32_t)u.w >= 0;
+        const uint32_t D = t;
+        const uint32_t op4 = u.y >> 28;
+        const bool waits = (0x1200u >> op4) & 1u;
+        const bool pulse_cls = (0x1B00u >> op4) & 1u;
+        const bool strobe = (0x0A00u >> op4) & 1u;
+        const uint32_t T = u.x;
+        uint32_t wait = T - qclk_at(D);
+        bool big = false, dbl = false;
+        if (D < qa_t) {
+            dbl = T == 0u;
+            const uint64_t w64 = dbl ? 0ull : (uint64_t)(qa_t - D) + (uint32_t)(T - qa_q);
+            wait = (uint32_t)w64;
+            big = (w64 >> 32) != 0ull;
+        }
+        const uint32_t max_cycles = p.max_cycles;
+        const bool top = D > max_cycles;
+        const bool over = waits && (big || wait > max_cycles - D);
+        flags |= (live && !top && waits && (big || wait >= 0x80000000u)) ? F_LATE : 0u;
+        const uint32_t fin = top ? (ST_MAX_CYCLES | ST_TOP) : over ? ST_MAX_CYCLES
+                           : pulse_cls ? 0u : (op4 >= 0xDu ? ST_HUNG_OPCODE : ST_DONE);
+        st = live ? fin : st;
+        const bool ok = live && fin == 0u;
+        const uint32_t tT = D + (waits ? wait : 0u);
+        pulse_write(u, pe, pp, pa);
+        pulse_regs(u);
+        const bool rst = op4 == 0xBu;
+        const bool two = ok && dbl && op4 == 0x9u;
+        flags |= two ? F_DOUBLE_STROBE : 0u;
+        emit1(ok && strobe, rst ? D : tT + 2u, rst ? 1u : 0u);
+        emit1(two, tT + 3u, 0u);
+        t = ok ? tT + 3u : t;
+        k += (live && !top) ? 1u : 0u;
+    }
+    // the wave's pulse slot: the trigger path (the RB shape) when every
+    // running lane that has the slot holds a PULSE_WRITE_TRIG past the reset
+    // hold and within max_cycles; else the general path
+    __device__ __forceinline__ void pulse_step(const uint4 u)
+    {
+        const bool pres = st == 0u && (int32_t)u.w >= 0;
+        if (__ballot(pres && ((u.y >> 28) != 0x9u || t > p.max_cycles || t < qa_t))) {
+            pulse_general(u);
+            return;
+        }
+        const uint32_t D = t;
+        const uint32_t wait = u.x - (qa_q + (D - qa_t));
+        const bool stop = pres && wait > p.max_cycles - D;   // includes every late cmd_time (wait >= 2^31)
+        flags |= (stop && wait >= 0x80000000u) ? F_LATE : 0u;
+        st = stop ? ST_MAX_CYCLES : st;
+        const bool ok = pres && !stop;
+        const uint32_t tT = D + wait;
+        pulse_write(u, pe, pp, pa);
+        pulse_regs(u);
+        emit1(ok, tT + 2u, 0u);
+        t = ok ? tT + 3u : t;
+        k += pres ? 1u : 0u;
+    }
+};
+
+template <int NR>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR == 16 ? 4 : 6))) macro_staged_kernel(const KParams p)
+{
+    constexpr uint32_t NW = BLOCK / 64, CH = MACRO_CHUNK, NS = MACRO_SLOTS;
+    constexpr uint32_t PIECES = NS * CH * 2;          // 16-B pieces of a chunk (2 per lane)
+    static_assert(PIECES == 128, "two pieces per lane");
+    __shared__ uint4 s_chunk0[NW][PIECES];            // [wave][slot][macro][2], double-buffered
+    __shared__ uint4 s_chunk1[NW][PIECES];
+    __shared__ uint32_t s_smb[NW][NS], s_sml[NW][NS]; // slot -> first / terminal macro
+    __shared__ uint32_t s_regs[NR == 16 ? 16 : 1][NR == 16 ? BLOCK : 1];
+    __shared__ uint32_t s_hist[HIST_LDS_MAX];
+    __shared__ uint32_t s_key[BLOCK];
+    const uint32_t tid = threadIdx.x, wv = tid >> 6, wl = tid & 63;
+    const uint32_t C = p.C;
+    uint32_t sl, core;
+    clear_hist_next(p);
+    block_core_major(p, sl, core);
+    const bool valid = sl < p.n_shots;
+    const uint32_t lane = out_lane(p, sl, core);
+
+    uint32_t prog = 0, mb = 0, ml = 0;
+    if (valid) {
+        const uint32_t grp = shot_group(p, sl);
+        prog = p.prog_table[(uint64_t)grp * C + core];
+        mb = p.macro_off[prog];
+        ml = p.macro_off[prog + 1] - 1u;
+    }
+    if (p.hist_lds) {
+        for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
+        __syncthreads();
+    }
+    if constexpr (NR == 16) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
+    }
+    MacroLane<NR> L(p, NR == 16 ? &s_regs[0][tid] : nullptr, lane, sl, core, valid);
+
+    // ---- the wave's distinct programs -> slots (a uniform waterfall) ----
+    uint32_t slot = 0, nslots = 0;
+    {
+        uint64_t rem = __ballot(valid);
+        while (rem) {
+            const int ld = (int)__builtin_ctzll(rem);
+            const uint32_t lp = __builtin_amdgcn_readlane(prog, ld);
+            const bool mine = valid && prog == lp;
+            if (mine) slot = nslots;
+            if (wl == 0 && nslots < NS) {
+                s_smb[wv][nslots] = __builtin_amdgcn_readlane(mb, ld);
+                s_sml[wv][nslots] = __builtin_amdgcn_readlane(ml, ld);
+            }
+            rem &= ~__ballot(mine);
+            nslots++;
+        }
+    }
+    // more programs than slots: the host's bound was wrong (internal error):
+    // those lanes share slot NS - 1's macros, their outputs are flagged
+    L.flags |= slot >= NS ? F_GUARD : 0u;
+    slot = min(slot, NS - 1u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // chunk c of every slot (macros [c CH, (c + 1) CH), the terminal macro
+    // repeating) goes global -> LDS directly (global_load_lds_dwordx4: no
+    // VGPRs hold it in flight), into the buffer the wave is NOT reading; lane
+    // wl of load instruction r fetches piece e = r * 64 + wl = slot e / 16,
+    // macro (e / 2) % 8, half e % 2 (the LDS image is lane-linear)
+    const uint32_t s0 = wl >> 4, s1 = 4u + (wl >> 4), pj = (wl >> 1) & 7u, ph = wl & 1u;
+    const uint4 *const mbase = p.macros;
+    // Only the lanes of the wave's nslots slots load (s_smb / s_sml of the
+    // others were never written -- all of them in a wave with no valid lane);
+    // the other pieces of the LDS image are never read.
+    const bool on0 = s0 < nslots, on1 = s1 < nslots;
+    auto stage = [&](uint32_t c, uint4 *buf) __attribute__((always_inline)) {
+        const uint32_t m = c * CH + pj;
+        if (on0) {
+            const uint32_t mb0 = s_smb[wv][s0], ml0 = s_sml[wv][s0];
+            __builtin_amdgcn_global_load_lds(mbase + 2ull * min(mb0 + m, ml0) + ph, buf, 16, 0, 0);
+        }
+        if (on1) {
+            const uint32_t mb1 = s_smb[wv][s1], ml1 = s_sml[wv][s1];
+            __builtin_amdgcn_global_load_lds(mbase + 2ull * min(mb1 + m, ml1) + ph, buf + 64, 16, 0, 0);
+        }
+    };
+    const uint32_t moff = slot * (CH * 2);
+    // the chunk loop, two phases per round so every LDS read names one
+    // buffer statically (the compiler then needs no vmcnt wait for the DMA
+    // into the other): phase A executes chunk c from s_chunk0 while chunk
+    // c + 1 streams into s_chunk1, phase B the reverse.  A phase always runs
+    // its CH macros (finished lanes are frozen); the DMA of the next chunk
+    // is waited for (vmcnt(0)) once per phase
+    auto phase = [&](const uint4 *buf) __attribute__((always_inline)) {
+        const uint4 *const cur = buf + moff;
+#pragma unroll 1
+        for (uint32_t i = 0; i < CH; i++) {
+            const uint4 a = cur[2 * i], u = cur[2 * i + 1];
+            L.alu_step(a.x, a.y);
+            L.alu_step(a.z, a.w);
+            L.pulse_step(u);
+        }
+    };
+    stage(0u, s_chunk0[wv]);
+    for (uint32_t c = 0; __ballot(L.st == 0u); c += 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        stage(c + 1u, s_chunk1[wv]);
+        phase(s_chunk0[wv]);
+        if (!__ballot(L.st == 0u)) break;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        stage(c + 2u, s_chunk0[wv]);
+        phase(s_chunk1[wv]);
+    }
+    // no LDS DMA may still be in flight when the workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    L.flags |= (L.n_ev > p.event_cap ? F_EVENT_OVF : 0u) | (L.n_meas > min(p.meas_cap, MEAS_LOOKUP) ? F_MEAS_OVF : 0u) |
+               (p.trace_cap && L.n_tr > p.trace_cap ? F_TRACE_OVF : 0u);
+
+    if (valid && p.summary) {
+        const uint32_t ip = (L.st & MacroLane<NR>::ST_TOP) ? L.k : L.k - 1u;
+        write_summary(p, lane, L.t, ip, L.st & 0xFFu, L.flags, L.n_ev, L.k, L.qclk_at(L.t), L.n_meas, L.meas_bits,
+                      L.n_tr);
+    }
+    if (valid && p.regs_out) {
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            p.regs_out[(uint64_t)r * p.n_lanes + lane] =
+                ((p.reg_used >> r) & 1u) ? L.reg_rd((uint32_t)(p.reg_map >> (4 * r)) & 15u) : 0u;
+    }
+    count_outcome_block(p, s_hist, s_key, valid, core, sl, valid ? shot_group(p, sl) : 0u, L.last_bit);
+}
+
+hipError_t launch_macro(const KParams &p, bool staged, int nr, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(macro_kernel, dim3(blocks), dim3(BLOCK), 0, stream, p);
+    if (!staged) hipLaunchKernelGGL(macro_kernel, dim3(blocks), dim3(BLOCK), 0, stream, p);
+    else if (nr == 2) hipLaunchKernelGGL(macro_staged_kernel<2>, dim3(blocks), dim3(BLOCK), 0, stream, p);
+    else hipLaunchKernelGGL(macro_staged_kernel<16>, dim3(blocks), dim3(BLOCK), 0, stream, p);
     return hipGetLastError();
 }
 

@@ -83,6 +83,8 @@ extern "C" {
 #define DPEMU_X_HIST_REPL   0x8   /* outcome histogram: privatised replicas + reduce          */
 #define DPEMU_X_PROG_MAJOR  0x10  /* fetch from the program-major image, not the command-major copy */
 #define DPEMU_X_GENERAL     0x20  /* run every program on the general interpreter (interp_kernel) */
+#define DPEMU_X_MACRO_DIRECT 0x40 /* branch-free register programs: per-lane macro fetch (macro_kernel),
+                                     not the LDS-staged program chunks (macro_staged_kernel) */
 
 #define DPEMU_MAX_CORES 64
 #define DPEMU_MEAS_LOOKUP 16      /* a core's first 16 measurements are visible to fproc;

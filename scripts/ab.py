@@ -48,11 +48,13 @@ def main():
     ap.add_argument('--reps', type=int, default=4)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--no-compare', action='store_true', help='probe builds: outputs may differ')
+    ap.add_argument('--flags', default='', help='per-library exec_flags (comma list, e.g. 0,0x40)')
     a = ap.parse_args()
     import torch
     from distributed_processor_amd.emulator import Emulator, alloc_device_outputs
     libs = [os.path.abspath(x) for x in a.libs.split(',')]
     ps, cfg, n = workload(a.workload)
+    flags = [int(x, 0) for x in a.flags.split(',')] if a.flags else [cfg.exec_flags] * len(libs)
     emus = [Emulator(0, lib_path=l) for l in libs]
     for e in emus:
         e.load(ps)
@@ -64,6 +66,7 @@ def main():
         order = range(len(emus)) if rep % 2 == 0 else reversed(range(len(emus)))
         for i in order:
             e = emus[i]
+            cfg.exec_flags = flags[i]
             e.kernel_timing(True)
             for _ in range(a.steps):
                 out['hist'].zero_()
@@ -79,8 +82,9 @@ def main():
             elif not a.no_compare:
                 same &= all(torch.equal(ref[k], snap[k]) for k in ref)
     print(json.dumps({'workload': a.workload, 'same_outputs': bool(same), 'kernels': [e.last_kernel() for e in emus],
-                      'median_ms': {os.path.basename(l): float(np.median(t)) for l, t in zip(libs, times)},
-                      'min_ms': {os.path.basename(l): float(np.min(t)) for l, t in zip(libs, times)}}))
+                      'flags': flags,
+                      'median_ms': [float(np.median(t)) for t in times],
+                      'min_ms': [float(np.min(t)) for t in times], 'libs': [os.path.basename(l) for l in libs]}))
 
 
 if __name__ == '__main__':

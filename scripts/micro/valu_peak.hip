@@ -37,6 +37,60 @@ __global__ void __launch_bounds__(256) valu_kernel(uint32_t *out, uint32_t iters
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// the same shape with one instruction type (inline asm, so nothing folds):
+// v_add_u32 only (int), v_fma_f32 only (float)
+template <int CH, int W>
+__global__ void __launch_bounds__(256) add_kernel(uint32_t *out, uint32_t iters, uint32_t k)
+{
+    uint32_t a[CH];
+#pragma unroll
+    for (int c = 0; c < CH; c++) a[c] = threadIdx.x * (c + 1) + blockIdx.x;
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int u = 0; u < 12; u++) {
+#pragma unroll
+            for (int c = 0; c < CH; c++) asm volatile("v_add_u32 %0, %1, %0" : "+v"(a[c]) : "s"(k));
+        }
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < CH; c++) s ^= a[c];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+template <int CH, int W>
+__global__ void __launch_bounds__(256) fma_kernel(uint32_t *out, uint32_t iters, uint32_t k)
+{
+    float a[CH];
+    const float m = 1.0f + 1e-7f * (float)k, q = 1e-3f * (float)k;
+#pragma unroll
+    for (int c = 0; c < CH; c++) a[c] = (float)(threadIdx.x * (c + 1) + blockIdx.x);
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int u = 0; u < 12; u++) {
+#pragma unroll
+            for (int c = 0; c < CH; c++) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[c]) : "s"(m), "s"(q));
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; c++) s += a[c];
+    out[blockIdx.x * 256 + threadIdx.x] = __float_as_uint(s);
+}
+
+template <int CH, int W>
+static void run_other(uint32_t iters, uint32_t *d)
+{
+    const uint32_t blocks = 256u * W, it = iters / CH;
+    hipLaunchKernelGGL((add_kernel<CH, W>), dim3(blocks), dim3(256), 0, 0, d, it, 7u);
+    hipLaunchKernelGGL((fma_kernel<CH, W>), dim3(blocks), dim3(256), 0, 0, d, it, 7u);
+    for (int r = 0; r < 3; r++) {
+        hipLaunchKernelGGL((add_kernel<CH, W>), dim3(blocks), dim3(256), 0, 0, d, it, 7u);
+        hipLaunchKernelGGL((fma_kernel<CH, W>), dim3(blocks), dim3(256), 0, 0, d, it, 7u);
+    }
+    CHECK(hipDeviceSynchronize());
+}
+
 template <int CH, int W>
 static void run(uint32_t iters, uint32_t *d, int reps)
 {
@@ -82,6 +136,9 @@ int main(int argc, char **argv)
     run_w<2>(iters, d, 5);
     run_w<4>(iters, d, 5);
     run_w<8>(iters, d, 5);
+    run_other<1, 8>(iters, d);
+    run_other<4, 8>(iters, d);
+    run_other<8, 8>(iters, d);
     CHECK(hipFree(d));
     return 0;
 }

@@ -12,10 +12,16 @@ writes <dest>/<tag>_<kernel>_pmc.json with per-launch means:
 * fetch_bytes     FETCH_SIZE x 1024 x 2: on gfx950 FETCH_SIZE reads 1/2 of a
                   wide coalesced read (MI355X_MICROARCH.md, HBM section)
 * hbm_bytes_per_launch = write_bytes + fetch_bytes
-* SQ_* / GRBM_* raw means; VALU busy = SQ_ACTIVE_INST_VALU * 4 / (4 SIMD x 256 CU)
-  / (GRBM_GUI_ACTIVE / 8 XCDs); VALU issue share = SQ_INSTS_VALU x 4 cycles on
-  the same denominator; lane utilisation = SQ_THREAD_CYCLES_VALU /
-  (SQ_ACTIVE_INST_VALU x 64)
+* SQ_* / GRBM_* raw means
+* VALU ratios, each from counters of the SAME pass and dispatch (prof_cmd.sh
+  puts GRBM_GUI_ACTIVE in both SQ passes), then averaged over dispatches:
+    valu_issue_pct   SQ_INSTS_VALU x c / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs),
+                     c = the measured cycles per wave64 integer-VALU
+                     instruction at the issue peak (profiles/r03_valu_peak_pmc.json)
+    valu_busy_pct    SQ_ACTIVE_INST_VALU x 4 (quad-cycles) on the same denominator
+    valu_frac_of_measured_peak  SQ_INSTS_VALU / duration / the measured peak
+  A ratio above 100 % is reported as measured and flagged in 'warnings'.
+* valu_lane_util_pct = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)
 """
 import collections
 import csv
@@ -27,14 +33,24 @@ import sys
 # summary key -> kernel-name substrings, one per bench leg: config 2 runs on
 # straight_kernel (pulse-only programs), config 3 on branch_kernel (fproc
 # branches, syncs), config 4 on macro_kernel, config 5 on dds_tile_kernel
-KERNELS = {'ramsey': ('straight_kernel',), 'active_reset': ('branch_kernel',), 'rb': ('macro_kernel',),
-           'dds': ('dds_tile_kernel',), 'dds_index': ('dds_index_kernel',), 'hist_reduce': ('hist_reduce_kernel',)}
+KERNELS = {'ramsey': ('straight_kernel',), 'active_reset': ('branch_kernel',), 'rb': ('macro_kernel', 'macro_staged_kernel'),
+           'dds': ('dds_tile_kernel',), 'dds_index': ('dds_index_kernel',), 'hist_reduce': ('hist_reduce_kernel',),
+           'config1': ('straight_kernel',)}
+# legs that share a kernel: the leg's launch grid (threads) picks its dispatches
+# (config 1: 10^6 single-core lanes; config 2: 10^6 shots x 8 cores)
+GRIDS = {'config1': (10 ** 6 + 255) // 256 * 256, 'ramsey': 8 * 10 ** 6}
 
 
-# wave64 integer-VALU instructions per second, whole chip: the best rate of
-# scripts/micro/valu_peak.hip (independent add/shift/xor chains, 2-8 waves per
-# SIMD) measured on MI355X (profiles/r01_valu_peak.jsonl)
-VALU_PEAK_WAVE_INSTS = 7.7e11
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def valu_peak():
+    """the measured wave64 integer-VALU issue peak (instructions/s, whole chip)
+    and its cycles per instruction per SIMD: scripts/micro/valu_peak.hip under
+    rocprofv3, summarised by scripts/valu_peak_summary.py"""
+    with open(os.path.join(REPO, 'profiles', 'r03_valu_peak_pmc.json')) as f:
+        v = json.load(f)
+    return v['peak_valu_insts_per_s'], v['peak_cycles_per_inst']
 
 
 def rows(pattern):
@@ -45,9 +61,9 @@ def rows(pattern):
     return out
 
 
-def which(name):
+def which(name, grid):
     for k, subs in KERNELS.items():
-        if any(sub in name for sub in subs):
+        if any(sub in name for sub in subs) and GRIDS.get(k, grid) == grid:
             return k
     return None
 
@@ -57,6 +73,7 @@ def main():
     dest = sys.argv[3] if len(sys.argv) > 3 else root
     if len(sys.argv) > 4:          # kernel keys of this run: key=substr|substr,...
         KERNELS.clear()
+        GRIDS.clear()
         for item in sys.argv[4].split(','):
             k, subs = item.split('=')
             KERNELS[k] = tuple(subs.split('|'))
@@ -66,33 +83,52 @@ def main():
     names = {}
     tdir = 'prof_trace' if os.path.isdir(os.path.join(root, 'prof_trace')) else 'trace'
     for r in rows(os.path.join(root, tdir, '**', '*kernel_trace.csv')):
-        k = which(r['Kernel_Name'])
+        grid = int(r['Grid_Size']) if r.get('Grid_Size') else \
+            int(r['Grid_Size_X']) * int(r.get('Grid_Size_Y') or 1) * int(r.get('Grid_Size_Z') or 1)
+        k = which(r['Kernel_Name'], grid)
         if k:
-            grid = int(r['Grid_Size']) if r.get('Grid_Size') else \
-                int(r['Grid_Size_X']) * int(r.get('Grid_Size_Y') or 1) * int(r.get('Grid_Size_Z') or 1)
             dur[(k, grid)].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
             names[(k, grid)] = r['Kernel_Name']
     shape = {}
     for (k, grid), v in dur.items():
         if k not in shape or len(v) > len(dur[(k, shape[k])]):
             shape[k] = grid
-    # counters: per (kernel, grid, dispatch, counter) sums
-    ctr = collections.defaultdict(lambda: collections.defaultdict(float))
+    peak, cpi = valu_peak()
+    # counters: per (kernel, grid) -> {(pass dir, dispatch): {counter: sum}}
+    ctr = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for d in sorted(glob.glob(os.path.join(root, '*'))):
         if not os.path.isdir(d) or os.path.basename(d) == tdir:
             continue
         for r in rows(os.path.join(d, '**', '*counter_collection.csv')):
-            k = which(r['Kernel_Name'])
+            grid = int(r.get('Grid_Size') or 0)
+            k = which(r['Kernel_Name'], grid)
             if not k:
                 continue
-            grid = int(r.get('Grid_Size') or 0)
-            ctr[(k, grid, r['Counter_Name'])][(d, r['Dispatch_Id'])] += float(r['Counter_Value'])
+            ctr[(k, grid)][(d, r['Dispatch_Id'])][r['Counter_Name']] += float(r['Counter_Value'])
     for k, grid in shape.items():
         res = {'kernel': names[(k, grid)], 'grid_size': grid, 'dispatches_traced': len(dur[(k, grid)]),
                'duration_ns': sum(dur[(k, grid)]) / len(dur[(k, grid)])}
-        for (kk, g, name), per in ctr.items():
-            if kk == k and g == grid:
-                res[name] = sum(per.values()) / len(per)
+        disp = ctr.get((k, grid), {})
+        names_c = sorted({c for v in disp.values() for c in v})
+        for name in names_c:
+            vals = [v[name] for v in disp.values() if name in v]
+            res[name] = sum(vals) / len(vals)
+        # same-pass, same-dispatch VALU ratios
+        def ratio(num, scale):
+            xs = [v[num] * scale / 1024.0 / (v['GRBM_GUI_ACTIVE'] / 8.0) * 100.0 for v in disp.values()
+                  if num in v and v.get('GRBM_GUI_ACTIVE')]
+            return sum(xs) / len(xs) if xs else None
+        res['valu_peak_insts_per_s'] = peak
+        res['valu_peak_cycles_per_inst'] = cpi
+        warnings = []
+        for key, num, scale in (('valu_issue_pct', 'SQ_INSTS_VALU', cpi), ('valu_busy_pct', 'SQ_ACTIVE_INST_VALU', 4.0)):
+            r_ = ratio(num, scale)
+            if r_ is not None:
+                res[key] = r_
+                if r_ > 100.0:
+                    warnings.append('{} = {:.1f} % exceeds 100 %: the counter basis does not hold here'.format(key, r_))
+        if warnings:
+            res['warnings'] = warnings
         if 'WRITE_SIZE' in res:
             res['write_bytes'] = res['WRITE_SIZE'] * 1024
         if 'FETCH_SIZE' in res:
@@ -100,19 +136,13 @@ def main():
         if 'write_bytes' in res and 'fetch_bytes' in res:
             res['hbm_bytes_per_launch'] = res['write_bytes'] + res['fetch_bytes']
             res['hbm_GBps_at_traced_duration'] = res['hbm_bytes_per_launch'] / res['duration_ns']
-        if 'SQ_ACTIVE_INST_VALU' in res and 'GRBM_GUI_ACTIVE' in res and res['GRBM_GUI_ACTIVE']:
-            # GRBM_GUI_ACTIVE is summed over the 8 XCDs; SQ_ACTIVE_INST_VALU counts quad-cycles
-            res['valu_busy_pct'] = 100.0 * res['SQ_ACTIVE_INST_VALU'] * 4 / (4 * 256) / (res['GRBM_GUI_ACTIVE'] / 8)
-        if 'SQ_INSTS_VALU' in res and 'GRBM_GUI_ACTIVE' in res and res['GRBM_GUI_ACTIVE']:
-            # a wave64 VALU instruction holds a 16-lane SIMD for 4 cycles: issue-limited share
-            res['valu_issue_pct'] = 100.0 * res['SQ_INSTS_VALU'] * 4 / (4 * 256) / (res['GRBM_GUI_ACTIVE'] / 8)
         if 'SQ_THREAD_CYCLES_VALU' in res and 'SQ_ACTIVE_INST_VALU' in res and res['SQ_ACTIVE_INST_VALU']:
             # active lanes per VALU instruction (divergence): thread-cycles / (quad-cycles * 64)
             res['valu_lane_util_pct'] = 100.0 * res['SQ_THREAD_CYCLES_VALU'] / (res['SQ_ACTIVE_INST_VALU'] * 64)
         if 'SQ_INSTS_VALU' in res and res.get('duration_ns'):
             # against the measured integer-VALU issue peak (scripts/micro/valu_peak.hip)
             res['valu_insts_per_s'] = res['SQ_INSTS_VALU'] / (res['duration_ns'] * 1e-9)
-            res['valu_frac_of_measured_peak'] = res['valu_insts_per_s'] / VALU_PEAK_WAVE_INSTS
+            res['valu_frac_of_measured_peak'] = res['valu_insts_per_s'] / peak
         if 'SQ_INSTS_VALU' in res and 'SQ_WAVES' in res and res['SQ_WAVES']:
             res['valu_insts_per_wave'] = res['SQ_INSTS_VALU'] / res['SQ_WAVES']
         path = os.path.join(dest, '{}_{}_pmc.json'.format(tag, k))

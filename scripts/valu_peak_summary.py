@@ -36,8 +36,8 @@ def rows(pattern):
 
 
 def variant(name):
-    m = re.search(r'valu_kernel<(\d+), (\d+)>', name)
-    return (int(m.group(1)), int(m.group(2))) if m else None
+    m = re.search(r'(valu|add|fma)_kernel<(\d+), (\d+)>', name)
+    return (m.group(1), int(m.group(2)), int(m.group(3))) if m else None
 
 
 def main():
@@ -62,7 +62,9 @@ def main():
         # per-dispatch ratios from the same pass, then averaged
         cpi = [SIMDS * (c['GRBM_GUI_ACTIVE'] / XCDS) / c['SQ_INSTS_VALU'] for c in disp
                if c.get('SQ_INSTS_VALU') and c.get('GRBM_GUI_ACTIVE')]
-        rec = {'kernel': 'valu_kernel<{}, {}>'.format(*v), 'chains': v[0], 'waves_per_simd': v[1],
+        rec = {'kernel': '{}_kernel<{}, {}>'.format(*v), 'mix': {'valu': 'add/shift/xor (int)', 'add': 'v_add_u32 only',
+                                                                  'fma': 'v_fma_f32 only'}[v[0]],
+               'chains': v[1], 'waves_per_simd': v[2],
                'dispatches_traced': len(dur[v]), 'dispatches_counted': len(disp), 'duration_ns': d_ns,
                'counters': mean,
                'valu_insts_per_s': mean['SQ_INSTS_VALU'] / (d_ns * 1e-9),
@@ -70,11 +72,13 @@ def main():
                'clock_ghz': mean['GRBM_GUI_ACTIVE'] / XCDS / d_ns,
                'cycles_per_inst': sum(cpi) / len(cpi) if cpi else None}
         res.append(rec)
-    best = max(res, key=lambda r: r['valu_insts_per_s'])
+    best = max((r for r in res if r['mix'] != 'v_fma_f32 only'), key=lambda r: r['valu_insts_per_s'])
     out = {'what': 'wave64 integer-VALU issue peak of MI355X, measured: scripts/micro/valu_peak.hip under '
                    'rocprofv3 (kernel trace + one PMC pass: SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU '
                    'SQ_BUSY_CYCLES GRBM_GUI_ACTIVE); summarised by scripts/valu_peak_summary.py',
            'peak_valu_insts_per_s': best['valu_insts_per_s'], 'peak_variant': best['kernel'],
+           'peak_note': 'best integer variant (the interpreter kernels are integer code); the fma variants '
+                        'are reported beside it for the float issue rate',
            'peak_cycles_per_inst': best['cycles_per_inst'], 'peak_clock_ghz': best['clock_ghz'],
            'guide_issue_model': '2 cycles per wave64 VALU instruction per SIMD (MI355X_MICROARCH.md:54): '
                                 '1024 SIMDs x 2.4 GHz / 2 = 1.229e12 /s',

@@ -34,7 +34,8 @@ def raw(op4, in0_reg=0, alu_op=0, imm=0, rs0=0, rs1=0, rd=0, target=0, fproc_id=
 
 class Gen:
     def __init__(self, rng, ncores, mode='meas', allow_late=False, allow_hang=False, meas_latency=20,
-                 straight=False, linear=False):
+                 straight=False, linear=False, regs=None):
+        self.regs = list(regs) if regs else list(range(16))   # register indices the ALU / pulse fields name
         self.straight = straight          # pulse / idle / pulse_reset / done only
         self.linear = linear              # plus reg_alu / inc_qclk: no jump, fproc or sync
         self.shape = None                 # fixed opcode-kind sequence (shaped_case)
@@ -56,7 +57,7 @@ class Gen:
         if r.random() < 0.2:
             k = r.choice(['freq', 'phase', 'amp', 'env'])
             f.pop(k + '_word', None)
-            f[k + '_regaddr'] = r.randint(0, 15)
+            f[k + '_regaddr'] = r.choice(self.regs)
         if r.random() < 0.1:
             f.pop('cfg_word', None)
         return f
@@ -92,11 +93,12 @@ class Gen:
                 q += 3
             elif kind == 'alu':
                 op = r.randrange(8)
+                rd = r.randint(0, 7) if len(self.regs) == 16 else r.choice(self.regs)
                 if r.random() < 0.5:
                     words.append(raw(1, 0, op, imm=r.choice([r.randint(-40, 40), r.getrandbits(32)]),
-                                     rs1=r.randint(0, 15), rd=r.randint(0, 7)))
+                                     rs1=r.choice(self.regs), rd=rd))
                 else:
-                    words.append(raw(1, 1, op, rs0=r.randint(0, 15), rs1=r.randint(0, 15), rd=r.randint(0, 7)))
+                    words.append(raw(1, 1, op, rs0=r.choice(self.regs), rs1=r.choice(self.regs), rd=rd))
                 q += 4
             elif kind == 'incq':
                 ops = [1, 1, 1, 0, 6, 7] + ([2] if self.allow_late else [])
@@ -193,13 +195,13 @@ def pack_programs(progs):
 
 
 def random_case(seed, ncores=None, mode=None, allow_late=True, allow_hang=True, n_groups=None, straight=False,
-                linear=False):
+                linear=False, regs=None):
     rng = random.Random(seed)
     ncores = ncores or rng.choice([1, 2, 4])
     mode = mode or rng.choice(['meas', 'meas', 'lut'])
     n_groups = n_groups or rng.choice([1, 2])
     n_sync = 0 if (straight or linear) else (rng.choice([0, 0, 1, 2]) if ncores > 1 else rng.choice([0, 1]))
-    g = Gen(rng, ncores, mode, allow_late, allow_hang, straight=straight, linear=linear)
+    g = Gen(rng, ncores, mode, allow_late, allow_hang, straight=straight, linear=linear, regs=regs)
     body = rng.randint(3, 14)
     progs = [g.program(n_sync, body) for _ in range(n_groups * ncores)]
     table = np.arange(n_groups * ncores, dtype=np.uint32)

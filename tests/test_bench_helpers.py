@@ -25,7 +25,7 @@ def test_hbm_roofline_caps_at_the_step_and_prefers_the_leg_profile(tmp_path, mon
     assert r['kernel_ms_rocprof'] == pytest.approx(0.2)
     assert r['frac_rocprof'] == pytest.approx(1e9 / 0.2e-3 / 1e9 / bench.HBM_PEAK_GBS)
     # no per-leg duration: the --stats row of the kernel
-    (tmp_path / 'r02_kernel_stats.csv').write_text('"Name","Calls","AverageNs"\n"void dpemu::my_kernel(x)",3,"150000"\n')
+    (tmp_path / (bench.PROFILE_TAG + '_kernel_stats.csv')).write_text('"Name","Calls","AverageNs"\n"void dpemu::my_kernel(x)",3,"150000"\n')
     monkeypatch.setattr(bench, 'PROFILE_DIR', str(tmp_path))
     r = bench.hbm_roofline(1e9, 0.2, 1.0, 'k', {'hbm_bytes_per_launch': None}, 'my_kernel')
     assert r['kernel_ms_rocprof'] == pytest.approx(0.15)
@@ -92,3 +92,16 @@ def test_committed_bench_agrees_with_its_same_box_rocprof(leg):
     roof = roof.get('hbm', roof)
     assert roof['kernel_ms'] <= x['ms_per_step'] + 1e-9
     assert roof['kernel_ms_rocprof'] == pytest.approx(roof['kernel_ms'], rel=0.05)
+
+
+def test_valu_view_recomputes_from_the_measured_peak():
+    """the interpreter legs' VALU fractions: SQ_INSTS_VALU over the kernel time
+    against the committed microbenchmark peak (profiles/r03_valu_peak_pmc.json)"""
+    peak, cpi, variant = bench._valu_peak()
+    assert 3e11 < peak < 1.3e12 and 2.0 <= cpi < 8.0 and 'kernel' in variant
+    prof = {'SQ_INSTS_VALU': 1e8, 'duration_ns': 250000.0, 'valu_issue_pct': 50.0}
+    v = bench.valu_view(prof, 0.2)
+    assert v['achieved'] == pytest.approx(1e8 / 0.2e-3)
+    assert v['frac'] == pytest.approx(1e8 / 0.2e-3 / peak)
+    assert v['frac_rocprof'] == pytest.approx(1e8 / 0.25e-3 / peak)
+    assert bench.valu_view({'duration_ns': 1.0}) is None

@@ -43,13 +43,14 @@ def compare_all(gpu, ref, ctx=''):
 def run_pair(emu, ps, cfg, n_shots, shot0=0):
     """GPU run and oracle; the execution variants (LDS-staged programs,
     histogram strategy, program-major fetch, the general interpreter for
-    branch-free programs) must produce the same bytes"""
+    branch-free programs, the per-lane macro fetch instead of the staged
+    macro chunks) must produce the same bytes"""
     emu.load(ps)
     g = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
     f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n_shots, want=ALL_OUT)
     base = cfg.exec_flags
     for flags in (_abi.X_PROG_LDS | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT | _abi.X_PROG_MAJOR,
-                  _abi.X_GENERAL | _abi.X_PROG_LDS):
+                  _abi.X_GENERAL | _abi.X_PROG_LDS, _abi.X_MACRO_DIRECT):
         cfg.exec_flags = flags
         g2 = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
         compare_all(g2.arrays, g.arrays, 'execution variant {:#x}'.format(flags))
@@ -128,6 +129,43 @@ def test_fuzz_linear_programs(emu, seed):
                            meas_cap=1 if tight else 16, meas_latency=1 + seed, seed=seed, meas_elem=seed % 4)
     g, f = run_pair(emu, ps, cfg, 900 + 41 * seed, shot0=seed * 13)
     compare_all(g, f, 'seed {}'.format(seed))
+
+
+@pytest.mark.parametrize('seed', range(12))
+def test_fuzz_linear_few_registers(emu, seed):
+    """branch-free register programs naming 1-4 registers (any indices): the
+    macro image renumbers up to 2 of them to VGPR slots (macro_staged_kernel<2>,
+    else the LDS file of macro_staged_kernel<16>);
+    many program groups with 5-16 shots each so a wave stages several
+    programs, traces on (register addresses map back), registers out;
+    against oracle_fast and every execution variant (macro_kernel included)"""
+    import random
+    rr = random.Random(seed)
+    C = [1, 2, 4][seed % 3]
+    regs = rr.sample(range(16), 1 + seed % 4)
+    case = random_case(17000 + seed, ncores=C, mode='meas', allow_late=seed % 2 == 1, allow_hang=True,
+                       n_groups=9 + seed, linear=True, regs=regs)
+    groups = [[case['progs'][case['table'][g * C + c]] for c in range(C)] for g in range(case['n_groups'])]
+    ps = ProgramSet(groups, cores_per_shot=C)
+    spg = [10, 16, 32, 5][seed % 4]
+    order = (seed // 4) % 2
+    cfg = _abi.make_config(C, n_groups=ps.n_groups, shots_per_group=spg, max_cycles=6000, event_cap=64,
+                           trace_cap=64, meas_cap=16, meas_latency=5, seed=seed, meas_elem=seed % 4,
+                           lane_order=order)
+    g, f = run_pair(emu, ps, cfg, 64 * 9 + 7 * seed, shot0=seed * 31)
+    compare_all(g, f, 'seed {} regs {}'.format(seed, regs))
+    # the kernel the run used: staged when a wave spans <= 8 distinct programs (capi.cpp)
+    shots_run = 64 // C if order else min(256 // C, 64)
+    cores_w = C if order else 64 // shots_run
+    staged = (-(-(shots_run - 1) // spg) + 1) * cores_w <= 8
+    emu.run(3, 0, cfg=cfg)
+    got = emu.last_kernel()
+    if not staged:
+        assert got == 'macro_kernel', got
+    elif len(regs) <= 2:
+        assert got == 'macro_staged_kernel<2>', got
+    else:                       # <2> when the programs happen to read / write at most 2 of them
+        assert got in ('macro_staged_kernel<2>', 'macro_staged_kernel<16>'), got
 
 
 @pytest.mark.parametrize('C', [1, 2, 4, 8, 16, 32, 64])
