@@ -19,6 +19,8 @@ Sub-objects on the same line, each with its own roofline and CPU baselines:
                   int16 I/Q on 16 channels per sequence at 16 samples/clk
   "active_reset"  config 3: fproc_meas branching + sync barriers, 1.25*10^6
                   shots per GPU (10^7 over 8 GPUs)
+  "lut"           config 3's circuit through the fproc_lut back end: every
+                  core waits on a syndrome LUT over the 8 measurements
   "rb"            config 4 at its stated size: 10^5 distinct 2-core depth-200
                   RB sequences x 10 shots per GPU
 
@@ -482,18 +484,21 @@ def leg_dds(emu, args, world, rank, stream):
     return res
 
 
-def leg_active_reset(emu, args, world, rank, stream):
+def leg_active_reset(emu, args, world, rank, stream, lut=False):
     """config 3 (BASELINE configs[2]): 8-core active reset -- readout,
     fproc_meas branch to a conditional X180, sync barriers -- 10^7 shots per
-    step over 8 GPUs, i.e. 1.25*10^6 shots per GPU (weak)"""
+    step over 8 GPUs, i.e. 1.25*10^6 shots per GPU (weak).  lut: the same
+    circuit through the fproc_lut back end (workloads.config3_lut: every core
+    waits on a syndrome LUT over all 8 measurements, hdl/fproc_lut.sv)"""
     import torch
     from distributed_processor_amd import _abi, sharding, workloads
     from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
-    ps = ProgramSet(workloads.config3_active_reset(8))
+    ps = ProgramSet(workloads.config3_lut(8) if lut else workloads.config3_active_reset(8))
     emu.load(ps)
+    lut_kw = dict(fproc_mode=_abi.FPROC_LUT, lut_mask=0xFF, lut_table=workloads.config3_lut_table(8)) if lut else {}
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
                            meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, hist_assign=True,
-                           lane_order=_abi.LANES_SHOT_MAJOR)       # whole-line event stores (DESIGN.md §3)
+                           lane_order=_abi.LANES_SHOT_MAJOR, **lut_kw)   # whole-line event stores (DESIGN.md §3)
     shot0, n = sharding.weak_shard(args.ar_shots, rank)
     out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
     pipe = sharding.HistogramPipeline(out['hist'], zero=False)     # each run assigns its histogram
@@ -510,21 +515,25 @@ def leg_active_reset(emu, args, world, rank, stream):
     assert (s['status'] == _abi.ST_DONE).all(), 'config 3: not every lane reached DONE'
     assert int(pipe.result().sum().item()) == n * world
     alg = float(bytes_per_lane(summ, cfg).sum())
-    prof = pmc('active_reset') if args.ar_shots == 1250000 else None
+    prof = pmc('lut' if lut else 'active_reset') if args.ar_shots == 1250000 else None
     ms_step = dt / args.steps * 1e3
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'branch_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
     roof['valu'] = valu_view(prof, roof['kernel_ms'])
-    res = {'metric': 'emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
-                     '1.25e6 shots/GPU)',
+    res = {'metric': ('emulated core-shots/s (config 3 via the fproc_lut back end: syndrome LUT over 8 '
+                      'measurements + sync, 1.25e6 shots/GPU)') if lut else
+                     ('emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
+                      '1.25e6 shots/GPU)'),
            'value': n * 8 * world * args.steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * args.steps / dt,
            'ms_per_step': ms_step, 'kernel_ms': kernel_ms,
            'instructions_per_s': float(s['n_instr'].astype(np.float64).sum()) * world * args.steps / dt,
-           'config': {'workload': 'config3_active_reset_8core', 'shots_per_gpu': n, 'global_shots_per_step': n * world,
+           'kernel': kernel,
+           'config': {'workload': 'config3_lut_8core' if lut else 'config3_active_reset_8core', 'shots_per_gpu': n,
+                      'global_shots_per_step': n * world,
                       'lane_order': LANE_ORDER_NAMES[cfg.lane_order]},
            'roofline': roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res['cpu_baseline'] = cpu_baselines(ps, cfg, 8192, 'config 3 active reset')
+        res['cpu_baseline'] = cpu_baselines(ps, cfg, 8192, 'config 3 ' + ('syndrome LUT' if lut else 'active reset'))
     del out
     torch.cuda.empty_cache()
     return res
@@ -613,7 +622,7 @@ def main():
     ap.add_argument('--rb-seqs', type=int, default=100000, help='config-4 RB sequences')
     ap.add_argument('--rb-spg', type=int, default=10, help='config-4 shots per sequence')
     ap.add_argument('--c1-shots', type=int, default=10 ** 6, help='config-1 shots per GPU per step')
-    ap.add_argument('--legs', default='config1,dds,active_reset,rb', help='sub-legs to run (comma list; "" for none)')
+    ap.add_argument('--legs', default='config1,dds,active_reset,lut,rb', help='sub-legs to run (comma list; "" for none)')
     args = ap.parse_args()
 
     import torch
@@ -654,7 +663,8 @@ def main():
               'cpu_baseline'):
         if k in main_leg:
             result[k] = main_leg[k]
-    fns = {'config1': leg_config1, 'dds': leg_dds, 'active_reset': leg_active_reset, 'rb': leg_rb}
+    fns = {'config1': leg_config1, 'dds': leg_dds, 'active_reset': leg_active_reset, 'rb': leg_rb,
+           'lut': lambda *a: leg_active_reset(*a, lut=True)}
     for name in [x for x in args.legs.split(',') if x]:
         result[name] = fns[name](emu, args, world, rank, stream)
     result['box'] = {'fill_GBps': fill_gbps(), 'device': torch.cuda.get_device_name(local)}

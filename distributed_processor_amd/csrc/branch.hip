@@ -33,8 +33,9 @@
 //
 // Branches guard only stores, LDS writes and the measurement draw.  The
 // meas_lut back end (FEAT_LUT: hdl/fproc_lut.sv, core_state_mgr.sv,
-// meas_lut.sv) runs the LUT FSM in each shot's leader lane over the shot's
-// merged measurement stream, as interp_kernel does.
+// meas_lut.sv) runs the LUT FSM over the shot's merged measurement stream in
+// all the shot's lanes at once (group min / ballots), where interp_kernel
+// runs it serially in the shot's leader lane.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -116,10 +117,8 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 
     __shared__ uint32_t s_regs[REGS ? 16 : 1][REGS ? BLOCK : 1];
     __shared__ uint32_t s_mt[MT][BLOCK];              // measurements {valid cycle << 1 | bit}, readable by the shot
-    // meas_lut (hdl/meas_lut.sv, core_state_mgr.sv), per shot: the leader's
-    // merge cursor into each lane's s_mt, and the fires it published, each
-    // as {fire cycle << 1 | this lane's bit of lut_out}
-    __shared__ uint32_t s_cur[LUT ? BLOCK : 1];
+    // meas_lut (hdl/meas_lut.sv, core_state_mgr.sv): the shot's fires so
+    // far, each as {fire cycle << 1 | this lane's bit of lut_out}
     __shared__ uint32_t s_fire[NF][LUT ? BLOCK : 1];
     __shared__ uint32_t s_pref[PLDS ? BLOCK + 1 : 1];
     __shared__ uint32_t s_scan[BLOCK / 64];
@@ -171,11 +170,11 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 #pragma unroll
         for (int m = 0; m < MT; m++) s_mt[m][tid] = INF32;
     }
-    if constexpr (LUT) s_cur[tid] = 0;
-    // leader-only meas_lut state (meas_lut.sv:27-56): OR-accumulated valid /
-    // measurement bits of the masked cores, the last fire, fires so far
+    // meas_lut state (meas_lut.sv:27-56), the same in every lane of a shot:
+    // OR-accumulated valid / measurement bits of the masked cores, the last
+    // fire, fires so far; and this lane's merge cursor into its s_mt records
     uint64_t lut_valid = 0, lut_addr = 0;
-    uint32_t lut_last_fire = INF32, nfire = 0;
+    uint32_t lut_last_fire = INF32, nfire = 0, lut_cur = 0;
 
     uint32_t mode = valid ? B_RUN : B_FIN;
     // qclk(x) = x + qoff for every decode after the first (hdl/qclk.v: it
@@ -478,20 +477,22 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             }
         }
 
-        // ---- meas_lut (LUT): the shot's leader merges the group's recorded
+        // ---- meas_lut (LUT): the shot merges its recorded
         // measurements in time order up to the horizon before which no
         // measurement can still appear (the group's bound on its next strobe
         // + meas_latency), runs the LUT FSM over them (hdl/meas_lut.sv:27-56:
         // OR-accumulate the masked cores' valid / bits, fire when every masked
         // core is valid, then clear; the cycle after a fire ignores inputs)
         // and publishes the fires; a lane waiting on the LUT (core_state_mgr
-        // WAIT_LUT) takes the first fire after its read.  Skipped in
-        // iterations where no lane waits and no measurement is unmerged. ----
+        // WAIT_LUT) takes the first fire after its read. ----
         bool lut_rel = false;
         if constexpr (LUT) {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // this iteration's s_mt writes
             __builtin_amdgcn_wave_barrier();
-            if (__any(mode == B_LUT || (valid && min(n_meas, (uint32_t)MT) > s_cur[tid]))) {
+            // merged lazily, only while some lane waits on the LUT: the
+            // records stay in s_mt, and a fire matters only to a waiting lane,
+            // so merging them later in the same order yields the same fires
+            if (__any(mode == B_LUT)) {
                 uint32_t bound = mode == B_RUN ? t + 2u : mode == B_LUT ? wait_d + 7u : INF32;
                 if constexpr (SYNC) {
                     if (__any(mode == B_SYNC)) {
@@ -501,55 +502,46 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
                 }
                 const uint32_t gmin = group_reduce<0>(bound, C);
                 const bool any_run_grp = group_bits(__ballot(mode == B_RUN), wl, C) != 0ull;
-                bool fired = false;
-                if (tid == leader_tid && valid) {
-                    uint32_t H = INF32;
-                    if (any_run_grp && gmin != INF32) {
-                        const uint64_t h = (uint64_t)gmin + p.meas_latency - 1u;
-                        H = h > INF32 ? INF32 : (uint32_t)h;
-                    }
-                    // nothing runs: every later measurement follows a release, i.e. a fire
-                    const bool stop_at_fire = !any_run_grp;
-                    for (;;) {
-                        uint32_t tmin = INF32;
-                        for (uint32_t c = 0; c < C; c++) {
-                            const uint32_t cur = s_cur[tid + c];
-                            const uint32_t e = cur < (uint32_t)MT ? s_mt[cur < (uint32_t)MT ? cur : 0u][tid + c] : INF32;
-                            tmin = (e != INF32 && (e >> 1) < tmin) ? e >> 1 : tmin;
-                        }
-                        if (tmin == INF32 || tmin > H) break;
-                        uint64_t v = 0, mv = 0;
-                        for (uint32_t c = 0; c < C; c++) {
-                            const uint32_t cur = s_cur[tid + c];
-                            const uint32_t e = cur < (uint32_t)MT ? s_mt[cur < (uint32_t)MT ? cur : 0u][tid + c] : INF32;
-                            if (e != INF32 && (e >> 1) == tmin) {
-                                v |= 1ull << c;
-                                mv |= (uint64_t)(e & 1u) << c;
-                                s_cur[tid + c] = cur + 1u;
-                            }
-                        }
-                        if (lut_last_fire != INF32 && tmin == lut_last_fire + 1u) continue;
-                        const uint64_t nv = lut_valid | v, na = lut_addr | (v & mv);
-                        if (((uint64_t)p.lut_mask & nv) == (uint64_t)p.lut_mask) {
-                            lut_last_fire = tmin;
-                            if (nfire < (uint32_t)NF) {
-                                const uint64_t o = p.lut_table[na & 0xFFu];
-                                for (uint32_t c = 0; c < C; c++)
-                                    s_fire[nfire < (uint32_t)NF ? nfire : 0u][tid + c] = (tmin << 1) | (uint32_t)((o >> c) & 1ull);
-                            }
-                            nfire++;
-                            lut_valid = 0;
-                            lut_addr = 0;
-                            fired = true;
-                            if (stop_at_fire) break;
-                        } else {
-                            lut_valid = nv;
-                            lut_addr = na;
-                        }
-                    }
+                uint32_t H = INF32;
+                if (any_run_grp && gmin != INF32) {
+                    const uint64_t h = (uint64_t)gmin + p.meas_latency - 1u;
+                    H = h > INF32 ? INF32 : (uint32_t)h;
                 }
-                const uint32_t nf_grp = (uint32_t)__shfl((int)nfire, (int)(wl & ~(C - 1u)), 64);
-                const bool grp_fired = group_bits(__ballot(fired), wl, C) != 0ull;
+                // nothing runs: every later measurement follows a release, i.e. a fire
+                const bool stop_at_fire = !any_run_grp;
+                // Every lane of a shot runs the merge and the FSM on
+                // group-uniform values (no serial scan by a leader): the
+                // shot's next measurement cycle is the DPP group minimum over
+                // each lane's own next unmerged record, its valid / bit
+                // vectors are ballots
+                bool fired = false, busy = valid;            // busy: this shot still merges
+                while (__any(busy)) {
+                    const uint32_t e = lut_cur < (uint32_t)MT ? s_mt[lut_cur < (uint32_t)MT ? lut_cur : 0u][tid] : INF32;
+                    const uint32_t my = e == INF32 ? INF32 : e >> 1;
+                    const uint32_t tmin = group_reduce<0>(my, C);
+                    busy = busy && tmin != INF32 && tmin <= H;
+                    const bool hit = busy && my == tmin;
+                    const uint64_t v = group_bits(__ballot(hit), wl, C);
+                    const uint64_t mv = group_bits(__ballot(hit && (e & 1u)), wl, C);
+                    lut_cur += hit ? 1u : 0u;
+                    const bool upd = busy && !(lut_last_fire != INF32 && tmin == lut_last_fire + 1u);
+                    const uint64_t nv = lut_valid | v, na = lut_addr | (v & mv);
+                    const bool fire = upd && (((uint64_t)p.lut_mask & nv) == (uint64_t)p.lut_mask);
+                    if (fire) {
+                        if (nfire < (uint32_t)NF) {
+                            const uint64_t o = p.lut_table[na & 0xFFu];
+                            s_fire[nfire < (uint32_t)NF ? nfire : 0u][tid] = (tmin << 1) | (uint32_t)((o >> core) & 1ull);
+                        }
+                        lut_last_fire = tmin;
+                        nfire++;
+                        fired = true;
+                    }
+                    lut_valid = fire ? 0ull : upd ? nv : lut_valid;
+                    lut_addr = fire ? 0ull : upd ? na : lut_addr;
+                    busy = busy && !(fire && stop_at_fire);
+                }
+                const uint32_t nf_grp = nfire;               // the same in every lane of the shot
+                const bool grp_fired = fired;
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 if (mode == B_LUT) {

@@ -158,7 +158,10 @@ hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream);
 // register slots the macro image names: 2, else 16 in LDS), else
 // macro_kernel (staged = false)
 constexpr uint32_t MACRO_SLOTS = 8;     // distinct programs per wave whose macros are staged in LDS
-constexpr uint32_t MACRO_CHUNK = 8;     // macros per program per staged chunk
+#ifndef DPEMU_MACRO_CHUNK
+#define DPEMU_MACRO_CHUNK 16
+#endif
+constexpr uint32_t MACRO_CHUNK = DPEMU_MACRO_CHUNK;   // macros per program per staged chunk (A/B: -DDPEMU_MACRO_CHUNK=)
 hipError_t launch_macro(const KParams &p, bool staged, int nr, hipStream_t stream);
 constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no command; ALU ctl bit 31: present
 

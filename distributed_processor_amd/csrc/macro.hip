@@ -448,9 +448,14 @@ struct MacroLane {
             alu_general(imm, ctl);
             return;
         }
+        // the batched shape: every present lane runs a reg_alu with op key_u
+        // within max_cycles.  Operands are read only where the op and the
+        // lanes' forms need them (uniform tests), the result written to rd,
+        // the register trace only when it is on
         const uint32_t D = t;
-        const uint32_t in0 = (ctl & 8u) ? reg_rd((ctl >> 12) & 15u) : imm;
-        const uint32_t b = reg_rd((ctl >> 4) & 15u);
+        uint32_t in0 = imm;
+        if (__ballot(pres && (ctl & 8u))) in0 = (ctl & 8u) ? reg_rd((ctl >> 12) & 15u) : imm;
+        const uint32_t b = (key_u == 0u || key_u == 7u) ? 0u : reg_rd((ctl >> 4) & 15u);
         uint32_t out;
         switch (key_u) {                                     // alu.v:20-50
         case 0: out = in0; break;
@@ -462,7 +467,13 @@ struct MacroLane {
         case 6: out = b; break;
         default: out = 0u; break;
         }
-        alu_common(pres, D, ctl, out);
+        const uint32_t rd = (ctl >> 8) & 15u;
+        reg_wr(pres, rd, out);
+        if (tr_on && pres && n_tr < p.trace_cap)
+            p.trace[(uint64_t)n_tr * p.n_lanes + lane] = make_uint4(D + 3u, (uint32_t)(p.reg_inv >> (4 * rd)) & 15u, out, 0u);
+        n_tr += pres ? 1u : 0u;
+        t = pres ? D + 4u : t;
+        k += pres ? 1u : 0u;
     }
     // pulse slot (a decode_cmd word, w bit 31 = absent): any command, the
     // first included (reset hold: qclk(0) = qclk(1) = 0, proc.sv:125-136;
@@ -516,12 +527,14 @@ struct MacroLane {
         const uint32_t D = t;
         const uint32_t wait = u.x - (qa_q + (D - qa_t));
         const bool stop = pres && wait > p.max_cycles - D;   // includes every late cmd_time (wait >= 2^31)
-        flags |= (stop && wait >= 0x80000000u) ? F_LATE : 0u;
-        st = stop ? ST_MAX_CYCLES : st;
+        if (__ballot(stop)) {
+            flags |= (stop && wait >= 0x80000000u) ? F_LATE : 0u;
+            st = stop ? ST_MAX_CYCLES : st;
+        }
         const bool ok = pres && !stop;
         const uint32_t tT = D + wait;
         pulse_write(u, pe, pp, pa);
-        pulse_regs(u);
+        if (__ballot(pres && (u.w & UOP_ANY_RS))) pulse_regs(u);
         emit1(ok, tT + 2u, 0u);
         t = ok ? tT + 3u : t;
         k += pres ? 1u : 0u;
@@ -529,17 +542,18 @@ struct MacroLane {
 };
 
 template <int NR>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR == 16 ? 4 : 6))) macro_staged_kernel(const KParams p)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR == 16 ? 3 : 4))) macro_staged_kernel(const KParams p)
 {
     constexpr uint32_t NW = BLOCK / 64, CH = MACRO_CHUNK, NS = MACRO_SLOTS;
-    constexpr uint32_t PIECES = NS * CH * 2;          // 16-B pieces of a chunk (2 per lane)
-    static_assert(PIECES == 128, "two pieces per lane");
+    constexpr uint32_t PIECES = NS * CH * 2;          // 16-B pieces of a chunk
+    constexpr uint32_t PL = PIECES / 64;              // pieces per lane
+    static_assert(PIECES % 64 == 0 && (CH & (CH - 1)) == 0, "whole pieces per lane, power-of-two chunk");
     __shared__ uint4 s_chunk0[NW][PIECES];            // [wave][slot][macro][2], double-buffered
     __shared__ uint4 s_chunk1[NW][PIECES];
     __shared__ uint32_t s_smb[NW][NS], s_sml[NW][NS]; // slot -> first / terminal macro
     __shared__ uint32_t s_regs[NR == 16 ? 16 : 1][NR == 16 ? BLOCK : 1];
-    __shared__ uint32_t s_hist[HIST_LDS_MAX];
     __shared__ uint32_t s_key[BLOCK];
+    extern __shared__ uint32_t s_hist[];              // HIST_LDS_MAX words when p.hist_lds (dynamic)
     const uint32_t tid = threadIdx.x, wv = tid >> 6, wl = tid & 63;
     const uint32_t C = p.C;
     uint32_t sl, core;
@@ -594,21 +608,21 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
     // VGPRs hold it in flight), into the buffer the wave is NOT reading; lane
     // wl of load instruction r fetches piece e = r * 64 + wl = slot e / 16,
     // macro (e / 2) % 8, half e % 2 (the LDS image is lane-linear)
-    const uint32_t s0 = wl >> 4, s1 = 4u + (wl >> 4), pj = (wl >> 1) & 7u, ph = wl & 1u;
+    // piece r of this lane: e = r * 64 + wl = slot e / (2 CH), macro (e / 2) % CH, half e % 2
+    const uint32_t pj = (wl >> 1) & (CH - 1u), ph = wl & 1u;
     const uint4 *const mbase = p.macros;
     // Only the lanes of the wave's nslots slots load (s_smb / s_sml of the
     // others were never written -- all of them in a wave with no valid lane);
     // the other pieces of the LDS image are never read.
-    const bool on0 = s0 < nslots, on1 = s1 < nslots;
     auto stage = [&](uint32_t c, uint4 *buf) __attribute__((always_inline)) {
         const uint32_t m = c * CH + pj;
-        if (on0) {
-            const uint32_t mb0 = s_smb[wv][s0], ml0 = s_sml[wv][s0];
-            __builtin_amdgcn_global_load_lds(mbase + 2ull * min(mb0 + m, ml0) + ph, buf, 16, 0, 0);
-        }
-        if (on1) {
-            const uint32_t mb1 = s_smb[wv][s1], ml1 = s_sml[wv][s1];
-            __builtin_amdgcn_global_load_lds(mbase + 2ull * min(mb1 + m, ml1) + ph, buf + 64, 16, 0, 0);
+#pragma unroll
+        for (uint32_t r = 0; r < PL; r++) {
+            const uint32_t sr = (r * 64u + wl) / (2u * CH);
+            if (sr < nslots) {
+                const uint32_t b0 = s_smb[wv][sr], l0 = s_sml[wv][sr];
+                __builtin_amdgcn_global_load_lds(mbase + 2ull * min(b0 + m, l0) + ph, buf + r * 64u, 16, 0, 0);
+            }
         }
     };
     const uint32_t moff = slot * (CH * 2);
@@ -664,8 +678,11 @@ hipError_t launch_macro(const KParams &p, bool staged, int nr, hipStream_t strea
     const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
     if (blocks == 0) return hipSuccess;
     if (!staged) hipLaunchKernelGGL(macro_kernel, dim3(blocks), dim3(BLOCK), 0, stream, p);
-    else if (nr == 2) hipLaunchKernelGGL(macro_staged_kernel<2>, dim3(blocks), dim3(BLOCK), 0, stream, p);
-    else hipLaunchKernelGGL(macro_staged_kernel<16>, dim3(blocks), dim3(BLOCK), 0, stream, p);
+    else {
+        const size_t shmem = p.hist_lds ? HIST_LDS_MAX * sizeof(uint32_t) : 0;
+        if (nr == 2) hipLaunchKernelGGL(macro_staged_kernel<2>, dim3(blocks), dim3(BLOCK), shmem, stream, p);
+        else hipLaunchKernelGGL(macro_staged_kernel<16>, dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    }
     return hipGetLastError();
 }
 

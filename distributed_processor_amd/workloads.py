@@ -178,6 +178,54 @@ def config3_active_reset(n_cores=8, extra_pulses=0):
 CONFIG3_MEAS_LATENCY = READ_CLKS + 32   # rdlo strobe -> meas_valid, inside the 64-clock hold
 
 
+def config3_lut(n_cores=8):
+    """Config 3 with the fproc_lut back end (hdl/fproc_lut.sv): sync; read;
+    wait for the syndrome LUT (jump_fproc with fproc id 1 != 0:
+    core_state_mgr WAIT_LUT, hdl/core_state_mgr.sv:58-69) -- issued right
+    after the readout pulses, so every core waits before the measurements
+    arrive; the LUT fires once every masked core has measured
+    (meas_lut.sv:27-49) -- X90 X90 on the core's LUT bit; sync; read; done.
+    Run it with fproc_mode FPROC_LUT, lut_mask = all cores and lut_table =
+    config3_lut_table(n_cores), meas_latency CONFIG3_MEAS_LATENCY."""
+    prog = {}
+    for c in range(n_cores):
+        q = qubit_params(c)
+        b = CoreBuilder()
+        b.emit(isa.pulse_reset())
+        b.emit(isa.sync(0))
+        t_end = readout(b, q, 10)
+        jf = len(b.words)
+        b.emit(0)                                      # jump_fproc placeholder (LUT wait)
+        b.emit(isa.jump_i(jf + 4))                     # -> second sync
+        # the LUT fires at rdlo strobe + meas_latency (<= t_end + 64); decode
+        # after a taken jump_fproc 6 later: the X90 pair after that
+        t1 = t_end + HOLD_CLKS + 3 + 8 + 4
+        b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t1)
+        b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t1 + X90_CLKS)
+        b.words[jf] = isa.alu_cmd('jump_fproc', 'i', 1, 'eq', jump_cmd_ptr=jf + 2, func_id=1)
+        b.emit(isa.sync(1))
+        readout(b, q, 10)
+        b.emit(isa.done_cmd())
+        prog[str(c)] = b.assembled()
+    return prog
+
+
+def config3_lut_table(n_cores=8):
+    """syndrome table of config3_lut: address a = the cores' outcomes (bit c
+    = core c); core c's correction bit = a_c XOR a_(c+1 mod n) -- the
+    neighbour-parity syndrome of a repetition code -- so a core flips when
+    its outcome differs from its neighbour's.  256 entries (meas_lut
+    addresses are 8 bits wide, include/dpemu.h lut_table)"""
+    n = int(n_cores)
+    full = (1 << n) - 1
+    table = []
+    for a in range(256):
+        a &= full
+        rot = ((a >> 1) | ((a & 1) << (n - 1))) & full
+        table.append(a ^ rot)
+    return table
+
+
 # ---------------------------------------------------------------- config 4
 # single-qubit Cliffords as X90 / Y90 pulses with virtual Z (phase register);
 # index -> (list of ('x'|'y'), z quarter turns applied after)

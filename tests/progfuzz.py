@@ -57,7 +57,7 @@ class Gen:
         if r.random() < 0.2:
             k = r.choice(['freq', 'phase', 'amp', 'env'])
             f.pop(k + '_word', None)
-            f[k + '_regaddr'] = r.choice(self.regs)
+            f[k + '_regaddr'] = r.randint(0, 15) if len(self.regs) == 16 else r.choice(self.regs)
         if r.random() < 0.1:
             f.pop('cfg_word', None)
         return f
@@ -93,12 +93,14 @@ class Gen:
                 q += 3
             elif kind == 'alu':
                 op = r.randrange(8)
-                rd = r.randint(0, 7) if len(self.regs) == 16 else r.choice(self.regs)
+                # (the default register set draws exactly as before: same random streams)
+                reg = (lambda: r.randint(0, 15)) if len(self.regs) == 16 else (lambda: r.choice(self.regs))
+                dst = (lambda: r.randint(0, 7)) if len(self.regs) == 16 else (lambda: r.choice(self.regs))
                 if r.random() < 0.5:
                     words.append(raw(1, 0, op, imm=r.choice([r.randint(-40, 40), r.getrandbits(32)]),
-                                     rs1=r.choice(self.regs), rd=rd))
+                                     rs1=reg(), rd=dst()))
                 else:
-                    words.append(raw(1, 1, op, rs0=r.choice(self.regs), rs1=r.choice(self.regs), rd=rd))
+                    words.append(raw(1, 1, op, rs0=reg(), rs1=reg(), rd=dst()))
                 q += 4
             elif kind == 'incq':
                 ops = [1, 1, 1, 0, 6, 7] + ([2] if self.allow_late else [])

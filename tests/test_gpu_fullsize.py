@@ -130,3 +130,21 @@ def test_config5_full_launch_sampled_channels(emu):
         raise AssertionError('{} mismatching samples, first at channel {} sample {}'.format(
             len(bad), int(pick[bad[0][0]]), int(bad[0][1])))
     assert (ref[0::2] != 0).any(axis=1).all() and (ref[1::2] != 0).any(axis=1).all()   # qdrv and rdrv play
+
+
+@pytest.mark.parametrize('shape', [{}, BENCH_SHAPE], ids=['core_major', 'bench_shape'])
+def test_config3_lut_full_shard_bit_exact(emu, shape):
+    """config 3 through the fproc_lut back end (workloads.config3_lut: every
+    core waits on the syndrome LUT, hdl/fproc_lut.sv) at the per-GPU shard
+    size, rank 3's shard: branch_kernel with the LUT FSM, every output equal
+    to oracle_fast"""
+    ps = ProgramSet(workloads.config3_lut(8))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
+                           fproc_mode=_abi.FPROC_LUT, meas_latency=workloads.CONFIG3_MEAS_LATENCY, lut_mask=0xFF,
+                           lut_table=workloads.config3_lut_table(8), seed=0x5EED, p1=0.5, **shape)
+    n = 1250000
+    g = run_full(emu, ps, cfg, n, 3 * n, ('summary', 'events', 'meas', 'hist'))
+    assert emu.last_kernel().startswith('branch_kernel<'), emu.last_kernel()
+    s = _abi.unpack_summary(g['summary'].view(np.uint32))
+    assert (s['status'] == _abi.ST_DONE).all()
+    assert int(g['hist'].sum()) == n

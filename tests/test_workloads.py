@@ -65,7 +65,31 @@ def test_from_arrays_validates():
         ProgramSet.from_arrays(w, [0], [2], [0, 0, 0], 1, 3)         # C not a power of two
 
 
-@pytest.mark.parametrize('name', ['config1', 'config2', 'config3', 'config4'])
+def lut_case():
+    ps = ProgramSet(workloads.config3_lut(8))
+    cfg = _abi.make_config(8, max_cycles=50000, event_cap=16, trace_cap=16, meas_cap=4, fproc_mode=_abi.FPROC_LUT,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, lut_mask=0xFF,
+                           lut_table=workloads.config3_lut_table(8), p1=0.5)
+    return ps, cfg
+
+
+def test_config3_lut_syndrome():
+    """the syndrome-LUT workload on oracle_fast: every shot DONE, each core
+    plays its X90 pair exactly when bit c of lut_table[outcomes] is set"""
+    ps, cfg = lut_case()
+    n, C = 3000, 8
+    f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n, want=('summary',))
+    s = _abi.unpack_summary(f['summary'])
+    assert (s['status'] == _abi.ST_DONE).all() and (s['flags'] == 0).all()
+    first = (s['meas_bits'].reshape(C, n) & 1).astype(np.int64)
+    a = (first << np.arange(C)[:, None]).sum(0)
+    tab = np.array(workloads.config3_lut_table(C))
+    flip = (tab[a][None, :] >> np.arange(C)[:, None]) & 1
+    np.testing.assert_array_equal(s['n_events'].reshape(C, n), 5 + 2 * flip)
+    assert 0.4 < flip.mean() < 0.6
+
+
+@pytest.mark.parametrize('name', ['config1', 'config2', 'config3', 'config4', 'config3_lut'])
 def test_rtl_batch_matches_fast(name):
     if name == 'config1':
         ps = ProgramSet(workloads.config1_linear())
@@ -77,6 +101,8 @@ def test_rtl_batch_matches_fast(name):
         ps = ProgramSet(workloads.config3_active_reset(8))
         cfg = _abi.make_config(8, max_cycles=50000, event_cap=16, trace_cap=16, meas_cap=4,
                                meas_latency=workloads.CONFIG3_MEAS_LATENCY)
+    elif name == 'config3_lut':
+        ps, cfg = lut_case()
     else:
         ps = workloads.config4_rb_set(n_seq=12, depth=40)
         cfg = _abi.make_config(2, n_groups=12, shots_per_group=3, event_cap=200, trace_cap=300, meas_cap=2)
