@@ -49,6 +49,17 @@ __device__ __forceinline__ uint32_t alu_macro(uint32_t op, uint32_t a, uint32_t 
     return r;
 }
 
+// alu.v:20-50 as a select tree on op's bits (no per-op compares)
+__device__ __forceinline__ uint32_t alu_eval(uint32_t op, uint32_t a, uint32_t b)
+{
+    const uint32_t sub = a - b;
+    const uint32_t lt = (int32_t)a < (int32_t)b;
+    const bool b0 = op & 1u, b1 = op & 2u;
+    const uint32_t lo = b1 ? (b0 ? (uint32_t)(sub == 0u) : sub) : (b0 ? a + b : a);   // 0-3
+    const uint32_t hi = b1 ? (b0 ? 0u : b) : (lt ^ (uint32_t)b0);                     // 4-7
+    return (op & 4u) ? hi : lo;
+}
+
 // 6 waves per SIMD: the register budget of the prefetched loop (80 VGPRs);
 // same-process A/B on config 4 (scripts/ab.py): 4.76 ms vs 5.05 without the
 // prefetch and 6.7 when squeezed to 7 waves (spills)
@@ -539,6 +550,50 @@ struct MacroLane {
         t = ok ? tT + 3u : t;
         k += pres ? 1u : 0u;
     }
+
+    // ---- the RB-shape iteration: ONE wave-uniform test for the whole macro
+    // (simple_ok), then all three slots branch-free, written through selects.
+    // Holds when every running lane is past the reset hold, at least 8 cycles
+    // inside max_cycles (so no slot can be stopped before its decode), its
+    // ALU slots hold reg_alu (not inc_qclk), its pulse slot (if present) a
+    // PULSE_WRITE_TRIG, and no register trace is requested: then the slots
+    // retire exactly as alu_step / pulse_step would, without their per-slot
+    // ballots and the uniform-op switch (a chain of scalar branches).
+    __device__ __forceinline__ bool simple_ok(const uint4 a, const uint4 u) const
+    {
+        const bool bad = ((int32_t)a.y < 0 && (a.y & 0x40000000u)) || ((int32_t)a.w < 0 && (a.w & 0x40000000u)) ||
+                         ((int32_t)u.w >= 0 && (u.y >> 28) != 0x9u) || t < qa_t || t + 8u > p.max_cycles;
+        return !tr_on && !__ballot(st == 0u && bad);
+    }
+    __device__ __forceinline__ void alu_simple(uint32_t imm, uint32_t ctl)
+    {
+        const bool pres = st == 0u && (int32_t)ctl < 0;
+        const uint32_t in0 = (ctl & 8u) ? reg_rd((ctl >> 12) & 15u) : imm;
+        const uint32_t out = alu_eval(ctl & 7u, in0, reg_rd((ctl >> 4) & 15u));
+        reg_wr(pres, (ctl >> 8) & 15u, out);
+        n_tr += pres ? 1u : 0u;
+        t = pres ? t + 4u : t;
+        k += pres ? 1u : 0u;
+    }
+    __device__ __forceinline__ void pulse_simple(const uint4 u)
+    {
+        const bool pres = st == 0u && (int32_t)u.w >= 0;
+        const uint32_t D = t;
+        const uint32_t wait = u.x - (qa_q + (D - qa_t));
+        const bool stop = pres && wait > p.max_cycles - D;   // includes every late cmd_time (wait >= 2^31)
+        flags |= (stop && wait >= 0x80000000u) ? F_LATE : 0u;
+        st = stop ? ST_MAX_CYCLES : st;
+        const bool ok = pres && !stop;
+        pulse_write(u, pe, pp, pa);
+        const uint32_t reg0 = reg_rd((u.w >> 20) & 15u);     // register-sourced fields (cleared by decode_cmd)
+        pe |= (u.w & UOP_RS_ENV) ? (reg0 & 0xFFFFFFu) : 0u;
+        pp |= (u.w & UOP_RS_PH) ? (reg0 & 0x1FFFFu) : 0u;
+        pp |= (u.w & UOP_RS_FR) ? ((reg0 & 0x1FFu) << 17) : 0u;
+        pa = (u.w & UOP_RS_AMP) ? (reg0 & 0xFFFFu) : pa;
+        emit1(ok, D + wait + 2u, 0u);
+        t = ok ? D + wait + 3u : t;
+        k += pres ? 1u : 0u;
+    }
 };
 
 template <int NR>
@@ -637,9 +692,15 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
 #pragma unroll 1
         for (uint32_t i = 0; i < CH; i++) {
             const uint4 a = cur[2 * i], u = cur[2 * i + 1];
-            L.alu_step(a.x, a.y);
-            L.alu_step(a.z, a.w);
-            L.pulse_step(u);
+            if (L.simple_ok(a, u)) {
+                L.alu_simple(a.x, a.y);
+                L.alu_simple(a.z, a.w);
+                L.pulse_simple(u);
+            } else {
+                L.alu_step(a.x, a.y);
+                L.alu_step(a.z, a.w);
+                L.pulse_step(u);
+            }
         }
     };
     stage(0u, s_chunk0[wv]);
