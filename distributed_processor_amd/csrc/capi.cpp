@@ -34,6 +34,8 @@ struct dpemu_ctx {
     bool has_fproc = false, has_sync = false, straight = false, linear = false, reg_writes = false;
     // register slots of the macro image (remap_macro_regs): 2 or 4 in VGPRs, else 16 (identity map)
     int macro_nr = 16;
+    bool macro_addid = false;               // every ALU slot of the macro image is id0 / add
+    uint32_t macro_rs = 0;                  // UOP_RS_* fields its pulse slots register-source
     uint64_t reg_map = 0xFEDCBA9876543210ull, reg_inv = 0xFEDCBA9876543210ull;
     uint32_t reg_used = 0xFFFFu;
     uint32_t max_len = 0;              // longest program (commands)
@@ -203,6 +205,34 @@ static int remap_macro_regs(std::vector<uint32_t> &mac, uint64_t &map, uint64_t 
     return 2;
 }
 
+// Mark every macro of the lean-path shape (MACRO_SIMPLE, kernels.h) in the
+// image's pulse slots, and return whether every ALU slot is reg_alu id0 / add
+// (alu.v ops 0 / 1) and which pulse fields are register-sourced
+static bool mark_simple_macros(std::vector<uint32_t> &mac, const std::vector<uint32_t> &moff, uint32_t &rs)
+{
+    bool addid = true;
+    rs = 0;
+    size_t prog = 0;
+    for (size_t m = 0, i = 0; i < mac.size(); i += 8, m++) {
+        while (prog + 1 < moff.size() && moff[prog + 1] <= m) prog++;
+        const bool first = moff[prog] == m;
+        bool simple = !first;
+        for (int a = 0; a < 2; a++) {
+            const uint32_t ctl = mac[i + 2 * a + 1];
+            if (!(ctl >> 31)) continue;
+            if ((ctl >> 30) & 1u) simple = false;               // inc_qclk
+            if ((ctl & 7u) > 1u) addid = false;
+        }
+        uint32_t &w = mac[i + 7];
+        if (!(w >> 31)) {
+            if ((mac[i + 5] >> 28) != 0x9u) simple = false;    // not PULSE_WRITE_TRIG
+            rs |= w & (UOP_RS_ENV | UOP_RS_PH | UOP_RS_FR | UOP_RS_AMP);
+        }
+        if (simple) w |= MACRO_SIMPLE;
+    }
+    return addid;
+}
+
 static void free_programs(dpemu_ctx *ctx)
 {
     for (void *q : {(void *)ctx->d_uops, (void *)ctx->d_uops_t, (void *)ctx->d_macro, (void *)ctx->d_moff,
@@ -357,6 +387,7 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, 
         }
         moff[n_programs] = (uint32_t)(mac.size() / 8);
         ctx->macro_nr = remap_macro_regs(mac, ctx->reg_map, ctx->reg_inv, ctx->reg_used);
+        ctx->macro_addid = mark_simple_macros(mac, moff, ctx->macro_rs);
         HIPCHK(ctx, hipMalloc(&ctx->d_macro, mac.size() * 4));
         HIPCHK(ctx, hipMemcpy(ctx->d_macro, mac.data(), mac.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(ctx, hipMalloc(&ctx->d_moff, moff.size() * 4));
@@ -443,6 +474,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.max_len = ctx->max_len;
     p.macros = ctx->d_macro; p.macro_off = ctx->d_moff;
     p.reg_map = ctx->reg_map; p.reg_inv = ctx->reg_inv; p.reg_used = ctx->reg_used;
+    p.macro_rs = ctx->macro_rs;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
     p.summary = out->summary;
     p.events = reinterpret_cast<uint4 *>(out->events);
@@ -616,7 +648,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
-    else if (macro) HIPCHK(ctx, launch_macro(p, staged, ctx->macro_nr, stream));
+    else if (macro) HIPCHK(ctx, launch_macro(p, staged, ctx->macro_nr, ctx->macro_addid, stream));
     else if (branch) HIPCHK(ctx, launch_branch(p, bfeat, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, stream));
@@ -626,7 +658,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             snprintf(name, sizeof name, "straight_kernel<%s,fb%d>",
                      src == STRAIGHT_ROWS ? "rows" : src == STRAIGHT_PROG ? "prog" : "lds", fetch_batch);
         else if (macro && staged)
-            snprintf(name, sizeof name, "macro_staged_kernel<%d>", ctx->macro_nr);
+            snprintf(name, sizeof name, "macro_staged_kernel<%d%s>", ctx->macro_nr, ctx->macro_addid ? ",addid" : "");
         else if (macro)
             snprintf(name, sizeof name, "macro_kernel");
         else if (branch)

@@ -111,6 +111,7 @@ struct KParams {
     uint64_t reg_map;             // macro image register slots: reg_file register r is slot (reg_map >> 4 r) & 15
     uint64_t reg_inv;             //   for r in the reg_used mask (others are never named: they read 0);
     uint32_t reg_used;            //   slot s holds register (reg_inv >> 4 s) & 15 (trace addresses)
+    uint32_t macro_rs;            // UOP_RS_* fields some pulse slot of the macro image register-sources
     const uint32_t *p1_thr;
     const uint64_t *lut_table;
     // outputs (device, nullable); lane L = core * n_shots + shot (core-major)
@@ -162,8 +163,14 @@ constexpr uint32_t MACRO_SLOTS = 8;     // distinct programs per wave whose macr
 #define DPEMU_MACRO_CHUNK 16
 #endif
 constexpr uint32_t MACRO_CHUNK = DPEMU_MACRO_CHUNK;   // macros per program per staged chunk (A/B: -DDPEMU_MACRO_CHUNK=)
-hipError_t launch_macro(const KParams &p, bool staged, int nr, hipStream_t stream);
+// addid: every ALU slot of the image is reg_alu id0 / add (RB phase updates)
+hipError_t launch_macro(const KParams &p, bool staged, int nr, bool addid, hipStream_t stream);
 constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no command; ALU ctl bit 31: present
+// pulse slot w bit 30 (capi.cpp mark_simple_macros): not a program's first
+// macro, its ALU slots are reg_alu (no inc_qclk) and its pulse slot is a
+// PULSE_WRITE_TRIG or absent -- the shape macro_staged_kernel retires on its
+// lean path (runtime conditions permitting)
+constexpr uint32_t MACRO_SIMPLE = 0x40000000u;
 
 // ---- DDS ------------------------------------------------------------------
 // Two launches per synthesis (dds.hip): dds_index_kernel compacts each

@@ -336,12 +336,12 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
 // their closures (and a copy of the kernel arguments) in scratch memory
 // here -- 848 B per lane, every access a scratch round trip under vmcnt.
 
-template <int NR>
+template <int NR, bool ADDID>
 struct MacroLane {
     const KParams &p;
     uint32_t *s_regs_lane;                 // NR == 16: &s_regs[0][tid], stride BLOCK
     uint32_t lane, sl, core;
-    uint32_t rg[NR == 16 ? 1 : NR];
+    uint32_t rg[NR == 16 ? 2 : NR];          // (NR == 16: unused)
     uint32_t t, pe, pp, pa, qa_t, qa_q;
     uint32_t flags, n_ev, n_meas, meas_bits, last_bit, n_tr, k, st;
     uint4 *evp;                            // event slot n_ev of this lane
@@ -353,7 +353,7 @@ struct MacroLane {
         : p(p_), s_regs_lane(srl), lane(lane_), sl(sl_), core(core_)
     {
 #pragma unroll
-        for (int r = 0; r < (NR == 16 ? 1 : NR); r++) rg[r] = 0;
+        for (int r = 0; r < (NR == 16 ? 2 : NR); r++) rg[r] = 0;
         t = pe = pp = pa = 0;
         qa_t = 1; qa_q = 0;
         flags = n_ev = n_meas = meas_bits = last_bit = n_tr = k = 0;
@@ -391,7 +391,12 @@ struct MacroLane {
     __device__ __forceinline__ void emit1(bool ok, uint32_t te, uint32_t kind)
     {
         if (ok) {
-            if (n_ev < p.event_cap && ev_on) *evp = event_record(te, pe, pp, pa, kind);
+#ifdef MACRO_PROBE_NOSTORE                              // A/B probe only: no event stores
+            if (n_ev == 0xFFFFFFFFu)
+#else
+            if (n_ev < p.event_cap && ev_on)
+#endif
+                *evp = event_record(te, pe, pp, pa, kind);
             evp += p.n_lanes;
             n_ev++;
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {        // meas_elem 0xFF: none
@@ -575,6 +580,58 @@ struct MacroLane {
         t = pres ? t + 4u : t;
         k += pres ? 1u : 0u;
     }
+    // ---- the lean path (NR == 2, registers r0 / r1 in VGPRs): the macro
+    // carries MACRO_SIMPLE (capi.cpp: not a program's first, so past the
+    // reset hold; reg_alu ALU slots; a PULSE_WRITE_TRIG or no pulse slot) and
+    // every running lane is 8 cycles or more inside max_cycles, no trace.  The
+    // remapped register fields are one bit each (slot 0 / 1), so operand
+    // selection and the register write are v_bfe_i32 masks and v_bitop3
+    // selects, and the counters advance by masks (k - pm: +1 where present)
+    __device__ __forceinline__ bool lean_ok(const uint4 u) const
+    {
+        return !tr_on && !__ballot(st == 0u && (!(u.w & MACRO_SIMPLE) || t + 8u > p.max_cycles));
+    }
+    static __device__ __forceinline__ uint32_t bmask(uint32_t v, int b)     // bit b of v as 0 / ~0
+    {
+        return (uint32_t)(((int32_t)(v << (31 - b))) >> 31);
+    }
+    __device__ __forceinline__ void alu_lean(uint32_t run, uint32_t imm, uint32_t ctl)
+    {
+        const uint32_t pm = run & (uint32_t)((int32_t)ctl >> 31);             // present (bit 31) and running
+        const uint32_t in0 = bit_select(bmask(ctl, 3), bit_select(bmask(ctl, 12), rg[1], rg[0]), imm);
+        const uint32_t b = bit_select(bmask(ctl, 4), rg[1], rg[0]);
+        const uint32_t out = ADDID ? in0 + (b & bmask(ctl, 0)) : alu_eval(ctl & 7u, in0, b);
+        const uint32_t wm = bmask(ctl, 8);                                    // rd: slot 1
+        rg[1] = bit_select(pm & wm, out, rg[1]);
+        rg[0] = bit_select(pm & ~wm, out, rg[0]);
+        t += pm & 4u;
+        k -= pm;
+        n_tr -= pm;
+    }
+    __device__ __forceinline__ void pulse_lean(uint32_t run, const uint4 u)
+    {
+        const bool pres = run != 0u && (int32_t)u.w >= 0;
+        const uint32_t D = t;
+        const uint32_t wait = u.x - (qa_q + (D - qa_t));
+        const bool stop = pres && wait > p.max_cycles - D;   // includes every late cmd_time (wait >= 2^31)
+        flags |= (stop && wait >= 0x80000000u) ? F_LATE : 0u;
+        st = stop ? ST_MAX_CYCLES : st;
+        const bool ok = pres && !stop;
+        pulse_write(u, pe, pp, pa);
+        // register-sourced fields (decode_cmd cleared them), only those the image uses
+        const uint32_t rs = p.macro_rs;
+        if (rs) {
+            const uint32_t reg0 = bit_select(bmask(u.w, 20), rg[1], rg[0]);
+            if (rs & UOP_RS_ENV) pe |= reg0 & bmask(u.w, 16) & 0xFFFFFFu;
+            if (rs & UOP_RS_PH) pp |= reg0 & bmask(u.w, 17) & 0x1FFFFu;
+            if (rs & UOP_RS_FR) pp |= (reg0 << 17) & bmask(u.w, 18) & (0x1FFu << 17);
+            if (rs & UOP_RS_AMP) pa = bit_select(bmask(u.w, 19), reg0 & 0xFFFFu, pa);
+        }
+        emit1(ok, D + wait + 2u, 0u);
+        t = ok ? D + wait + 3u : t;
+        k += pres ? 1u : 0u;
+    }
+
     __device__ __forceinline__ void pulse_simple(const uint4 u)
     {
         const bool pres = st == 0u && (int32_t)u.w >= 0;
@@ -596,8 +653,11 @@ struct MacroLane {
     }
 };
 
-template <int NR>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR == 16 ? 3 : 4))) macro_staged_kernel(const KParams p)
+#ifndef MACRO_STAGED_WAVES
+#define MACRO_STAGED_WAVES 4
+#endif
+template <int NR, bool ADDID>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR == 16 ? 3 : MACRO_STAGED_WAVES))) macro_staged_kernel(const KParams p)
 {
     constexpr uint32_t NW = BLOCK / 64, CH = MACRO_CHUNK, NS = MACRO_SLOTS;
     constexpr uint32_t PIECES = NS * CH * 2;          // 16-B pieces of a chunk
@@ -632,7 +692,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
 #pragma unroll
         for (int r = 0; r < 16; r++) s_regs[r][tid] = 0;
     }
-    MacroLane<NR> L(p, NR == 16 ? &s_regs[0][tid] : nullptr, lane, sl, core, valid);
+    MacroLane<NR, ADDID> L(p, NR == 16 ? &s_regs[0][tid] : nullptr, lane, sl, core, valid);
 
     // ---- the wave's distinct programs -> slots (a uniform waterfall) ----
     uint32_t slot = 0, nslots = 0;
@@ -692,6 +752,15 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
 #pragma unroll 1
         for (uint32_t i = 0; i < CH; i++) {
             const uint4 a = cur[2 * i], u = cur[2 * i + 1];
+            if constexpr (NR == 2) {
+                if (L.lean_ok(u)) {
+                    const uint32_t run = L.st == 0u ? ~0u : 0u;
+                    L.alu_lean(run, a.x, a.y);
+                    L.alu_lean(run, a.z, a.w);
+                    L.pulse_lean(run, u);
+                    continue;
+                }
+            }
             if (L.simple_ok(a, u)) {
                 L.alu_simple(a.x, a.y);
                 L.alu_simple(a.z, a.w);
@@ -721,7 +790,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
                (p.trace_cap && L.n_tr > p.trace_cap ? F_TRACE_OVF : 0u);
 
     if (valid && p.summary) {
-        const uint32_t ip = (L.st & MacroLane<NR>::ST_TOP) ? L.k : L.k - 1u;
+        const uint32_t ip = (L.st & MacroLane<NR, ADDID>::ST_TOP) ? L.k : L.k - 1u;
         write_summary(p, lane, L.t, ip, L.st & 0xFFu, L.flags, L.n_ev, L.k, L.qclk_at(L.t), L.n_meas, L.meas_bits,
                       L.n_tr);
     }
@@ -734,15 +803,16 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
     count_outcome_block(p, s_hist, s_key, valid, core, sl, valid ? shot_group(p, sl) : 0u, L.last_bit);
 }
 
-hipError_t launch_macro(const KParams &p, bool staged, int nr, hipStream_t stream)
+hipError_t launch_macro(const KParams &p, bool staged, int nr, bool addid, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
     if (blocks == 0) return hipSuccess;
     if (!staged) hipLaunchKernelGGL(macro_kernel, dim3(blocks), dim3(BLOCK), 0, stream, p);
     else {
         const size_t shmem = p.hist_lds ? HIST_LDS_MAX * sizeof(uint32_t) : 0;
-        if (nr == 2) hipLaunchKernelGGL(macro_staged_kernel<2>, dim3(blocks), dim3(BLOCK), shmem, stream, p);
-        else hipLaunchKernelGGL(macro_staged_kernel<16>, dim3(blocks), dim3(BLOCK), shmem, stream, p);
+        if (nr == 2 && addid) hipLaunchKernelGGL((macro_staged_kernel<2, true>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
+        else if (nr == 2) hipLaunchKernelGGL((macro_staged_kernel<2, false>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
+        else hipLaunchKernelGGL((macro_staged_kernel<16, false>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
     }
     return hipGetLastError();
 }

@@ -159,7 +159,7 @@ def test_fuzz_linear_few_registers(emu, seed):
     cores_w = C if order else 64 // shots_run
     staged = (-(-(shots_run - 1) // spg) + 1) * cores_w <= 8
     emu.run(3, 0, cfg=cfg)
-    got = emu.last_kernel()
+    got = emu.last_kernel().replace(',addid', '')   # addid: every ALU op of the image is id0 / add
     if not staged:
         assert got == 'macro_kernel', got
     elif len(regs) <= 2:

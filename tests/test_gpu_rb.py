@@ -114,3 +114,29 @@ def test_full_size_properties(rb):
         assert torch.equal(o['hist'][g0:g0 + half // SPG], out['hist'][g0:g0 + half // SPG])
         assert int(o['hist'].sum()) == half
         del o
+
+
+@pytest.mark.parametrize('max_cycles', [9, 700, 1501, 4003, 20000])
+def test_rb_lean_path_edges(max_cycles):
+    """macro_staged_kernel's lean path (MACRO_SIMPLE macros, id0 / add ALU
+    image) hands over to the general slots when a lane comes within 8 cycles
+    of max_cycles, and on late cmd_times (stops): small RB tables cut at
+    several max_cycles, both lane orders, traces off and on (trace forces the
+    general path), every output against oracle_fast"""
+    ps = workloads.config4_rb_set(96, 40)
+    ops = ps.words[:, 3] >> 28
+    strobes = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
+                              ps.offsets.astype(np.int64))
+    from tests.test_gpu_parity import compare_all, run_pair
+    with Emulator(0) as emu:
+        for order in (_abi.LANES_CORE_MAJOR, _abi.LANES_SHOT_MAJOR):
+            for trace_cap in (0, 8):
+                cfg = _abi.make_config(2, n_groups=ps.n_groups, shots_per_group=SPG, max_cycles=max_cycles,
+                                       event_cap=int(strobes.max()) + 1, trace_cap=trace_cap, meas_cap=2,
+                                       meas_latency=64, seed=7, p1=0.5, lane_order=order)
+                g, f = run_pair(emu, ps, cfg, 960, 13)
+                compare_all(g, f, 'max_cycles {} order {} trace {}'.format(max_cycles, order, trace_cap))
+                emu.run(3, 0, cfg=cfg)
+                # shot-major waves span 5 sequences x 2 cores > MACRO_SLOTS: the per-lane macro_kernel
+                want = 'macro_staged_kernel<2,addid>' if order == _abi.LANES_CORE_MAJOR else 'macro_kernel'
+                assert emu.last_kernel() == want, emu.last_kernel()
