@@ -345,6 +345,7 @@ struct MacroLane {
     uint32_t t, pe, pp, pa, qa_t, qa_q;
     uint32_t flags, n_ev, n_meas, meas_bits, last_bit, n_tr, k, st;
     uint4 *evp;                            // event slot n_ev of this lane
+    uint32_t it = 0;                       // (A/B probe MACRO_PROBE_ITERSLOT only)
     bool tr_on, ev_on;
     static constexpr uint32_t ST_TOP = 0x100u;
 
@@ -396,7 +397,11 @@ struct MacroLane {
 #else
             if (n_ev < p.event_cap && ev_on)
 #endif
+#ifdef MACRO_PROBE_ITERSLOT                             // A/B probe only: record at slot = macro iteration
+                p.events[(uint64_t)min(it, p.event_cap - 1u) * p.n_lanes + lane] = event_record(te, pe, pp, pa, kind);
+#else
                 *evp = event_record(te, pe, pp, pa, kind);
+#endif
             evp += p.n_lanes;
             n_ev++;
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {        // meas_elem 0xFF: none
@@ -752,6 +757,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
 #pragma unroll 1
         for (uint32_t i = 0; i < CH; i++) {
             const uint4 a = cur[2 * i], u = cur[2 * i + 1];
+#ifdef MACRO_PROBE_ITERSLOT
+            L.it++;
+#endif
             if constexpr (NR == 2) {
                 if (L.lean_ok(u)) {
                     const uint32_t run = L.st == 0u ? ~0u : 0u;
