@@ -147,9 +147,12 @@ def config2_ramsey(n_cores=8, n_points=100, tau_step=4):
 HOLD_CLKS = 64    # hwconfig.FPROC_MEAS_CLKS: idle after the readout window
 
 
-def config3_active_reset(n_cores=8, extra_pulses=0):
+def config3_active_reset(n_cores=8, extra_pulses=0, read_shift=0):
     """sync; read; hold; if (1 == meas) X90 X90; sync; read; done.
-    extra_pulses: that many X90s after the second readout (per-command cost probes)."""
+    extra_pulses: that many X90s after the second readout (per-command cost probes).
+    read_shift: core c conditions on core (c + read_shift) % n_cores's outcome
+    (fproc_meas id, hdl/fproc_meas.sv:18-35: a cross-core read, as in
+    cocotb/fproc_meas/test_meas.py:62-83); 0 = its own."""
     prog = {}
     for c in range(n_cores):
         q = qubit_params(c)
@@ -165,7 +168,8 @@ def config3_active_reset(n_cores=8, extra_pulses=0):
         t1 = t_idle + 3 + 8 + 4                        # decode after jump_fproc (taken) + slack
         b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t1)
         b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t1 + X90_CLKS)
-        b.words[jf] = isa.alu_cmd('jump_fproc', 'i', 1, 'eq', jump_cmd_ptr=jf + 2, func_id=c)
+        b.words[jf] = isa.alu_cmd('jump_fproc', 'i', 1, 'eq', jump_cmd_ptr=jf + 2,
+                                  func_id=(c + read_shift) % n_cores)
         b.emit(isa.sync(1))
         t_x = readout(b, q, 10)
         for k in range(extra_pulses):

@@ -148,3 +148,24 @@ def test_config3_lut_full_shard_bit_exact(emu, shape):
     s = _abi.unpack_summary(g['summary'].view(np.uint32))
     assert (s['status'] == _abi.ST_DONE).all()
     assert int(g['hist'].sum()) == n
+
+
+def test_config3_cross_core_reads_full_shard(emu):
+    """config 3 with every core conditioning on ANOTHER core's outcome
+    (fproc_meas id = (c + 3) % 8: the cross-lane lookup through LDS of
+    branch_kernel), rank 5's 1.25 * 10^6-shot shard in the bench's launch
+    shape, every output equal to oracle_fast; the X90 pair ran exactly where
+    the read core's first outcome was 1"""
+    ps = ProgramSet(workloads.config3_active_reset(8, read_shift=3))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, **BENCH_SHAPE)
+    n = 1250000
+    g = run_full(emu, ps, cfg, n, 5 * n, ('summary', 'events', 'meas', 'hist'))
+    assert emu.last_kernel().startswith('branch_kernel<'), emu.last_kernel()
+    s = _abi.unpack_summary(g['summary'].view(np.uint32))
+    assert (s['status'] == _abi.ST_DONE).all()
+    first = (s['meas_bits'] & 1).astype(bool).reshape(n, 8)        # shot-major lanes
+    flip = np.roll(first, -3, axis=1)                              # core c reads core (c + 3) % 8
+    ne = s['n_events'].reshape(n, 8)
+    assert (ne[flip] == ne[~flip].min() + 2).all()
+

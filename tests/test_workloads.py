@@ -110,3 +110,19 @@ def test_rtl_batch_matches_fast(name):
     r, done = oracle.rtl_run_batch(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 7, 36, 1 << 20, 2)
     assert done == 36
     assert np.array_equal(r, f['summary'])
+
+
+def test_config3_cross_core_reads_oracle():
+    """read_shift: core c's conditional X90 pair follows core (c + 3) % 8's first outcome (oracle_fast)"""
+    import oracle
+    ps = ProgramSet(workloads.config3_active_reset(8, read_shift=3))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, meas_cap=4,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=11, p1=0.5,
+                           lane_order=_abi.LANES_SHOT_MAJOR)
+    n = 1000
+    f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n, want=('summary',))
+    s = _abi.unpack_summary(f['summary'].view(np.uint32))
+    assert (s['status'] == _abi.ST_DONE).all()
+    flip = np.roll((s['meas_bits'] & 1).astype(bool).reshape(n, 8), -3, axis=1)
+    ne = s['n_events'].reshape(n, 8)
+    assert (ne[flip] == ne[~flip].min() + 2).all() and flip.any() and (~flip).any()
