@@ -38,6 +38,16 @@ __device__ __forceinline__ uint32_t event_word(uint32_t pe, uint32_t kind)
     return (pe & 0x0FFFFFFFu) | (kind << 28);
 }
 
+// a * b as 64 bits in ONE v_mad_u64_u32 (hipcc emits a v_mul_lo_u32 +
+// v_mul_hi_u32 pair for lo / __umulhi: scripts/micro/mul_rate.hip measured a
+// Philox round 1.3x faster this way on gfx950, profiles/r03_mul_rate.jsonl)
+__device__ __forceinline__ uint64_t mul_wide(uint32_t a, uint32_t b)
+{
+    uint64_t r, carry;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(carry) : "v"(a), "s"(b));
+    return r;
+}
+
 // Philox4x32-10, output words 0..2 (counter = shot_lo, shot_hi, core, m; key = seed)
 __device__ __forceinline__ uint3 philox3(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m)
 {
@@ -45,8 +55,9 @@ __device__ __forceinline__ uint3 philox3(uint64_t seed, uint64_t shot, uint32_t 
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
     for (int r = 0; r < 10; r++) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint64_t p0 = mul_wide(c0, 0xD2511F53u), p1 = mul_wide(c2, 0xCD9E8D57u);
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;

@@ -1,69 +1,55 @@
-// Integer multiply issue rates on gfx950 (sizing the Philox measurement draw,
-// lane.h philox3): wave64 instructions/s of v_add_u32, v_mul_lo_u32,
-// v_mul_hi_u32 and v_mad_u64_u32 over 8 independent chains per lane at full
-// occupancy.  One JSON line per instruction.
+// mul_rate.hip -- throughput of the Philox round's 32x32 -> 64-bit products on
+// gfx950: v_mul_hi_u32 + v_mul_lo_u32 pairs (what hipcc emits for __umulhi and
+// a * b) against one v_mad_u64_u32 per product.  One JSON line per variant:
+// ms and products per second over the whole chip.
 #include <hip/hip_runtime.h>
-#include <cstdio>
+#include <stdint.h>
+#include <stdio.h>
 
-template <int OP>
-__global__ void __launch_bounds__(256) mul_kernel(uint32_t *out, uint32_t iters, uint32_t k)
+template <int MODE>
+__global__ void __launch_bounds__(256) rounds(uint32_t *out, uint32_t n)
 {
-    uint32_t a[8];
-#pragma unroll
-    for (int c = 0; c < 8; c++) a[c] = threadIdx.x * (c + 3) + blockIdx.x;
-    for (uint32_t i = 0; i < iters; i++) {
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[c]) : "s"(k));
-            if constexpr (OP == 1) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[c]) : "s"(k));
-            if constexpr (OP == 2) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[c]) : "s"(k));
-            if constexpr (OP == 3) {
-                uint64_t r;
-                asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a[c]), "s"(k) : "vcc");
-                a[c] = (uint32_t)r ^ (uint32_t)(r >> 32);
-            }
-            if constexpr (OP == 4) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[c]) : "s"(k));
+    uint32_t c0 = threadIdx.x, c1 = blockIdx.x, c2 = c0 ^ 0x55u, c3 = c1 * 7u;
+    uint32_t k0 = 1u, k1 = 2u;
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t hi0, lo0, hi1, lo1;
+        if constexpr (MODE == 0) {
+            hi0 = __umulhi(0xD2511F53u, c0); lo0 = 0xD2511F53u * c0;
+            hi1 = __umulhi(0xCD9E8D57u, c2); lo1 = 0xCD9E8D57u * c2;
+        } else {
+            uint64_t a, b, ca, cb;
+            asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(a), "=s"(ca) : "v"(c0), "s"(0xD2511F53u));
+            asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(b), "=s"(cb) : "v"(c2), "s"(0xCD9E8D57u));
+            hi0 = (uint32_t)(a >> 32); lo0 = (uint32_t)a; hi1 = (uint32_t)(b >> 32); lo1 = (uint32_t)b;
         }
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
-    uint32_t s = 0;
-#pragma unroll
-    for (int c = 0; c < 8; c++) s += a[c];
-    out[blockIdx.x * 256 + threadIdx.x] = s;
-}
-
-template <int OP>
-static void run(const char *name, uint32_t blocks, uint32_t iters, uint32_t *d)
-{
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    mul_kernel<OP><<<blocks, 256>>>(d, iters, 0x9E3779B9u);
-    hipDeviceSynchronize();
-    float best = 1e30f;
-    for (int r = 0; r < 5; r++) {
-        hipEventRecord(e0);
-        mul_kernel<OP><<<blocks, 256>>>(d, iters, 0x9E3779B9u);
-        hipEventRecord(e1);
-        hipEventSynchronize(e1);
-        float ms;
-        hipEventElapsedTime(&ms, e0, e1);
-        if (ms < best) best = ms;
-    }
-    const double n = blocks * 4.0 * iters * 8;   // wave-instructions of the op (mad: + 1 xor each)
-    printf("{\"op\": \"%s\", \"blocks\": %u, \"ms\": %.4f, \"wave_insts_per_s\": %.4e}\n", name, blocks, best,
-           n / (best * 1e-3));
+    out[blockIdx.x * 256 + threadIdx.x] = c0 ^ c1 ^ c2 ^ c3;
 }
 
 int main()
 {
-    uint32_t *d;
-    hipMalloc(&d, 256u * 8192u * 4u);
-    const uint32_t blocks = 8192, iters = 512;
-    run<0>("v_add_u32", blocks, iters, d);
-    run<1>("v_mul_lo_u32", blocks, iters, d);
-    run<2>("v_mul_hi_u32", blocks, iters, d);
-    run<3>("v_mad_u64_u32+v_xor", blocks, iters, d);
-    run<4>("v_mul_u32_u24", blocks, iters, d);
-    hipFree(d);
+    const uint32_t blocks = 256 * 16, n = 4096;
+    uint32_t *out;
+    hipMalloc(&out, blocks * 256 * 4);
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    for (int rep = 0; rep < 3; rep++) {
+        for (int mode = 0; mode < 2; mode++) {
+            hipEventRecord(a);
+            if (mode == 0) hipLaunchKernelGGL(rounds<0>, dim3(blocks), dim3(256), 0, 0, out, n);
+            else hipLaunchKernelGGL(rounds<1>, dim3(blocks), dim3(256), 0, 0, out, n);
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms = 0;
+            hipEventElapsedTime(&ms, a, b);
+            const double products = 2.0 * n * blocks * 256;
+            if (rep) printf("{\"variant\": \"%s\", \"ms\": %.4f, \"products_per_s\": %.4g}\n",
+                            mode == 0 ? "mul_hi+mul_lo" : "mad_u64_u32", ms, products / (ms * 1e-3));
+        }
+    }
+    hipFree(out);
     return 0;
 }
