@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libdpemu.so')
 
 # every entry point declared in include/dpemu.h
-EXPORTS = ('dpemu_abi_version', 'dpemu_create', 'dpemu_destroy', 'dpemu_last_error',
+EXPORTS = ('dpemu_abi_version', 'dpemu_struct_sizes', 'dpemu_create', 'dpemu_destroy', 'dpemu_last_error',
            'dpemu_load_programs', 'dpemu_run', 'dpemu_run_host', 'dpemu_dds', 'dpemu_dds_sin_lut',
            'dpemu_set_kernel_timing', 'dpemu_kernel_times', 'dpemu_last_kernel')
 
@@ -38,6 +38,7 @@ def load_library(path=LIB_PATH):
     L = C.CDLL(path)
     vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
     L.dpemu_abi_version.restype = C.c_int
+    L.dpemu_struct_sizes.argtypes = [vp]
     L.dpemu_create.argtypes = [C.c_int, C.POINTER(vp)]
     L.dpemu_destroy.argtypes = [vp]
     L.dpemu_last_error.argtypes = [vp]
@@ -55,6 +56,13 @@ def load_library(path=LIB_PATH):
     if L.dpemu_abi_version() != _abi.ABI_VERSION:
         raise DpemuError('ABI version mismatch: library {} vs host {}'.format(
             L.dpemu_abi_version(), _abi.ABI_VERSION))
+    # the struct layouts too: two builds of one ABI version from different
+    # header states must not share a process with a mismatched ctypes mirror
+    sizes = (C.c_uint64 * 3)()
+    L.dpemu_struct_sizes(sizes)
+    mine = (C.sizeof(_abi.Config), C.sizeof(_abi.Outputs), C.sizeof(_abi.DDSChannels))
+    if tuple(sizes) != mine:
+        raise DpemuError('struct layout mismatch: library {} vs host {} ({})'.format(tuple(sizes), mine, path))
     _libs[path] = L
     return L
 

@@ -247,6 +247,15 @@ extern "C" {
 
 int dpemu_abi_version(void) { return DPEMU_ABI_VERSION; }
 
+int dpemu_struct_sizes(uint64_t *out)
+{
+    if (!out) return DPEMU_E_INVALID;
+    out[0] = sizeof(dpemu_config);
+    out[1] = sizeof(dpemu_outputs);
+    out[2] = sizeof(dpemu_dds_channels);
+    return DPEMU_OK;
+}
+
 int dpemu_create(int device, dpemu_ctx **out)
 {
     if (!out) return DPEMU_E_INVALID;

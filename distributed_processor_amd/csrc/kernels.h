@@ -165,6 +165,10 @@ constexpr uint32_t MACRO_SLOTS = 8;     // distinct programs per wave whose macr
 constexpr uint32_t MACRO_CHUNK = DPEMU_MACRO_CHUNK;   // macros per program per staged chunk (A/B: -DDPEMU_MACRO_CHUNK=)
 // addid: every ALU slot of the image is reg_alu id0 / add (RB phase updates)
 hipError_t launch_macro(const KParams &p, bool staged, int nr, bool addid, hipStream_t stream);
+#ifndef DPEMU_MACRO_RING
+#define DPEMU_MACRO_RING 4
+#endif
+constexpr uint32_t MACRO_RING = DPEMU_MACRO_RING;     // event rows a staged wave holds in LDS (power of two >= 4; 0: A/B only)
 constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no command; ALU ctl bit 31: present
 // pulse slot w bit 30 (capi.cpp mark_simple_macros): not a program's first
 // macro, its ALU slots are reg_alu (no inc_qclk) and its pulse slot is a

@@ -188,6 +188,11 @@ typedef struct dpemu_ctx dpemu_ctx;
 
 /* Library / device --------------------------------------------------- */
 int         dpemu_abi_version(void);
+/* sizeof(dpemu_config), sizeof(dpemu_outputs), sizeof(dpemu_dds_channels) as
+ * this library was compiled: a binding compares them with its own layout
+ * before the first call (the version number alone does not catch a build
+ * from a half-edited header).  out: 3 entries. */
+int         dpemu_struct_sizes(uint64_t *out);
 int         dpemu_create(int device, dpemu_ctx **out);
 int         dpemu_destroy(dpemu_ctx *ctx);
 const char *dpemu_last_error(dpemu_ctx *ctx);

@@ -35,6 +35,10 @@ def test_abi_version_and_struct_sizes():
     assert C.sizeof(_abi.Config) == 12 * 4 + 16 + 8 + 64 * 4 + 256 * 8 + 16 + 8
     assert C.sizeof(_abi.Outputs) == 7 * 8
     assert C.sizeof(_abi.DDSChannels) == 4 * 4 + 8 * 8
+    sizes = (C.c_uint64 * 3)()
+    assert L.dpemu_struct_sizes(sizes) == 0
+    assert tuple(sizes) == (C.sizeof(_abi.Config), C.sizeof(_abi.Outputs), C.sizeof(_abi.DDSChannels))
+    assert L.dpemu_struct_sizes(None) != 0
 
 
 def test_output_struct_matches_header():
@@ -78,3 +82,17 @@ def test_config_validation():
         _abi.make_config(4, readout=dict(sep=1, win=4096))
     cfg = _abi.make_config(8, p1=[0.0, 1.0, 0.5])
     assert cfg.p1_threshold[0] == 0 and cfg.p1_threshold[1] == 0xFFFFFFFF and cfg.p1_threshold[2] == 2 ** 31
+
+
+def test_struct_layout_mismatch_refused(tmp_path, monkeypatch):
+    """a library whose struct layouts differ from the binding's ctypes mirror
+    is refused at load (dpemu_struct_sizes), whatever its version number"""
+    import shutil
+    lib = str(tmp_path / 'libdpemu_copy.so')
+    shutil.copy(_native.LIB_PATH, lib)
+
+    class Shorter(C.Structure):                 # a mirror missing dpemu_config's last field
+        _fields_ = [('x', C.c_uint8 * (C.sizeof(_abi.Config) - 4))]
+    monkeypatch.setattr(_abi, 'Config', Shorter)
+    with pytest.raises(_native.DpemuError, match='struct layout mismatch'):
+        _native.load_library(lib)
