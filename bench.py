@@ -155,7 +155,7 @@ def valu_view(prof, kernel_ms=None):
         v['frac'] = v['achieved'] / VALU_PEAK
     if prof.get('duration_ns'):
         v['frac_rocprof'] = n / (prof['duration_ns'] * 1e-9) / VALU_PEAK
-    for k in ('valu_insts_per_wave', 'valu_issue_pct', 'valu_busy_pct', 'valu_lane_util_pct', 'duration_ns',
+    for k in ('valu_insts_per_wave', 'valu_issue_pct', 'valu_lane_util_pct', 'duration_ns',
               'kernel', 'warnings'):
         if prof.get(k) is not None:
             v[k] = prof.get(k)

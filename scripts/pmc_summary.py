@@ -18,7 +18,9 @@ writes <dest>/<tag>_<kernel>_pmc.json with per-launch means:
     valu_issue_pct   SQ_INSTS_VALU x c / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs),
                      c = the measured cycles per wave64 integer-VALU
                      instruction at the issue peak (profiles/r03_valu_peak_pmc.json)
-    valu_busy_pct    SQ_ACTIVE_INST_VALU x 4 (quad-cycles) on the same denominator
+    (SQ_ACTIVE_INST_VALU equals SQ_INSTS_VALU on the peak microbenchmark, so
+    a 'busy' ratio of it at an assumed 4 cycles per instruction overstates the
+    VALU share wherever the kernel issues faster than 4; it is not reported)
     valu_frac_of_measured_peak  SQ_INSTS_VALU / duration / the measured peak
   A ratio above 100 % is reported as measured and flagged in 'warnings'.
 * valu_lane_util_pct = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)
@@ -121,7 +123,7 @@ def main():
         res['valu_peak_insts_per_s'] = peak
         res['valu_peak_cycles_per_inst'] = cpi
         warnings = []
-        for key, num, scale in (('valu_issue_pct', 'SQ_INSTS_VALU', cpi), ('valu_busy_pct', 'SQ_ACTIVE_INST_VALU', 4.0)):
+        for key, num, scale in (('valu_issue_pct', 'SQ_INSTS_VALU', cpi),):
             r_ = ratio(num, scale)
             if r_ is not None:
                 res[key] = r_
@@ -148,7 +150,7 @@ def main():
         path = os.path.join(dest, '{}_{}_pmc.json'.format(tag, k))
         with open(path, 'w') as f:
             json.dump(res, f, indent=1, sort_keys=True)
-        print(path, json.dumps({x: res.get(x) for x in ('duration_ns', 'hbm_bytes_per_launch', 'valu_busy_pct',
+        print(path, json.dumps({x: res.get(x) for x in ('duration_ns', 'hbm_bytes_per_launch',
                                                         'valu_issue_pct', 'valu_lane_util_pct')}))
 
 
