@@ -44,10 +44,6 @@
 
 #include "lane.h"
 
-#ifndef BRANCH_RING
-#define BRANCH_RING 0             // A/B builds: -DBRANCH_RING=4 keeps event rows in an LDS ring
-#endif
-
 namespace dpemu {
 
 namespace {
@@ -125,9 +121,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // far, each as {fire cycle << 1 | this lane's bit of lut_out}
     __shared__ uint32_t s_fire[NF][LUT ? BLOCK : 1];
     __shared__ uint32_t s_pref[PLDS ? BLOCK + 1 : 1];
-#if BRANCH_RING
-    __shared__ uint4 s_ring[BRANCH_RING][BLOCK];      // (A/B build) event rows in flight
-#endif
     __shared__ uint32_t s_scan[BLOCK / 64];
     // dynamic LDS: the staged programs (prog_lds_words commands), then the
     // histogram pre-aggregation bins when hist_lds
@@ -203,15 +196,8 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // stores and the same bytes (config 3: 0.480 -> 0.447 ms median,
     // profiles/r02_ar_rows_ab.json).  Slots [n_st, min(n_ev, cap)) are
     // pending in pend0, pend1; a third record pushes the oldest out.
-#if BRANCH_RING
-    // (A/B build) the records in an LDS ring instead: lane column, row k at
-    // s_ring[k % BRANCH_RING]; rows below the wave-uniform `rbase` are stored
-    uint4 *const ring = &s_ring[0][tid];
-    uint32_t rbase = 0;
-#else
     uint4 pend0 = make_uint4(0u, 0u, 0u, 0u), pend1 = pend0;
     uint32_t n_st = 0;
-#endif
 
     // pulse_iface strobe at cycle te (kind 0: trigger, 1: phase reset) with the
     // current pulse registers for lanes with `ok`; readout-element triggers
@@ -220,10 +206,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         if (ok) {
             if (n_ev < p.event_cap && p.events) {
                 const uint4 rec = event_record(te, pe, pp, pa, kind);
-#if BRANCH_RING
-                if (n_ev < rbase) ev_lane[(uint64_t)n_ev * n_lanes] = rec;   // row pushed out already
-                else ring[(n_ev & (BRANCH_RING - 1u)) * BLOCK] = rec;
-#else
                 const bool full = n_ev - n_st == 2u;    // the oldest goes out now
                 if (full) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
                 pend0 = sel4(full, pend1, pend0);
@@ -231,7 +213,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
                 const bool first = n_ev == n_st;
                 pend0 = sel4(first, rec, pend0);
                 pend1 = sel4(first, pend1, rec);
-#endif
             }
             n_ev++;
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {   // meas_elem 0xFF: none
@@ -298,25 +279,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     };
 
     // store the pending rows every unfinished lane has passed (all: at the end)
-#if BRANCH_RING
-    auto flush_base = [&]() __attribute__((always_inline)) {
-        if (min(n_ev, p.event_cap) > rbase) ev_lane[(uint64_t)rbase * n_lanes] = ring[(rbase & (BRANCH_RING - 1u)) * BLOCK];
-        rbase++;
-    };
-    // rows every unfinished lane has passed (all: every row), then push out
-    // rows a running lane could wrap onto in the next iteration (<= 1 record;
-    // the peeled first iteration makes <= 2 from rbase 0)
-    auto flush_rows = [&](bool all) __attribute__((always_inline)) {
-        if (!p.events) return;
-        if (all) {
-            while (__any(min(n_ev, p.event_cap) > rbase)) flush_base();
-            return;
-        }
-        const uint32_t done = min(wave_min(mode == B_FIN ? INF32 : n_ev), p.event_cap);
-        while (rbase < done) flush_base();
-        while (__any(mode != B_FIN && n_ev + 1u > rbase + (BRANCH_RING - 1u))) flush_base();
-    };
-#else
     auto flush_rows = [&](bool all) __attribute__((always_inline)) {
         if (!p.events) return;
         const uint32_t ne = min(n_ev, p.event_cap);
@@ -331,7 +293,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             n_st += f ? 1u : 0u;
         }
     };
-#endif
 
     // One lockstep iteration: every running lane retires at most one command.
     // FIRST: the peeled first iteration, where every lane decodes at cycle 0
