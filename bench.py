@@ -138,7 +138,7 @@ def rocprof_avg_ms(kernel_substr):
     return None
 
 
-def valu_view(prof, kernel_ms=None):
+def valu_view(prof, kernel_ms=None, instrs=None):
     """the kernel's VALU roofline beside its HBM one: VALU instructions per
     launch (rocprof SQ_INSTS_VALU) over the kernel time against the measured
     integer-VALU issue peak -- at the bench's HIP-event kernel time (`frac`)
@@ -155,6 +155,9 @@ def valu_view(prof, kernel_ms=None):
         v['frac'] = v['achieved'] / VALU_PEAK
     if prof.get('duration_ns'):
         v['frac_rocprof'] = n / (prof['duration_ns'] * 1e-9) / VALU_PEAK
+    if instrs:
+        # VALU lane-ops per emulated instruction (the kernel's constant)
+        v['valu_ops_per_instruction'] = n * 64 / instrs
     for k in ('valu_insts_per_wave', 'valu_issue_pct', 'valu_lane_util_pct', 'duration_ns',
               'kernel', 'warnings'):
         if prof.get(k) is not None:
@@ -353,7 +356,7 @@ def leg_ramsey(emu, args, world, rank, stream):
     prof = pmc('ramsey') if args.shots == 10 ** 6 else None         # profiled at the default size only
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'straight_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
-    roof['valu'] = valu_view(prof, roof['kernel_ms'])
+    roof['valu'] = valu_view(prof, roof['kernel_ms'], float(s['n_instr'].astype(np.float64).sum()))
     res = {'value': n * 8 * world * args.steps / dt, 'ms_per_step': ms_step,
            'shots_per_s': n * world * args.steps / dt,
            'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * args.steps / dt,
@@ -408,7 +411,7 @@ def leg_config1(emu, args, world, rank, stream):
     prof = pmc('config1') if args.c1_shots == 10 ** 6 else None
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'straight_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
-    roof['valu'] = valu_view(prof, roof['kernel_ms'])
+    roof['valu'] = valu_view(prof, roof['kernel_ms'], float(s['n_instr'].astype(np.float64).sum()))
     res = {'metric': 'emulated core-shots/s (config 1: the reference\'s golden single-core program, '
                      'test_linear_compile_globalasm core 0)',
            'value': n * world * args.steps / dt, 'unit': 'core-shots/s', 'ms_per_step': ms_step, 'kernel_ms': kernel_ms,
@@ -519,7 +522,7 @@ def leg_active_reset(emu, args, world, rank, stream, lut=False):
     ms_step = dt / args.steps * 1e3
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'branch_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
-    roof['valu'] = valu_view(prof, roof['kernel_ms'])
+    roof['valu'] = valu_view(prof, roof['kernel_ms'], float(s['n_instr'].astype(np.float64).sum()))
     res = {'metric': ('emulated core-shots/s (config 3 via the fproc_lut back end: syndrome LUT over 8 '
                       'measurements + sync, 1.25e6 shots/GPU)') if lut else
                      ('emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
