@@ -169,3 +169,28 @@ def test_config3_cross_core_reads_full_shard(emu):
     ne = s['n_events'].reshape(n, 8)
     assert (ne[flip] == ne[~flip].min() + 2).all()
 
+
+
+def test_config3_eight_shards_equal_one_launch(emu):
+    """config 3 at its stated total, 10^7 shots x 8 cores (BASELINE configs[2]):
+    the eight 1.25 * 10^6-shot shards that eight GPUs would run (global shot
+    offsets, bench launch shape) sum to the histogram of ONE 10^7-shot launch,
+    and that histogram equals oracle_fast's over the same 10^7 shots"""
+    import torch
+    ps = ProgramSet(workloads.config3_active_reset(8))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
+                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, **BENCH_SHAPE)
+    emu.load(ps)
+    n, G = 1250000, 8
+    out = alloc_device_outputs(cfg, n * G, want=('hist',))
+    emu.run_device(cfg, n * G, 0, out)
+    full = out['hist'].clone()
+    total = torch.zeros_like(full)
+    for r in range(G):
+        emu.run_device(cfg, n, r * n, out)
+        total += out['hist']
+    torch.cuda.synchronize()
+    assert torch.equal(total, full)
+    assert int(full.sum().item()) == n * G
+    f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n * G, threads=THREADS, want=('hist',))
+    assert np.array_equal(full.cpu().numpy().view(f['hist'].dtype).reshape(f['hist'].shape), f['hist'])
