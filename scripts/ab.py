@@ -56,6 +56,8 @@ def main():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--no-compare', action='store_true', help='probe builds: outputs may differ')
     ap.add_argument('--flags', default='', help='per-library exec_flags (comma list, e.g. 0,0x40)')
+    ap.add_argument('--outputs', default='summary,events,meas,hist', help='outputs the runs write')
+    ap.add_argument('--lane-order', type=int, default=None, help='override the workload lane order')
     a = ap.parse_args()
     import torch
     from distributed_processor_amd.emulator import Emulator, alloc_device_outputs
@@ -65,7 +67,10 @@ def main():
     emus = [Emulator(0, lib_path=l) for l in libs]
     for e in emus:
         e.load(ps)
-    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))   # one buffer set for all
+    if a.lane_order is not None:
+        cfg.lane_order = a.lane_order
+    want = tuple(x for x in a.outputs.split(',') if x)
+    out = alloc_device_outputs(cfg, n, want=want)   # one buffer set for all
     ref = None
     times = [[] for _ in emus]
     same = True
@@ -76,14 +81,15 @@ def main():
             cfg.exec_flags = flags[i]
             e.kernel_timing(True)
             for _ in range(a.steps):
-                out['hist'].zero_()
+                if 'hist' in out:
+                    out['hist'].zero_()
                 e.run_device(cfg, n, 0, out)
             torch.cuda.synchronize()
             kt = e.kernel_times()
             e.kernel_timing(False)
             if rep:
                 times[i] += kt
-            snap = {k: out[k].clone() for k in ('summary', 'meas', 'hist')}
+            snap = {k: out[k].clone() for k in ('summary', 'meas', 'hist') if k in out}
             if ref is None:
                 ref = snap
             elif not a.no_compare:
