@@ -503,6 +503,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.n_groups = cfg->n_groups; p.shots_per_group = cfg->shots_per_group;
     p.grp_g0 = (uint32_t)((shot_begin / cfg->shots_per_group) % cfg->n_groups);
     p.grp_r0 = (uint32_t)(shot_begin % cfg->shots_per_group);
+    fast_div_init(cfg->shots_per_group, p.spg_div);
+    fast_div_init(cfg->n_groups, p.ng_div);
     p.max_cycles = cfg->max_cycles;
     p.event_cap = cfg->event_cap;           // the overflow flags follow the caps whether or not a buffer is given
     p.trace_cap = cfg->trace_cap;

@@ -96,6 +96,20 @@ __host__ __device__ inline void decode_cmd(const uint32_t w[4], uint32_t u[4])
     }
 }
 
+// Division of a 32-bit n by a run constant d >= 1 without a divide sequence
+// (Hacker's Delight 10-8, unsigned): l = ceil(log2 d), m = floor(2^32 (2^l -
+// d) / d) + 1 < 2^32, q = (t + ((n - t) >> min(l, 1))) >> max(l - 1, 0) with
+// t = mulhi(m, n); exact for every n < 2^32 (tests/test_capi.py checks the
+// formula).  A runtime-divisor u32 division costs ~20 VALU per lane.
+inline void fast_div_init(uint32_t d, uint32_t out[3])
+{
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) l++;
+    out[0] = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    out[1] = l < 1 ? l : 1u;
+    out[2] = l > 1 ? l - 1 : 0u;
+}
+
 struct KParams {
     // programs, as decode_cmd words (16 B per command)
     const uint4 *uops;            // program-major: program p's command i at offsets[p] + i
@@ -126,6 +140,7 @@ struct KParams {
     uint32_t n_lanes, n_shots, C, log2C, n_groups, shots_per_group;
     uint32_t shot_major;          // dpemu_config.lane_order: lane = shot * C + core (else core * n_shots + shot)
     uint32_t grp_g0, grp_r0;      // (shot_begin / spg) % n_groups, shot_begin % spg
+    uint32_t spg_div[3], ng_div[3];   // FastDiv of shots_per_group / n_groups (shot_group)
     uint32_t max_cycles, event_cap, trace_cap, meas_cap;
     uint32_t fproc_mode, meas_elem, meas_latency, sync_latency;
     uint64_t sync_mask, seed;

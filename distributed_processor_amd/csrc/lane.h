@@ -94,14 +94,27 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot, uint32_t lane_in
     return (ballot >> base) & gm;
 }
 
+__device__ __forceinline__ uint32_t fast_div(uint32_t n, const uint32_t d[3])
+{
+    const uint32_t t = __umulhi(d[0], n);
+    return (t + ((n - t) >> d[1])) >> d[2];
+}
+
 // program group of the run's shot sl: (shot / spg) % n_groups from the run's
-// first shot (g0, r0 from the host) in 32-bit arithmetic -- a u64 division
-// would cost ~150 VALU instructions per lane
-__device__ __forceinline__ uint32_t shot_group(const KParams &p, uint32_t sl)
+// first shot (g0, r0 from the host) in 32-bit arithmetic, the divisions by
+// multiply-high with host-made constants (kernels.h fast_div_init); a u64
+// division would cost ~150 VALU instructions per lane, a u32 one ~20
+// (r0 + sl) / spg: the group step of run shot sl past the run's first group
+__device__ __forceinline__ uint32_t group_q(const KParams &p, uint32_t sl)
 {
     const uint64_t num = (uint64_t)p.grp_r0 + sl;
-    const uint32_t q = (num >> 32) ? (uint32_t)(num / p.shots_per_group) : (uint32_t)num / p.shots_per_group;
-    const uint32_t g = p.grp_g0 + q % p.n_groups;       // < 2 n_groups <= 2^32
+    return (num >> 32) ? (uint32_t)(num / p.shots_per_group) : fast_div((uint32_t)num, p.spg_div);
+}
+
+__device__ __forceinline__ uint32_t shot_group(const KParams &p, uint32_t sl)
+{
+    const uint32_t q = group_q(p, sl);
+    const uint32_t g = p.grp_g0 + (q - fast_div(q, p.ng_div) * p.n_groups);   // < 2 n_groups <= 2^32
     return g >= p.n_groups ? g - p.n_groups : g;
 }
 
@@ -109,9 +122,8 @@ __device__ __forceinline__ uint32_t shot_group(const KParams &p, uint32_t sl)
 __device__ __forceinline__ uint32_t group_step(const KParams &p, uint32_t sp, uint32_t sp0)
 {
     if (p.n_groups == 1) return 0;
-    const uint64_t a = (p.shot_begin + sp) / p.shots_per_group;
-    const uint64_t b = (p.shot_begin + sp0) / p.shots_per_group;
-    return (uint32_t)(a - b);
+    // (shot_begin + x) / spg = shot_begin / spg + (r0 + x) / spg
+    return group_q(p, sp) - group_q(p, sp0);
 }
 
 // output lane of (run shot sl, core) (include/dpemu.h): core-major, or
