@@ -153,11 +153,12 @@ __device__ __forceinline__ uint32_t stage_programs(const KParams &p, uint4 *s_pr
     const uint32_t n_shots = p.n_lanes >> p.log2C;
     const uint32_t sp0 = (blockIdx.x * BLOCK) >> p.log2C;
     const uint32_t spl = min(sp0 + (BLOCK >> p.log2C), n_shots) - 1u;
-    const uint32_t g0 = (uint32_t)(((p.shot_begin + sp0) / p.shots_per_group) % p.n_groups);
+    const uint32_t g0 = shot_group(p, sp0);
     const uint32_t nslots = (group_step(p, spl, sp0) + 1u) * C;
     uint32_t len = 0;
     if (tid < nslots) {
-        const uint32_t g = (g0 + tid / C) % p.n_groups;
+        const uint32_t gx = g0 + tid / C;
+        const uint32_t g = gx - fast_div(gx, p.ng_div) * p.n_groups;
         len = p.n_instr[p.prog_table[(uint64_t)g * C + (tid & (C - 1))]] + 1u;   // + guard
     }
     uint32_t total;
@@ -171,7 +172,8 @@ __device__ __forceinline__ uint32_t stage_programs(const KParams &p, uint4 *s_pr
             const uint32_t mid = (lo + hi) >> 1;
             if (s_pref[mid] <= idx) lo = mid; else hi = mid;
         }
-        const uint32_t g = (g0 + lo / C) % p.n_groups;
+        const uint32_t gx = g0 + lo / C;
+        const uint32_t g = gx - fast_div(gx, p.ng_div) * p.n_groups;
         const uint32_t prog = p.prog_table[(uint64_t)g * C + (lo & (C - 1))];
         s_prog[idx] = p.uops[p.offsets[prog] + (idx - s_pref[lo])];
     }
