@@ -103,7 +103,9 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v)
 
 }  // namespace
 
-template <int FEAT>
+// CT: the cores per shot when fixed at compile time (8: the BASELINE
+// configs), so group reductions and lane arithmetic are straight-line; 0 = p.C
+template <int FEAT, int CT>
 __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 {
     constexpr bool FPROC = (FEAT & FEAT_FPROC) != 0;
@@ -130,11 +132,12 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 
     clear_hist_next(p);
     const uint32_t tid = threadIdx.x;
-    const uint32_t C = p.C;
+    const uint32_t C = CT ? (uint32_t)CT : p.C;
+    const uint32_t log2C = CT ? (uint32_t)__builtin_ctz(CT) : p.log2C;
     const uint32_t pos = blockIdx.x * BLOCK + tid;   // thread position; a shot's cores are adjacent
     const bool valid = pos < p.n_lanes;
     const uint32_t core = pos & (C - 1);
-    const uint32_t spos = pos >> p.log2C;
+    const uint32_t spos = pos >> log2C;
     const uint32_t lane = out_lane(p, spos, core);   // output lane index (core-major)
     const uint64_t shot = p.shot_begin + spos;
     const uint32_t wl = tid & 63;
@@ -621,7 +624,8 @@ static hipError_t launch_f(const KParams &p, uint32_t blocks, hipStream_t stream
 {
     const size_t shmem = ((F & FEAT_PROG_LDS) ? (size_t)p.prog_lds_words * sizeof(uint4) : 0) +
                          (p.hist_lds ? HIST_LDS_MAX * sizeof(uint32_t) : 0);
-    hipLaunchKernelGGL(branch_kernel<F>, dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    if (p.C == 8) hipLaunchKernelGGL((branch_kernel<F, 8>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    else hipLaunchKernelGGL((branch_kernel<F, 0>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
     return hipGetLastError();
 }
 

@@ -673,7 +673,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
         else if (macro)
             snprintf(name, sizeof name, "macro_kernel");
         else if (branch)
-            snprintf(name, sizeof name, "branch_kernel<feat=0x%x>", bfeat);
+            snprintf(name, sizeof name, "branch_kernel<feat=0x%x%s>", bfeat, C == 8 ? ",c8" : "");
         else
             snprintf(name, sizeof name, "interp_kernel<feat=0x%x>", feat);
         ctx->last_kernel = name;
