@@ -435,7 +435,7 @@ def leg_dds(emu, args, world, rank, stream):
     """config 5: DDS over the config-4 RB timelines, 8 cores x {qdrv, rdrv}"""
     import torch
     from distributed_processor_amd import _abi, sharding, workloads
-    from distributed_processor_amd.dds import ChannelPlan
+    from distributed_processor_amd.dds import ChannelPlan, SynthesisPipeline
     from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
     ps = ProgramSet(workloads.config4_rb(n_seq=args.dds_seqs, depth=200, n_cores=8))
     emu.load(ps)
@@ -453,9 +453,17 @@ def leg_dds(emu, args, world, rank, stream):
     chans = [(shot0 + q, c, e) for q in range(n) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
     plan = ChannelPlan(ps, cfg, shot0, n, chans, params)
     iq = torch.empty((plan.n_channels, n_samples), dtype=torch.int32, device='cuda')
-    step = lambda: emu.synthesize(plan, ev, n_samples, iq, stream)
-    dt = timed(step, lambda: None, args.steps, args.warmup, world)
-    kernel_ms = kernel_pass(emu, args.steps, step, lambda: None)
+    # a step is one batch's whole synthesis (index + tiles); two batches in
+    # flight on two contexts / streams, so batch k + 1's index kernel runs
+    # beside batch k's tile kernel (dds.SynthesisPipeline)
+    pipe = SynthesisPipeline(torch.cuda.current_device(), depth=2)
+    step = lambda: pipe.synthesize(plan, ev, n_samples)
+    dt = timed(step, pipe.drain, args.steps, args.warmup, world)
+    pipe.drain()
+    pipe.close()
+    serial = lambda: emu.synthesize(plan, ev, n_samples, iq, stream)
+    dt_serial = timed(serial, lambda: None, args.steps, args.warmup, world)
+    kernel_ms = kernel_pass(emu, args.steps, serial, lambda: None)
     samples = plan.n_channels * n_samples
     ms_step = dt / args.steps * 1e3
     prof = pmc('dds') if args.dds_seqs == 128 else None
@@ -463,9 +471,12 @@ def leg_dds(emu, args, world, rank, stream):
     res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
            'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s', 'ms_per_step': ms_step,
            'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
-           'step': 'dds_index_kernel (per-channel event index + tile windows) + dds_tile_kernel; kernel_ms and '
-                   'the roofline hold dds_tile_kernel alone, value and ms_per_step the whole step',
+           'step': 'dds_index_kernel (per-channel event index + tile windows) + dds_tile_kernel per batch, two '
+                   'batches in flight (dds.SynthesisPipeline: two contexts and streams); kernel_ms and the '
+                   'roofline hold dds_tile_kernel alone (one context, one stream), value and ms_per_step the '
+                   'whole step',
            'step_roofline_frac': samples * 4 / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           'serial_ms_per_step': dt_serial / args.steps * 1e3,
            'config': {'workload': 'config5_dds_rb8', 'sequences_per_gpu': n, 'channels_per_gpu': plan.n_channels,
                       'samples_per_channel': n_samples, 'rb_depth': 200},
            'roofline': roof}
