@@ -16,13 +16,15 @@ Sub-objects on the same line, each with its own roofline and CPU baselines:
                   (test_linear_compile_globalasm core 0) at 10^6 shots, beside
                   oracle_rtl (the per-clock stand-in for the Verilator testbench)
   "dds"           config 5: RB timelines (8 cores, depth 200) synthesised to
-                  int16 I/Q on 16 channels per sequence at 16 samples/clk
+                  int16 I/Q on 16 channels per sequence at 16 samples/clk,
+                  --dds-depth batches in flight (dds.SynthesisPipeline)
   "active_reset"  config 3: fproc_meas branching + sync barriers, 1.25*10^6
                   shots per GPU (10^7 over 8 GPUs)
   "lut"           config 3's circuit through the fproc_lut back end: every
                   core waits on a syndrome LUT over the 8 measurements
   "rb"            config 4 at its stated size: 10^5 distinct 2-core depth-200
-                  RB sequences x 10 shots per GPU
+                  RB sequences x 10 shots per GPU, --rb-depth batches in
+                  flight (emulator.RunPipeline)
 
 CPU baselines (rank 0, one GPU): the reference's Verilator/cocotb testbench
 cannot run here or on the box, so each leg reports
@@ -453,10 +455,11 @@ def leg_dds(emu, args, world, rank, stream):
     chans = [(shot0 + q, c, e) for q in range(n) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
     plan = ChannelPlan(ps, cfg, shot0, n, chans, params)
     iq = torch.empty((plan.n_channels, n_samples), dtype=torch.int32, device='cuda')
-    # a step is one batch's whole synthesis (index + tiles); two batches in
-    # flight on two contexts / streams, so batch k + 1's index kernel runs
-    # beside batch k's tile kernel (dds.SynthesisPipeline)
-    pipe = SynthesisPipeline(torch.cuda.current_device(), depth=2)
+    # a step is one batch's whole synthesis (index + tiles); `dds_depth`
+    # batches in flight on as many contexts / streams (dds.SynthesisPipeline):
+    # batch k + 1's index kernel runs beside batch k's tiles, and the tile
+    # kernels of several batches share the GPU
+    pipe = SynthesisPipeline(torch.cuda.current_device(), depth=max(1, args.dds_depth), streams=args.pipe_streams)
     step = lambda: pipe.synthesize(plan, ev, n_samples)
     dt = timed(step, pipe.drain, args.steps, args.warmup, world)
     pipe.drain()
@@ -471,10 +474,11 @@ def leg_dds(emu, args, world, rank, stream):
     res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
            'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s', 'ms_per_step': ms_step,
            'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
-           'step': 'dds_index_kernel (per-channel event index + tile windows) + dds_tile_kernel per batch, two '
-                   'batches in flight (dds.SynthesisPipeline: two contexts and streams); kernel_ms and the '
+           'step': 'dds_index_kernel (per-channel event index + tile windows) + dds_tile_kernel per batch, '
+                   '{} batches in flight (dds.SynthesisPipeline: contexts and streams); kernel_ms and the '
                    'roofline hold dds_tile_kernel alone (one context, one stream), value and ms_per_step the '
-                   'whole step',
+                   'whole step'.format(args.dds_depth),
+           'batches_in_flight': args.dds_depth,
            'step_roofline_frac': samples * 4 / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
            'serial_ms_per_step': dt_serial / args.steps * 1e3,
            'config': {'workload': 'config5_dds_rb8', 'sequences_per_gpu': n, 'channels_per_gpu': plan.n_channels,
@@ -563,7 +567,7 @@ def leg_rb(emu, args, world, rank, stream):
     active lanes per VALU instruction (divergence) from the PMC pass."""
     import torch
     from distributed_processor_amd import _abi, isa, sharding, workloads
-    from distributed_processor_amd.emulator import alloc_device_outputs
+    from distributed_processor_amd.emulator import RunPipeline, alloc_device_outputs
     t0 = time.perf_counter()
     ps = workloads.config4_rb_set(args.rb_seqs, 200)
     gen_s = time.perf_counter() - t0
@@ -577,18 +581,39 @@ def leg_rb(emu, args, world, rank, stream):
                            event_cap=int(strobes.max()) + 1, trace_cap=0, meas_cap=2, meas_latency=64,
                            seed=0x5EED, p1=0.5)
     shot0, n = sharding.weak_shard(args.rb_seqs * args.rb_spg, rank)
-    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
+    want = ('summary', 'events', 'meas', 'hist')
+    steps = max(1, args.steps)
+    # a step is one batch (10^6 shots), `rb_depth` batches in flight on as many
+    # contexts / streams (emulator.RunPipeline): the next batch's waves fill
+    # the CUs this batch's tail of long sequences leaves idle
+    depth = max(1, args.rb_depth)
+    rp = RunPipeline(ps, cfg, n, want=want, depth=depth, device=torch.cuda.current_device(), first=emu,
+                     streams=args.pipe_streams)
+    hp = sharding.HistogramPipeline(rp.outputs[0]['hist'], n_buffers=max(2, depth))
+
+    def step():
+        with torch.cuda.stream(rp.streams[rp.k % depth]):
+            hp.step(lambda h: rp.launch(cfg, n, shot0, hist=h))
+    dt = timed(step, hp.drain, steps, min(args.warmup, 2), world)
+    hp.drain()
+    rp.drain()
+    assert int(hp.result().sum().item()) == n * world
+    s_pipe = rp.outputs[(rp.k - 1) % depth]['summary'].cpu().numpy()
+    rp.close()
+    del rp
+    # the same batches one at a time on one context: the kernel's own time
+    out = alloc_device_outputs(cfg, n, want=want)
     pipe = sharding.HistogramPipeline(out['hist'])
 
     def launch(h):
         out['hist'] = h
         emu.run_device(cfg, n, shot0, out, stream)
-    step = lambda: pipe.step(launch)
-    steps = max(1, args.steps // 4)
-    dt = timed(step, pipe.drain, steps, min(args.warmup, 2), world)
+    serial = lambda: pipe.step(launch)
+    dt_serial = timed(serial, pipe.drain, steps, min(args.warmup, 2), world)
     kernel = emu.last_kernel()
-    kernel_ms, kernel_ms_blk = interp_kernel_ms(emu, cfg, n, shot0, out, stream, steps, step, pipe.drain)
+    kernel_ms, kernel_ms_blk = interp_kernel_ms(emu, cfg, n, shot0, out, stream, steps, serial, pipe.drain)
     summ = out['summary'].cpu().numpy().view(np.uint32)
+    assert np.array_equal(summ, s_pipe.view(np.uint32)), 'config 4: pipelined and serial batches differ'
     s = _abi.unpack_summary(summ)
     assert (s['status'] == _abi.ST_DONE).all(), 'config 4: not every lane reached DONE'
     assert int(pipe.result().sum().item()) == n * world
@@ -609,6 +634,7 @@ def leg_rb(emu, args, world, rank, stream):
     res = {'metric': 'emulated core-shots/s (config 4: 2-qubit RB, 1e5 sequences x depth 200, 10 shots each)',
            'value': n * 2 * world * steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * steps / dt,
            'ms_per_step': ms_step, 'kernel_ms': kernel_ms, 'steps': steps,
+           'serial_ms_per_step': dt_serial / steps * 1e3, 'batches_in_flight': depth,
            'instructions_per_s': instrs * world * steps / dt,
            'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * steps / dt,
            'config': {'workload': 'config4_rb_2core_1e5seq_depth200', 'sequences': args.rb_seqs,
@@ -632,6 +658,8 @@ def main():
     ap.add_argument('--shots', type=int, default=10 ** 6, help='config-2 shots per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
+    ap.add_argument('--dds-depth', type=int, default=8, help='DDS batches in flight (dds.SynthesisPipeline)')
+    ap.add_argument('--rb-depth', type=int, default=2, help='config-4 batches in flight (emulator.RunPipeline)')
     ap.add_argument('--ar-shots', type=int, default=1250000, help='config-3 shots per GPU per step')
     ap.add_argument('--rb-seqs', type=int, default=100000, help='config-4 RB sequences')
     ap.add_argument('--rb-spg', type=int, default=10, help='config-4 shots per sequence')
@@ -651,6 +679,9 @@ def main():
         dist.init_process_group(os.environ.get('DPEMU_BENCH_BACKEND', 'nccl'))
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    # the pipelines' streams, made before any other: each on its own hardware
+    # queue where the process has enough (emulator.RunPipeline)
+    args.pipe_streams = [torch.cuda.Stream() for _ in range(max(1, args.dds_depth, args.rb_depth))]
 
     from distributed_processor_amd.emulator import Emulator
     emu = Emulator(local)

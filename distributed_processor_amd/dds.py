@@ -119,11 +119,13 @@ class SynthesisPipeline:
     waits for every batch.
     """
 
-    def __init__(self, device: int = 0, depth: int = 2, lib_path: Optional[str] = None):
+    def __init__(self, device: int = 0, depth: int = 2, lib_path: Optional[str] = None, streams=None):
         import torch
         from .emulator import Emulator
         if depth < 1:
             raise ValueError('depth must be >= 1')
+        if streams is not None and len(streams) < depth:
+            raise ValueError('need {} streams, got {}'.format(depth, len(streams)))
         self.device = torch.device('cuda', device)
         self.emus = []
         try:
@@ -132,7 +134,10 @@ class SynthesisPipeline:
         except Exception:
             self.close()
             raise
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(depth)]
+        # streams: the caller's (e.g. created once at start-up, each on its own
+        # hardware queue: streams that share a queue run their kernels in turn)
+        self.streams = list(streams[:depth]) if streams is not None else \
+            [torch.cuda.Stream(device=self.device) for _ in range(depth)]
         self.iq = [None] * depth
         self.k = 0
 
@@ -161,6 +166,7 @@ class SynthesisPipeline:
         for e in self.emus:
             e.close()
         self.emus = []
+        self.iq = [None] * len(self.iq) if hasattr(self, 'iq') else []
 
 
 def split_iq(iq_u32: np.ndarray):

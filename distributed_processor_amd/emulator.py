@@ -309,6 +309,83 @@ class Emulator:
         return iq
 
 
+class RunPipeline:
+    """Successive device runs with ``depth`` batches in flight.
+
+    One context runs its calls in call order (dpemu.h), so batch k + 1's
+    launch cannot start before batch k's kernel has drained.  A launch whose
+    waves run programs of different lengths (config 4: each wave holds ~7
+    RB sequences) has a long tail in which most of the GPU idles; the
+    pipeline holds ``depth`` contexts with the same programs loaded, one
+    stream and one output set each, and sends batch k to context k % depth,
+    so batch k + 1's waves fill the CUs batch k's tail leaves idle (config 4:
+    3.65 -> 2.86 ms per batch at depth 2, ``profiles/r03_pipe_probe.json``).
+
+    ``streams``: the caller's streams (default: new ones from torch's pool).
+    Streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, 4 by
+    default) share queues, and kernels on one queue run in turn: a pipeline
+    whose streams were created after many others measured no overlap at all
+    in bench.py (3.60 ms per batch), the same on the first streams of the
+    process 2.79 -- so the bench makes its pipeline streams first.
+
+    ``launch(cfg, n_shots, shot_begin, hist=None)`` makes the slot's stream
+    wait for the caller's current stream, runs the batch there (into
+    ``hist`` instead of the slot's own histogram when given) and returns
+    (outputs, stream); the outputs are valid on that stream and are
+    overwritten by the launch ``depth`` batches later.  ``drain()`` waits
+    for every batch.  Memory: ``depth`` output sets and program images.
+    """
+
+    def __init__(self, programs, cfg: _abi.Config, n_shots: int, want=('summary', 'events', 'meas', 'hist'),
+                 depth: int = 2, device: int = 0, first: Optional['Emulator'] = None, streams=None):
+        import torch
+        if depth < 1:
+            raise ValueError('depth must be >= 1')
+        if streams is not None and len(streams) < depth:
+            raise ValueError('need {} streams, got {}'.format(depth, len(streams)))
+        self.emus, self._own = [], []
+        try:
+            for j in range(depth):
+                if j == 0 and first is not None:
+                    e = first                                  # the caller's context, programs loaded
+                else:
+                    e = Emulator(device)
+                    self._own.append(e)
+                    e.load(programs)
+                self.emus.append(e)
+        except Exception:
+            self.close()
+            raise
+        self.device = torch.device('cuda', device)
+        # streams: the caller's (e.g. created once at start-up, each on its own
+        # hardware queue: streams that share a queue run their kernels in turn)
+        self.streams = list(streams[:depth]) if streams is not None else \
+            [torch.cuda.Stream(device=self.device) for _ in range(depth)]
+        self.outputs = [alloc_device_outputs(cfg, n_shots, want=want, device=self.device) for _ in range(depth)]
+        self.k = 0
+
+    def launch(self, cfg: _abi.Config, n_shots: int, shot_begin: int, hist=None):
+        import torch
+        j = self.k % len(self.emus)
+        s = self.streams[j]
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        out = self.outputs[j]
+        if hist is not None:
+            out = dict(out, hist=hist)
+        self.emus[j].run_device(cfg, n_shots, shot_begin, out, s)
+        self.k += 1
+        return out, s
+
+    def drain(self):
+        for s in self.streams:
+            s.synchronize()
+
+    def close(self):
+        for e in self._own:
+            e.close()
+        self._own, self.emus = [], []
+
+
 def device_output_specs(cfg: _abi.Config, n_shots: int):
     """{name: (shape, torch dtype)} of the dpemu_outputs arrays of a run"""
     import torch

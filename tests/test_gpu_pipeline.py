@@ -232,3 +232,47 @@ def test_load_programs_bounds_in_commands(short):
         assert (rc == 0) == (short == 0), (short, rc)
         if rc:
             assert rc == -22 and b'run past' in L.dpemu_last_error(emu._h)
+
+
+@pytest.mark.parametrize('depth', [1, 2, 3])
+def test_run_pipeline_batches_in_flight(depth):
+    """emulator.RunPipeline (bench.py's config-4 step: batches on `depth`
+    contexts and streams) with the histogram exchange pipeline: each batch's
+    outputs, read on its own stream before the slot is reused, and its
+    histogram equal oracle_fast over that batch's shots"""
+    import torch
+    from distributed_processor_amd.emulator import RunPipeline
+    ps = workloads.config4_rb_set(24, 20)
+    cfg = _abi.make_config(2, n_groups=ps.n_groups, shots_per_group=3, max_cycles=1 << 20, event_cap=80,
+                           meas_cap=2, meas_latency=64, seed=0x5EED, p1=0.5)
+    n, batches = 30, 7
+    want = ('summary', 'events', 'meas', 'hist')
+    with Emulator(0) as emu:
+        emu.load(ps)
+        rp = RunPipeline(ps, cfg, n, want=want, depth=depth, first=emu)
+        hp = sharding.HistogramPipeline(rp.outputs[0]['hist'], n_buffers=max(2, depth))
+        got = []
+        try:
+            for b in range(batches):
+                with torch.cuda.stream(rp.streams[rp.k % depth]):
+                    h = hp.step(lambda t, b=b: rp.launch(cfg, n, b * n, hist=t))
+                    out = rp.outputs[(rp.k - 1) % depth]
+                    got.append({k: (h if k == 'hist' else out[k]).clone() for k in want})
+            hp.drain()
+            rp.drain()
+            assert rp.k == batches
+        finally:
+            rp.close()
+    for b, g in enumerate(got):
+        ref = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, b * n, n, want=want)
+        s = _abi.unpack_summary(ref['summary'])
+        # the records a batch wrote (slots past a lane's count keep an earlier
+        # batch's records: the output contract leaves them undefined)
+        valid = {'events': np.minimum(s['n_events'], cfg.event_cap), 'meas': np.minimum(s['n_meas'], cfg.meas_cap)}
+        for k in want:
+            a = g[k].cpu().numpy().view(ref[k].dtype).reshape(ref[k].shape)
+            r = ref[k]
+            if k in valid:
+                m = np.arange(r.shape[0])[:, None] < valid[k][None, :]
+                a, r = a[m], r[m]
+            assert np.array_equal(a, r), 'depth {} batch {}: {} differs'.format(depth, b, k)
