@@ -470,7 +470,10 @@ def leg_dds(emu, args, world, rank, stream):
     samples = plan.n_channels * n_samples
     ms_step = dt / args.steps * 1e3
     prof = pmc('dds') if args.dds_seqs == 128 else None
-    roof = hbm_roofline(samples * 4, kernel_ms, ms_step, 'dpemu::dds_tile_kernel', prof, 'dds_tile_kernel')
+    # the kernel's own roofline: capped at the one-context step, not at the
+    # pipelined step (batches overlap, so that is shorter than one kernel)
+    roof = hbm_roofline(samples * 4, kernel_ms, dt_serial / args.steps * 1e3, 'dpemu::dds_tile_kernel', prof,
+                        'dds_tile_kernel')
     res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
            'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s', 'ms_per_step': ms_step,
            'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
@@ -619,10 +622,11 @@ def leg_rb(emu, args, world, rank, stream):
     assert int(pipe.result().sum().item()) == n * world
     instrs = float(s['n_instr'].astype(np.float64).sum())
     ms_step = dt / steps * 1e3
-    k_ms = min(kernel_ms, ms_step)
+    serial_ms = dt_serial / steps * 1e3
+    k_ms = min(kernel_ms, serial_ms)            # (capped at the one-context step: batches in flight overlap)
     prof = pmc('rb') if (args.rb_seqs, args.rb_spg) == (100000, 10) else None
     alg = float(bytes_per_lane(summ, cfg).sum())
-    hbm = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, kernel.split('<')[0])
+    hbm = hbm_roofline(alg, kernel_ms, serial_ms, 'dpemu::' + kernel, prof, kernel.split('<')[0])
     hbm['kernel_ms_block'] = kernel_ms_blk
     valu = valu_view(prof, k_ms)
     if valu:

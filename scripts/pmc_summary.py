@@ -7,7 +7,10 @@ other subdirectory's PMC pass (counter_collection.csv), groups dispatches by (ke
 keeps each kernel's most frequent shape (the bench's timed launches) and
 writes <dest>/<tag>_<kernel>_pmc.json with per-launch means:
 
-* duration_ns     kernel-trace average over those dispatches
+* duration_ns     kernel-trace average over those dispatches that overlap no
+                  other dispatch (the bench's pipelines run batches
+                  concurrently; a kernel sharing the GPU takes longer);
+                  dispatches_overlapped counts the ones left out
 * write_bytes     WRITE_SIZE x 1024 (exact for 16-B-per-lane streaming stores)
 * fetch_bytes     FETCH_SIZE x 1024 x 2: on gfx950 FETCH_SIZE reads 1/2 of a
                   wide coalesced read (MI355X_MICROARCH.md, HBM section)
@@ -82,18 +85,33 @@ def main():
     os.makedirs(dest, exist_ok=True)
     # kernel trace: per (kernel, grid) durations
     dur = collections.defaultdict(list)
+    n_over = collections.Counter()
     names = {}
     tdir = 'prof_trace' if os.path.isdir(os.path.join(root, 'prof_trace')) else 'trace'
+    spans = []
     for r in rows(os.path.join(root, tdir, '**', '*kernel_trace.csv')):
         grid = int(r['Grid_Size']) if r.get('Grid_Size') else \
             int(r['Grid_Size_X']) * int(r.get('Grid_Size_Y') or 1) * int(r.get('Grid_Size_Z') or 1)
-        k = which(r['Kernel_Name'], grid)
-        if k:
-            dur[(k, grid)].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
-            names[(k, grid)] = r['Kernel_Name']
+        spans.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), which(r['Kernel_Name'], grid), grid,
+                      r['Kernel_Name']))
+    spans.sort()
+    end_before = -1                                   # latest end of any earlier-starting dispatch
+    for i, (t0, t1, k, grid, name) in enumerate(spans):
+        alone = end_before <= t0 and (i + 1 == len(spans) or spans[i + 1][0] >= t1)
+        end_before = max(end_before, t1)
+        if not k:
+            continue
+        names[(k, grid)] = name
+        if alone:
+            dur[(k, grid)].append(t1 - t0)
+        else:
+            n_over[(k, grid)] += 1
+    for key in n_over:
+        dur.setdefault(key, [])
     shape = {}
     for (k, grid), v in dur.items():
-        if k not in shape or len(v) > len(dur[(k, shape[k])]):
+        nk = len(v) + n_over[(k, grid)]
+        if k not in shape or nk > len(dur[(k, shape[k])]) + n_over[(k, shape[k])]:
             shape[k] = grid
     peak, cpi = valu_peak()
     # counters: per (kernel, grid) -> {(pass dir, dispatch): {counter: sum}}
@@ -108,8 +126,9 @@ def main():
                 continue
             ctr[(k, grid)][(d, r['Dispatch_Id'])][r['Counter_Name']] += float(r['Counter_Value'])
     for k, grid in shape.items():
-        res = {'kernel': names[(k, grid)], 'grid_size': grid, 'dispatches_traced': len(dur[(k, grid)]),
-               'duration_ns': sum(dur[(k, grid)]) / len(dur[(k, grid)])}
+        d = dur[(k, grid)]
+        res = {'kernel': names[(k, grid)], 'grid_size': grid, 'dispatches_traced': len(d),
+               'dispatches_overlapped': n_over[(k, grid)], 'duration_ns': sum(d) / len(d) if d else None}
         disp = ctr.get((k, grid), {})
         names_c = sorted({c for v in disp.values() for c in v})
         for name in names_c:
@@ -137,7 +156,8 @@ def main():
             res['fetch_bytes'] = res['FETCH_SIZE'] * 1024 * 2
         if 'write_bytes' in res and 'fetch_bytes' in res:
             res['hbm_bytes_per_launch'] = res['write_bytes'] + res['fetch_bytes']
-            res['hbm_GBps_at_traced_duration'] = res['hbm_bytes_per_launch'] / res['duration_ns']
+            if res.get('duration_ns'):
+                res['hbm_GBps_at_traced_duration'] = res['hbm_bytes_per_launch'] / res['duration_ns']
         if 'SQ_THREAD_CYCLES_VALU' in res and 'SQ_ACTIVE_INST_VALU' in res and res['SQ_ACTIVE_INST_VALU']:
             # active lanes per VALU instruction (divergence): thread-cycles / (quad-cycles * 64)
             res['valu_lane_util_pct'] = 100.0 * res['SQ_THREAD_CYCLES_VALU'] / (res['SQ_ACTIVE_INST_VALU'] * 64)
