@@ -82,6 +82,15 @@ def host_cores():
     return use, {'nproc': aff, 'os_cpu_count': os.cpu_count(), 'omp_num_threads': omp}
 
 
+def share_note(threads, info):
+    """what the CPU baseline's thread count is a share of (BASELINE.md:46 asks
+    for every host core; the harness grants a one-GPU job OMP_NUM_THREADS of
+    the machine's nproc, and the baseline stays inside that share)"""
+    return ('{} threads = the job\'s CPU share (OMP_NUM_THREADS={}) of the {} CPUs this process sees; any GPU/CPU '
+            'ratio taken from `value` compares against {}/{} of the host, not all of it'.format(
+                threads, info.get('omp_num_threads'), info.get('nproc'), threads, info.get('nproc')))
+
+
 def median_rate(run, units_per_n, n0, target_s=0.8, reps=5):
     """one warm-up / calibration run of n0, then `reps` timed runs of a fixed
     n sized to ~target_s each; returns (median units/s, n, [seconds])"""
@@ -109,6 +118,7 @@ def cpu_baselines(ps, cfg, horizon, what):
     r1_rate, r1_n, r1_t = median_rate(rtl(1), C, 20)
     ra_rate, ra_n, ra_t = median_rate(rtl(threads), C, 20 * threads)
     return dict(value=f_rate, unit='core-shots/s', cores=threads, kind='port', **info,
+                per_core=f_rate / threads, share_note=share_note(threads, info),
                 method='median of 5 timed runs of a fixed sample after one warm-up run',
                 sample='{}: {} shots x {} cores per oracle_fast run (event-driven C restatement, OpenMP over '
                        'shots, {} threads)'.format(what, f_n, C, threads),
@@ -315,6 +325,30 @@ def fill_gbps(device='cuda'):
     return gbs
 
 
+def _sig(x, n=4):
+    return None if x is None else float('{:.{}g}'.format(x, n))
+
+
+def compact_leg(res):
+    """the few numbers of a leg that must survive a truncated record (the
+    driver keeps the last 2,000 characters of stdout): value, step and kernel
+    ms, the graded roofline's bound and fraction, and for a pipelined leg the
+    whole step's fraction / the one-context step"""
+    roof = res.get('roofline') or {}
+    c = {'value': _sig(res['value']), 'ms_per_step': _sig(res['ms_per_step']),
+         'kernel_ms': _sig(roof.get('kernel_ms', res.get('kernel_ms'))), 'bound': roof.get('bound'),
+         'frac': _sig(roof.get('frac'), 3)}
+    if roof.get('bound') == 'valu' and roof.get('hbm'):
+        c['hbm_frac'] = _sig(roof['hbm'].get('frac'), 3)
+    if 'step_roofline_frac' in res:
+        c['step_frac'] = _sig(res['step_roofline_frac'], 3)
+    if 'serial_ms_per_step' in res:
+        c['serial_ms'] = _sig(res['serial_ms_per_step'])
+    if 'cpu_baseline' in res:
+        c['cpu'] = _sig(res['cpu_baseline']['value'], 3)
+    return c
+
+
 # ---------------------------------------------------------------------------- legs
 def leg_ramsey(emu, args, world, rank, stream):
     """config 2 (the headline line)"""
@@ -460,13 +494,22 @@ def leg_dds(emu, args, world, rank, stream):
     # batch k + 1's index kernel runs beside batch k's tiles, and the tile
     # kernels of several batches share the GPU
     pipe = SynthesisPipeline(torch.cuda.current_device(), depth=max(1, args.dds_depth), streams=args.pipe_streams)
-    step = lambda: pipe.synthesize(plan, ev, n_samples)
+    last = {}
+
+    def step():
+        last['iq'] = pipe.synthesize(plan, ev, n_samples)[0]
     dt = timed(step, pipe.drain, args.steps, args.warmup, world)
     pipe.drain()
+    iq_pipe = last['iq'].clone()
     pipe.close()
     serial = lambda: emu.synthesize(plan, ev, n_samples, iq, stream)
     dt_serial = timed(serial, lambda: None, args.steps, args.warmup, world)
     kernel_ms = kernel_pass(emu, args.steps, serial, lambda: None)
+    torch.cuda.synchronize()
+    # the pipelined batches and the serial ones must produce the same I/Q (a
+    # cross-stream ordering bug would still yield a throughput number)
+    assert torch.equal(iq_pipe, iq), 'config 5: pipelined and serial I/Q differ'
+    del iq_pipe
     samples = plan.n_channels * n_samples
     ms_step = dt / args.steps * 1e3
     prof = pmc('dds') if args.dds_seqs == 128 else None
@@ -497,6 +540,7 @@ def leg_dds(emu, args, world, rank, stream):
                        plan.event_cap, threads)
         rate, k, times = median_rate(run, n_samples, max(threads, 16))
         res['cpu_baseline'] = dict(value=rate / 1e9, unit='GSamples/s', cores=threads, kind='port', **info,
+                                   per_core=rate / 1e9 / threads, share_note=share_note(threads, info),
                                    method='median of 5 timed runs of a fixed sample after one warm-up run',
                                    sample='{} channels x {} samples of the config-5 timelines per run, oracle_dds '
                                           '(C restatement, OpenMP over channels)'.format(k, n_samples))
@@ -717,6 +761,12 @@ def main():
     for name in [x for x in args.legs.split(',') if x]:
         result[name] = fns[name](emu, args, world, rank, stream)
     result['box'] = {'fill_GBps': fill_gbps(), 'device': torch.cuda.get_device_name(local)}
+    # LAST on the line: one compact record per leg, so that a reader who keeps
+    # only the tail of the line (the driver stores ~8 KB) still has every
+    # leg's number and roofline fraction
+    result['legs'] = {'config2': compact_leg(main_leg)}
+    for name in [x for x in args.legs.split(',') if x]:
+        result['legs'][name] = compact_leg(result[name])
     if rank == 0:
         print(json.dumps(result), flush=True)
     emu.close()

@@ -36,6 +36,12 @@ def load_library(path=LIB_PATH):
     except ImportError:
         pass
     L = C.CDLL(path)
+    # an older build lacks later entry points: name them instead of letting
+    # ctypes raise a bare AttributeError on the first argtypes assignment
+    missing = [s for s in EXPORTS if not hasattr(L, s)]
+    if missing:
+        raise DpemuError('{} lacks {} (a build older than this binding); rebuild it with '
+                         '__graft_entry__.build()'.format(path, ', '.join(missing)))
     vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
     L.dpemu_abi_version.restype = C.c_int
     L.dpemu_struct_sizes.argtypes = [vp]

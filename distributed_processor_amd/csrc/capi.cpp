@@ -18,8 +18,24 @@
 #include <vector>
 
 #include "kernels.h"
+#include "lds_grants.h"
 
 using namespace dpemu;
+
+namespace dpemu {
+static LdsGrants g_lds_grants;     // the process's dynamic-LDS opt-ins, per (device, kernel)
+
+hipError_t opt_in_dynamic_lds(const void *fn, size_t bytes)
+{
+    if (bytes <= LdsGrants::DEFAULT_LIMIT) return hipSuccess;
+    int dev = 0;
+    const hipError_t de = hipGetDevice(&dev);
+    if (de != hipSuccess) return de;
+    return (hipError_t)g_lds_grants.ensure(dev, fn, bytes, [&] {
+        return (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    });
+}
+}  // namespace dpemu
 
 struct dpemu_ctx {
     int device = 0;
@@ -29,6 +45,7 @@ struct dpemu_ctx {
     uint4 *d_uops_t = nullptr;              // command-major copy (KParams::fetch), or null
     uint4 *d_macro = nullptr;               // macro image of branch-free ALU programs (macro.hip), or null
     uint32_t *d_moff = nullptr;             // its per-program offsets (in macros)
+    uint32_t *d_mchunk = nullptr, *d_mcoff = nullptr;   // lean chunks (mark_lean_chunks) and their offsets
     uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
     uint32_t n_programs = 0, n_groups = 0, C = 0;
     bool has_fproc = false, has_sync = false, straight = false, linear = false, reg_writes = false;
@@ -233,12 +250,44 @@ static bool mark_simple_macros(std::vector<uint32_t> &mac, const std::vector<uin
     return addid;
 }
 
+// Per (program, chunk of MACRO_CHUNK macros as macro_staged_kernel stages
+// them: macros [c CH, (c + 1) CH) of the program, the terminal macro
+// repeating past its end): the largest pulse-slot cmd_time when every macro
+// of the chunk is MACRO_SIMPLE and none is the terminal one (0 when no slot
+// holds a pulse), else MACRO_CHUNK_MIXED.  A wave whose running lanes all
+// hold such a chunk and can reach no max_cycles stop before its end runs the
+// chunk's macros with no per-macro test (macro.hip lean_chunk_ok).
+// chunk_off[p]: program p's first entry.
+static void mark_lean_chunks(const std::vector<uint32_t> &mac, const std::vector<uint32_t> &moff,
+                             std::vector<uint32_t> &chunk, std::vector<uint32_t> &chunk_off)
+{
+    const size_t n_prog = moff.size() - 1;
+    chunk_off.resize(n_prog);
+    chunk.clear();
+    for (size_t pr = 0; pr < n_prog; pr++) {
+        chunk_off[pr] = (uint32_t)chunk.size();
+        const uint32_t nm = moff[pr + 1] - moff[pr];              // macros, the terminal one included
+        for (uint32_t c = 0; c * MACRO_CHUNK < nm; c++) {
+            uint32_t v = 0;
+            if ((c + 1) * MACRO_CHUNK >= nm) v = MACRO_CHUNK_MIXED;  // reaches the terminal macro
+            for (uint32_t j = 0; j < MACRO_CHUNK && v != MACRO_CHUNK_MIXED; j++) {
+                const uint32_t *m = &mac[8ull * (moff[pr] + c * MACRO_CHUNK + j)];
+                if (!(m[7] & MACRO_SIMPLE)) v = MACRO_CHUNK_MIXED;
+                else if (!(m[7] >> 31)) v = std::max(v, m[4]);        // a pulse slot: its cmd_time
+            }
+            chunk.push_back(v);
+        }
+    }
+}
+
 static void free_programs(dpemu_ctx *ctx)
 {
     for (void *q : {(void *)ctx->d_uops, (void *)ctx->d_uops_t, (void *)ctx->d_macro, (void *)ctx->d_moff,
+                    (void *)ctx->d_mchunk, (void *)ctx->d_mcoff,
                     (void *)ctx->d_offsets, (void *)ctx->d_ninstr, (void *)ctx->d_table})
         (void)hipFree(q);
     ctx->d_uops = ctx->d_uops_t = ctx->d_macro = nullptr;
+    ctx->d_mchunk = ctx->d_mcoff = nullptr;
     ctx->d_moff = ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
     ctx->n_programs = 0;
 }
@@ -401,6 +450,12 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, 
         HIPCHK(ctx, hipMemcpy(ctx->d_macro, mac.data(), mac.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(ctx, hipMalloc(&ctx->d_moff, moff.size() * 4));
         HIPCHK(ctx, hipMemcpy(ctx->d_moff, moff.data(), moff.size() * 4, hipMemcpyHostToDevice));
+        std::vector<uint32_t> mchunk, mcoff;
+        mark_lean_chunks(mac, moff, mchunk, mcoff);
+        HIPCHK(ctx, hipMalloc(&ctx->d_mchunk, mchunk.size() * 4));
+        HIPCHK(ctx, hipMemcpy(ctx->d_mchunk, mchunk.data(), mchunk.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMalloc(&ctx->d_mcoff, mcoff.size() * 4));
+        HIPCHK(ctx, hipMemcpy(ctx->d_mcoff, mcoff.data(), mcoff.size() * 4, hipMemcpyHostToDevice));
     }
     HIPCHK(ctx, hipMemcpy(ctx->d_offsets, goff.data(), n_programs * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->d_ninstr, n_instr, n_programs * 4, hipMemcpyHostToDevice));
@@ -482,6 +537,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.offsets = ctx->d_offsets; p.n_instr = ctx->d_ninstr; p.prog_table = ctx->d_table;
     p.max_len = ctx->max_len;
     p.macros = ctx->d_macro; p.macro_off = ctx->d_moff;
+    p.macro_chunk = ctx->d_mchunk; p.macro_coff = ctx->d_mcoff;
     p.reg_map = ctx->reg_map; p.reg_inv = ctx->reg_inv; p.reg_used = ctx->reg_used;
     p.macro_rs = ctx->macro_rs;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;

@@ -595,15 +595,6 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
         tile_sweep(p, L, d, stripe, stripes, n_t, quad, xs, 0u, xr, 0u);
 }
 
-// dynamic LDS above 64 KiB needs an opt-in per kernel, raised as requests grow
-static hipError_t opt_in_lds(const void *fn, uint32_t bytes, uint32_t *granted)
-{
-    if (bytes <= 64 * 1024 || bytes <= *granted) return hipSuccess;
-    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e == hipSuccess) *granted = bytes;
-    return e;
-}
-
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
@@ -616,8 +607,7 @@ hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
     const uint32_t lds = dds_lds_bytes(p.rec_lds, DDS_TILES_PER_STRIPE, p.env_lds, p.freq_lds);
-    static uint32_t granted = 0;
-    const hipError_t e = opt_in_lds(reinterpret_cast<const void *>(dds_tile_kernel), lds, &granted);
+    const hipError_t e = opt_in_dynamic_lds(reinterpret_cast<const void *>(dds_tile_kernel), lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(dds_tile_kernel, dim3(p.stripes, p.n_channels), dim3(BLOCK), lds, stream, p);
     return hipGetLastError();

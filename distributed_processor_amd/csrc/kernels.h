@@ -122,6 +122,10 @@ struct KParams {
     uint32_t max_len;             // longest program; the command-major image's guard row
     const uint4 *macros;          // macro.hip image: 2 x uint4 per macro (capi.cpp build_macros)
     const uint32_t *macro_off;    // [n_programs + 1]: program p's macros [macro_off[p], macro_off[p + 1])
+    const uint32_t *macro_chunk;  // per (program, MACRO_CHUNK-macro chunk): the largest pulse cmd_time of a
+                                  //   chunk whose macros are all MACRO_SIMPLE (0: no pulse), else
+                                  //   MACRO_CHUNK_MIXED (capi.cpp mark_lean_chunks)
+    const uint32_t *macro_coff;   // [n_programs]: program p's chunk c at macro_chunk[macro_coff[p] + c]
     uint64_t reg_map;             // macro image register slots: reg_file register r is slot (reg_map >> 4 r) & 15
     uint64_t reg_inv;             //   for r in the reg_used mask (others are never named: they read 0);
     uint32_t reg_used;            //   slot s holds register (reg_inv >> 4 s) & 15 (trace addresses)
@@ -167,6 +171,9 @@ hipError_t launch_interp(const KParams &p, int feat, hipStream_t stream);
 enum { STRAIGHT_ROWS = 0, STRAIGHT_PROG = 1, STRAIGHT_LDS = 2 };
 constexpr uint32_t STRAIGHT_LDS_MAX = 9216;   // commands (144 KiB) of dynamic LDS per workgroup
 hipError_t launch_straight(const KParams &p, int src, int fb, hipStream_t stream);
+// dynamic LDS above 64 KiB for kernel `fn` on the current device: the opt-in,
+// recorded per (device, kernel) under a lock (capi.cpp, lds_grants.h)
+hipError_t opt_in_dynamic_lds(const void *fn, size_t bytes);
 // programs with jumps / fproc_meas / sync (branch.hip): FEAT_FPROC | FEAT_SYNC | FEAT_REGS | FEAT_PROG_LDS bits of feat
 hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream);
 // branch-free programs with reg_alu / inc_qclk (macro.hip): macro_staged_kernel
@@ -190,6 +197,11 @@ constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no comm
 // PULSE_WRITE_TRIG or absent -- the shape macro_staged_kernel retires on its
 // lean path (runtime conditions permitting)
 constexpr uint32_t MACRO_SIMPLE = 0x40000000u;
+constexpr uint32_t MACRO_CHUNK_MIXED = 0xFFFFFFFFu;   // macro_chunk: not every macro MACRO_SIMPLE
+#ifndef DPEMU_MACRO_CHUNK_LEAN
+#define DPEMU_MACRO_CHUNK_LEAN 1
+#endif
+constexpr bool MACRO_CHUNK_LEAN = DPEMU_MACRO_CHUNK_LEAN;   // one wave test per chunk (A/B: -DDPEMU_MACRO_CHUNK_LEAN=0)
 
 // ---- DDS ------------------------------------------------------------------
 // Two launches per synthesis (dds.hip): dds_index_kernel compacts each

@@ -596,6 +596,23 @@ struct MacroLane {
     {
         return !tr_on && !__ballot(st == 0u && (!(u.w & MACRO_SIMPLE) || t + 8u > p.max_cycles));
     }
+    // ---- the lean CHUNK (NR == 2): one wave-uniform test for MACRO_CHUNK
+    // macros.  `info` is the lane's chunk marker (capi.cpp mark_lean_chunks):
+    // every macro MACRO_SIMPLE, the largest pulse cmd_time Tmax.  Within the
+    // chunk qa is fixed (no inc_qclk), an ALU slot adds 4 cycles and a pulse
+    // that does not stop the lane ends at Tc + 3 with Tc = its cmd_time +
+    // qa_t - qa_q >= its decode, so by induction macro m starts at or before
+    // B + 11 m, B = max(t, Tmax + qa_t - qa_q): B + 11 (CH - 1) + 8 <=
+    // max_cycles keeps every macro's decodes inside max_cycles -- lean_ok at
+    // every macro, without testing it.  (A late pulse stops its lane, which
+    // the lean pulse slot handles.)
+    __device__ __forceinline__ bool lean_chunk_ok(uint32_t info) const
+    {
+        const uint64_t tc = (uint64_t)info + qa_t;                       // Tmax's cycle + qa_q
+        const uint64_t b = max((uint64_t)t, tc > qa_q ? tc - qa_q + 3u : 0ull);
+        const bool ok = info != MACRO_CHUNK_MIXED && b + 12ull * MACRO_CHUNK + 8u <= p.max_cycles;
+        return !tr_on && !__ballot(st == 0u && !ok);
+    }
     static __device__ __forceinline__ uint32_t bmask(uint32_t v, int b)     // bit b of v as 0 / ~0
     {
         return (uint32_t)(((int32_t)(v << (31 - b))) >> 31);
@@ -668,9 +685,14 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
     constexpr uint32_t PIECES = NS * CH * 2;          // 16-B pieces of a chunk
     constexpr uint32_t PL = PIECES / 64;              // pieces per lane
     static_assert(PIECES % 64 == 0 && (CH & (CH - 1)) == 0, "whole pieces per lane, power-of-two chunk");
+    // the staging loop maps lane wl to macro (wl >> 1) & (CH - 1) in every load
+    // round, which is the round's macro only while a round covers <= CH macros
+    static_assert(CH <= 32, "staging assumes at most 32 macros per chunk");
     __shared__ uint4 s_chunk0[NW][PIECES];            // [wave][slot][macro][2], double-buffered
     __shared__ uint4 s_chunk1[NW][PIECES];
     __shared__ uint32_t s_smb[NW][NS], s_sml[NW][NS]; // slot -> first / terminal macro
+    __shared__ uint32_t s_scb[NW][NS];                // slot -> its first lean-chunk marker (macro_coff)
+    __shared__ uint32_t s_info0[NW][NS], s_info1[NW][NS];   // the staged chunk's markers, per slot
     __shared__ uint32_t s_regs[NR == 16 ? 16 : 1][NR == 16 ? BLOCK : 1];
     __shared__ uint32_t s_key[BLOCK];
     extern __shared__ uint32_t s_hist[];              // HIST_LDS_MAX words when p.hist_lds (dynamic)
@@ -682,12 +704,13 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
     const bool valid = sl < p.n_shots;
     const uint32_t lane = out_lane(p, sl, core);
 
-    uint32_t prog = 0, mb = 0, ml = 0;
+    uint32_t prog = 0, mb = 0, ml = 0, cb = 0;
     if (valid) {
         const uint32_t grp = shot_group(p, sl);
         prog = p.prog_table[(uint64_t)grp * C + core];
         mb = p.macro_off[prog];
         ml = p.macro_off[prog + 1] - 1u;
+        if constexpr (NR == 2 && MACRO_CHUNK_LEAN) cb = p.macro_coff[prog];
     }
     if (p.hist_lds) {
         for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
@@ -711,6 +734,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
             if (wl == 0 && nslots < NS) {
                 s_smb[wv][nslots] = __builtin_amdgcn_readlane(mb, ld);
                 s_sml[wv][nslots] = __builtin_amdgcn_readlane(ml, ld);
+                s_scb[wv][nslots] = __builtin_amdgcn_readlane(cb, ld);
             }
             rem &= ~__ballot(mine);
             nslots++;
@@ -734,7 +758,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
     // Only the lanes of the wave's nslots slots load (s_smb / s_sml of the
     // others were never written -- all of them in a wave with no valid lane);
     // the other pieces of the LDS image are never read.
-    auto stage = [&](uint32_t c, uint4 *buf) __attribute__((always_inline)) {
+    // (NR == 2: lane sr < nslots also fetches slot sr's lean-chunk marker of
+    // chunk c, clamped to the program's last chunk, into info[sr])
+    auto stage = [&](uint32_t c, uint4 *buf, uint32_t *info) __attribute__((always_inline)) {
         const uint32_t m = c * CH + pj;
 #pragma unroll
         for (uint32_t r = 0; r < PL; r++) {
@@ -742,6 +768,12 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
             if (sr < nslots) {
                 const uint32_t b0 = s_smb[wv][sr], l0 = s_sml[wv][sr];
                 __builtin_amdgcn_global_load_lds(mbase + 2ull * min(b0 + m, l0) + ph, buf + r * 64u, 16, 0, 0);
+            }
+        }
+        if constexpr (NR == 2 && MACRO_CHUNK_LEAN) {
+            if (wl < min(nslots, NS)) {
+                const uint32_t ci = min(c, (s_sml[wv][wl] - s_smb[wv][wl]) / CH);
+                __builtin_amdgcn_global_load_lds(p.macro_chunk + s_scb[wv][wl] + ci, info, 4, 0, 0);
             }
         }
     };
@@ -752,8 +784,23 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
     // c + 1 streams into s_chunk1, phase B the reverse.  A phase always runs
     // its CH macros (finished lanes are frozen); the DMA of the next chunk
     // is waited for (vmcnt(0)) once per phase
-    auto phase = [&](const uint4 *buf) __attribute__((always_inline)) {
+    auto phase = [&](const uint4 *buf, const uint32_t *info) __attribute__((always_inline)) {
         const uint4 *const cur = buf + moff;
+        if constexpr (NR == 2 && MACRO_CHUNK_LEAN) {
+            // one wave test for the whole chunk, then CH macros with no test
+            // and no branch between them but the stores' own
+            if (L.lean_chunk_ok(info[slot])) {
+#pragma unroll 2
+                for (uint32_t i = 0; i < CH; i++) {
+                    const uint4 a = cur[2 * i], u = cur[2 * i + 1];
+                    const uint32_t run = L.st == 0u ? ~0u : 0u;
+                    L.alu_lean(run, a.x, a.y);
+                    L.alu_lean(run, a.z, a.w);
+                    L.pulse_lean(run, u);
+                }
+                return;
+            }
+        }
 #pragma unroll 1
         for (uint32_t i = 0; i < CH; i++) {
             const uint4 a = cur[2 * i], u = cur[2 * i + 1];
@@ -780,17 +827,17 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
             }
         }
     };
-    stage(0u, s_chunk0[wv]);
+    stage(0u, s_chunk0[wv], s_info0[wv]);
     for (uint32_t c = 0; __ballot(L.st == 0u); c += 2) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        stage(c + 1u, s_chunk1[wv]);
-        phase(s_chunk0[wv]);
+        stage(c + 1u, s_chunk1[wv], s_info1[wv]);
+        phase(s_chunk0[wv], s_info0[wv]);
         if (!__ballot(L.st == 0u)) break;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        stage(c + 2u, s_chunk0[wv]);
-        phase(s_chunk1[wv]);
+        stage(c + 2u, s_chunk0[wv], s_info0[wv]);
+        phase(s_chunk1[wv], s_info1[wv]);
     }
     // no LDS DMA may still be in flight when the workgroup's LDS is released
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -233,16 +233,9 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
 template <int SRC, int FB>
 static hipError_t launch_src(const KParams &p, uint32_t blocks, size_t shmem, hipStream_t stream)
 {
-    if (shmem > 64 * 1024) {
-        // programs staged in dynamic LDS beyond the default 64 KiB need the opt-in
-        static size_t granted = 0;
-        if (shmem > granted) {
-            hipError_t e = hipFuncSetAttribute((const void *)straight_kernel<SRC, FB>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
-            if (e != hipSuccess) return e;
-            granted = shmem;
-        }
-    }
+    // programs staged in dynamic LDS beyond the default 64 KiB need the opt-in
+    const hipError_t e = opt_in_dynamic_lds((const void *)straight_kernel<SRC, FB>, shmem);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((straight_kernel<SRC, FB>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
     return hipGetLastError();
 }

@@ -192,6 +192,7 @@ class Emulator:
             raise DpemuError('dpemu_create(device={}) failed ({}): no usable HIP device'.format(device, rc))
         self._h = h
         self.device = device
+        self.lib_path = lib_path          # None: the in-tree build
         self.programs: Optional[ProgramSet] = None
 
     def close(self):
@@ -337,19 +338,24 @@ class RunPipeline:
     """
 
     def __init__(self, programs, cfg: _abi.Config, n_shots: int, want=('summary', 'events', 'meas', 'hist'),
-                 depth: int = 2, device: int = 0, first: Optional['Emulator'] = None, streams=None):
+                 depth: int = 2, device: int = 0, first: Optional['Emulator'] = None, streams=None,
+                 lib_path: Optional[str] = None):
         import torch
         if depth < 1:
             raise ValueError('depth must be >= 1')
         if streams is not None and len(streams) < depth:
             raise ValueError('need {} streams, got {}'.format(depth, len(streams)))
         self.emus, self._own = [], []
+        # every context on ONE library: the caller's, else first's (an A/B
+        # build passed as first=Emulator(0, lib_path=...) stays alone)
+        if lib_path is None and first is not None:
+            lib_path = first.lib_path
         try:
             for j in range(depth):
                 if j == 0 and first is not None:
                     e = first                                  # the caller's context, programs loaded
                 else:
-                    e = Emulator(device)
+                    e = Emulator(device, lib_path=lib_path)
                     self._own.append(e)
                     e.load(programs)
                 self.emus.append(e)

@@ -1,0 +1,174 @@
+// Store-shape probe for the config-5 DDS output (2048 channels x 209952
+// samples x 4 B = 1.72 GB, [channel][sample]).  Every variant writes the same
+// bytes; only which workgroup writes which 16-B piece, and when, changes.
+// Question: which channel-bound shape (a workgroup owns ONE channel, so it
+// can stage that channel's tables once) stores as fast as the torch fill?
+//
+//   fill     : WG b writes 4-KiB block b (one 16-B store per thread)
+//   cur      : the round-3 dds_tile_kernel shape: 13 stripes x 16 tiles per
+//              channel, channel-local 1024-sample tiles round-robin over the
+//              stripes, wave w of a stripe takes its tiles w, w + 4, ...
+//   cx<K><W|G>[s] : WG (ch, k, r), linear id (ch * K + k) * 8 + r, so that
+//              WGs dealt round-robin over the 8 XCDs put residue r on one XCD;
+//              it writes the GLOBAL 4-KiB blocks B of its channel with
+//              B % 8 == r, the i-th such block when i % K == k.  W: wave w
+//              takes its list entries w, w + 4, ... (a wave = one block);
+//              G: the workgroup writes each block together (wave w = row w).
+//              s: residue (r + 5 ch) % 8 instead -- the same shape with every
+//              XCD writing every residue (the XCD-affinity control).
+//   cc<K>W   : like cx<K>W but the K workgroups of (ch, r) take contiguous
+//              runs of the residue list instead of interleaving
+// The channel-boundary blocks are written partly by each channel's WG
+// (16-B granular masks), as a channel-bound kernel would.
+// Also records s_getreg(XCC_ID) per WG of one launch to check that WG g and
+// g + 8 share an XCD (MI355X_MICROARCH.md, workgroup dispatch).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int BLOCK = 256;
+constexpr uint32_t NCH = 2048, NS = 209952;
+
+__device__ __forceinline__ void st16(uint32_t *p, uint32_t v)
+{
+    const u32x4 w = {v, v + 1, v + 2, v + 3};
+    *reinterpret_cast<u32x4 *>(p) = w;
+}
+
+__device__ __forceinline__ uint32_t xcc_id()
+{
+    // HW_REG_XCC_ID (id 20), bits [3:0]
+    return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
+}
+
+__global__ void __launch_bounds__(BLOCK) fill_k(uint32_t *iq, uint64_t total)
+{
+    const uint64_t j = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) * 4;
+    if (j + 3 < total) st16(iq + j, (uint32_t)j);
+}
+
+__global__ void __launch_bounds__(BLOCK) cur_k(uint32_t *iq, uint32_t stripes, uint32_t *xcc)
+{
+    const uint32_t ch = blockIdx.x / stripes, s = blockIdx.x % stripes;
+    const uint32_t tiles = (NS + 1023) / 1024;
+    uint32_t *out = iq + (uint64_t)ch * NS;
+    const uint32_t n_t = (tiles - s + stripes - 1) / stripes;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    if (xcc && threadIdx.x == 0) xcc[blockIdx.x] = xcc_id();
+    for (uint32_t i = wv; i < n_t; i += 4) {
+        const uint32_t t = s + i * stripes;
+        for (int r = 0; r < 4; r++) {
+            const uint32_t j = t * 1024 + 4 * (64 * r + ln);
+            if (j + 3 < NS) st16(out + j, j);
+        }
+    }
+}
+
+// WG (ch, k, r): global blocks B of channel ch with B % 8 == res, list index i
+// (B = base8 + 8 i + res) with i % K == k (INTERLEAVE) or i in run k (contiguous)
+template <bool WAVE, bool INTERLEAVE>
+__global__ void __launch_bounds__(BLOCK) cx_k(uint32_t *iq, uint32_t K, uint32_t scramble, uint32_t *xcc)
+{
+    const uint32_t g = blockIdx.x;
+    const uint32_t r = g & 7u, k = (g >> 3) % K, ch = (g >> 3) / K;
+    const uint32_t res = scramble ? (r + 5 * ch) & 7u : r;
+    if (xcc && threadIdx.x == 0) xcc[g] = xcc_id();
+    const uint64_t j_lo = (uint64_t)ch * NS, j_hi = j_lo + NS;       // global samples of the channel
+    const uint64_t b_lo = j_lo / 1024, b_hi = (j_hi - 1) / 1024;     // its global blocks (inclusive)
+    const uint64_t base8 = b_lo & ~7ull;
+    const uint32_t n_list = (uint32_t)((b_hi - base8 - res) / 8 + 1); // i = 0 .. n_list-1 (B <= b_hi)
+    uint32_t i0, di, i1;
+    if (INTERLEAVE) { i0 = k; di = K; i1 = n_list; }
+    else { const uint32_t per = (n_list + K - 1) / K; i0 = k * per; di = 1; i1 = min(n_list, i0 + per); }
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    if (WAVE) {
+        for (uint32_t i = i0 + wv * di; i < i1; i += 4 * di) {
+            const uint64_t B = base8 + 8ull * i + res;
+            if (B < b_lo) continue;
+            for (int q = 0; q < 4; q++) {
+                const uint64_t j = B * 1024 + 4 * (64 * q + ln);
+                if (j >= j_lo && j < j_hi) st16(iq + j, (uint32_t)j);
+            }
+        }
+    } else {
+        for (uint32_t i = i0; i < i1; i += di) {
+            const uint64_t B = base8 + 8ull * i + res;
+            if (B < b_lo) continue;
+            const uint64_t j = B * 1024 + 4 * threadIdx.x;
+            if (j >= j_lo && j < j_hi) st16(iq + j, (uint32_t)j);
+        }
+    }
+}
+
+static uint32_t *g_iq;
+static uint32_t g_K, g_scr;
+
+template <typename F>
+static void bench(const char *name, F launch)
+{
+    const uint64_t bytes = (uint64_t)NCH * NS * 4;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    launch();
+    hipDeviceSynchronize();
+    std::vector<float> t;
+    for (int r = 0; r < 15; r++) {
+        hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    printf("{\"variant\": \"%s\", \"ms_min\": %.4f, \"ms_med\": %.4f, \"TB_s_min\": %.3f, \"TB_s_med\": %.3f}\n", name,
+           t[0], t[t.size() / 2], bytes / (t[0] * 1e-3) / 1e12, bytes / (t[t.size() / 2] * 1e-3) / 1e12);
+    fflush(stdout);
+    hipEventDestroy(e0); hipEventDestroy(e1);
+}
+
+// one launch with XCC ids recorded: fraction of WGs whose XCC == (g + c) % 8
+static void check_xcc(uint32_t n_wg, void (*launch)(uint32_t *), const char *name)
+{
+    uint32_t *d;
+    hipMalloc(&d, n_wg * 4);
+    launch(d);
+    hipDeviceSynchronize();
+    std::vector<uint32_t> h(n_wg);
+    hipMemcpy(h.data(), d, n_wg * 4, hipMemcpyDeviceToHost);
+    hipFree(d);
+    const uint32_t c = (h[0] + 8 - 0) & 7u;
+    uint32_t ok = 0;
+    for (uint32_t g = 0; g < n_wg; g++) ok += h[g] == ((g + c) & 7u);
+    printf("{\"xcc_check\": \"%s\", \"wgs\": %u, \"xcc_of_wg0\": %u, \"frac_round_robin\": %.5f}\n", name, n_wg, h[0],
+           (double)ok / n_wg);
+    fflush(stdout);
+}
+
+int main()
+{
+    const uint64_t total = (uint64_t)NCH * NS, bytes = total * 4;
+    if (hipMalloc(&g_iq, bytes) != hipSuccess) { printf("alloc failed\n"); return 1; }
+    check_xcc(NCH * 8, [](uint32_t *x) { cx_k<true, true><<<NCH * 8, BLOCK>>>(g_iq, 1, 0, x); }, "cx1W");
+    check_xcc(NCH * 13, [](uint32_t *x) { cur_k<<<NCH * 13, BLOCK>>>(g_iq, 13, x); }, "cur");
+    for (int rep = 0; rep < 2; rep++) {
+        bench("fill", [&] { fill_k<<<(uint32_t)(total / 4 / BLOCK), BLOCK>>>(g_iq, total); });
+        bench("cur", [&] { cur_k<<<NCH * 13, BLOCK>>>(g_iq, 13, nullptr); });
+        for (uint32_t K : {1u, 2u, 4u}) {
+            g_K = K;
+            char nm[32];
+            snprintf(nm, sizeof nm, "cx%uW", K);
+            bench(nm, [&] { cx_k<true, true><<<NCH * 8 * g_K, BLOCK>>>(g_iq, g_K, 0, nullptr); });
+            snprintf(nm, sizeof nm, "cx%uG", K);
+            bench(nm, [&] { cx_k<false, true><<<NCH * 8 * g_K, BLOCK>>>(g_iq, g_K, 0, nullptr); });
+            snprintf(nm, sizeof nm, "cx%uWs", K);
+            bench(nm, [&] { cx_k<true, true><<<NCH * 8 * g_K, BLOCK>>>(g_iq, g_K, 1, nullptr); });
+            if (K > 1) {
+                snprintf(nm, sizeof nm, "cc%uW", K);
+                bench(nm, [&] { cx_k<true, false><<<NCH * 8 * g_K, BLOCK>>>(g_iq, g_K, 0, nullptr); });
+            }
+        }
+    }
+    hipFree(g_iq);
+    return 0;
+}

@@ -35,9 +35,18 @@ def rows(pattern):
     return out
 
 
+# op_kernel<OP> of scripts/micro/valu_peak.hip: the opcode each one chains
+OPS = ['v_xor_b32', 'v_add_u32', 'v_sub_u32', 'v_and_b32', 'v_lshrrev_b32', 'v_lshlrev_b32', 'v_min_u32',
+       'v_mov_b32', 'v_cndmask_b32', 'v_bfe_i32', 'v_bitop3_b32', 'v_mad_u64_u32', 'v_lshl_add_u64',
+       'v_cmp_eq_u32', 'v_readlane_b32', 'v_mul_lo_u32', 'v_mul_hi_u32', 'v_ashrrev_i64']
+
+
 def variant(name):
     m = re.search(r'(valu|add|fma)_kernel<(\d+), (\d+)>', name)
-    return (m.group(1), int(m.group(2)), int(m.group(3))) if m else None
+    if m:
+        return (m.group(1), int(m.group(2)), int(m.group(3)))
+    m = re.search(r'op_kernel<(\d+)>', name)
+    return ('op', int(m.group(1)), 8) if m else None
 
 
 def main():
@@ -62,8 +71,12 @@ def main():
         # per-dispatch ratios from the same pass, then averaged
         cpi = [SIMDS * (c['GRBM_GUI_ACTIVE'] / XCDS) / c['SQ_INSTS_VALU'] for c in disp
                if c.get('SQ_INSTS_VALU') and c.get('GRBM_GUI_ACTIVE')]
-        rec = {'kernel': '{}_kernel<{}, {}>'.format(*v), 'mix': {'valu': 'add/shift/xor (int)', 'add': 'v_add_u32 only',
-                                                                  'fma': 'v_fma_f32 only'}[v[0]],
+        if v[0] == 'op':
+            kname, mix_ = 'op_kernel<{}>'.format(v[1]), OPS[v[1]] + ' only'
+        else:
+            kname = '{}_kernel<{}, {}>'.format(*v)
+            mix_ = {'valu': 'add/shift/xor (int)', 'add': 'v_add_u32 only', 'fma': 'v_fma_f32 only'}[v[0]]
+        rec = {'kernel': kname, 'mix': mix_,
                'chains': v[1], 'waves_per_simd': v[2],
                'dispatches_traced': len(dur[v]), 'dispatches_counted': len(disp), 'duration_ns': d_ns,
                'counters': mean,
@@ -72,7 +85,13 @@ def main():
                'clock_ghz': mean['GRBM_GUI_ACTIVE'] / XCDS / d_ns,
                'cycles_per_inst': sum(cpi) / len(cpi) if cpi else None}
         res.append(rec)
-    best = max((r for r in res if r['mix'] != 'v_fma_f32 only'), key=lambda r: r['valu_insts_per_s'])
+    best = max((r for r in res if r['mix'] != 'v_fma_f32 only' and not r['kernel'].startswith('op_')),
+               key=lambda r: r['valu_insts_per_s'])
+    # per opcode: cycles per wave64 instruction per SIMD of its chain kernel
+    # (the loop's few other VALU -- the iteration counter, the chains' seeds --
+    # are counted in with it, so an opcode's figure is a slight upper bound
+    # on its own rate)
+    opcode_cpi = {r['mix'].replace(' only', ''): r['cycles_per_inst'] for r in res if r['kernel'].startswith('op_')}
     out = {'what': 'wave64 integer-VALU issue peak of MI355X, measured: scripts/micro/valu_peak.hip under '
                    'rocprofv3 (kernel trace + one PMC pass: SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU '
                    'SQ_BUSY_CYCLES GRBM_GUI_ACTIVE); summarised by scripts/valu_peak_summary.py',
@@ -82,6 +101,7 @@ def main():
            'peak_cycles_per_inst': best['cycles_per_inst'], 'peak_clock_ghz': best['clock_ghz'],
            'guide_issue_model': '2 cycles per wave64 VALU instruction per SIMD (MI355X_MICROARCH.md:54): '
                                 '1024 SIMDs x 2.4 GHz / 2 = 1.229e12 /s',
+           'opcode_cycles_per_inst': opcode_cpi,
            'variants': res}
     with open(dest, 'w') as f:
         json.dump(out, f, indent=1)

@@ -274,26 +274,27 @@ def test_global_record_fallback(emu):
     assert (ref != 0).sum() > 10000
 
 
-def test_synthesis_pipeline_batches(emu):
-    """dds.SynthesisPipeline (two contexts / streams, batch k + 1's index
-    beside batch k's tiles, the bench's config-5 step): five batches of
-    different RB timelines, each batch's I/Q read on its returned stream while
-    later batches run, every one bit for bit equal to oracle_dds"""
+@pytest.mark.parametrize('depth', [2, 8])
+def test_synthesis_pipeline_batches(emu, depth):
+    """dds.SynthesisPipeline (`depth` contexts / streams, batch k + 1's index
+    beside batch k's tiles, the bench's config-5 step at depth 8): twelve
+    batches of different RB timelines, each batch's I/Q read on its returned
+    stream while later batches run, every one bit for bit equal to oracle_dds"""
     import torch
     from distributed_processor_amd.dds import SynthesisPipeline
-    ps = ProgramSet(workloads.config4_rb(n_seq=8, depth=12, n_cores=2))
+    ps = ProgramSet(workloads.config4_rb(n_seq=16, depth=12, n_cores=2))
     emu.load(ps)
     cfg = _abi.make_config(2, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=128, meas_cap=4,
                            meas_latency=64, seed=0x5EED)
     batches = []
-    for b in range(5):                                  # batch b: sequences [b, b + 3) of the table
+    for b in range(12):                                 # batch b: sequences [b, b + 3) of the table
         out = alloc_device_outputs(cfg, 3, want=('summary', 'events'))
         emu.run_device(cfg, 3, b, out)
         chans = [(b + q, c, e) for q in range(3) for c in range(2) for e in (workloads.QDRV, workloads.RDRV)]
         batches.append((out, ChannelPlan(ps, cfg, b, 3, chans, ELEM_PARAMS)))
     torch.cuda.synchronize()
     n_samples = 4096
-    pipe = SynthesisPipeline(0, depth=2)
+    pipe = SynthesisPipeline(0, depth=depth)
     try:
         got = []
         for out, plan in batches:
@@ -301,7 +302,7 @@ def test_synthesis_pipeline_batches(emu):
             with torch.cuda.stream(s):                   # consume on the batch's stream
                 got.append(iq.clone())
         pipe.drain()
-        assert pipe.k == 5
+        assert pipe.k == 12
         for b, ((out, plan), g) in enumerate(zip(batches, got)):
             ref = oracle.dds(plan.desc, host(out['summary']), host(out['events']), plan.env, plan.freq, n_samples,
                              cfg.event_cap)

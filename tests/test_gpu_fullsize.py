@@ -14,8 +14,8 @@ the oracle (config 4 at full size: tests/test_gpu_rb.py).
   run's histogram (dpemu_outputs.hist_next), config 3 with hist_assign;
 * config 5 (configs[4]): DDS of 128 RB timelines x 16 channels at 16
   samples / clock, the bench's full-size launch (2048 channels x 209,952
-  samples); 256 channels spread over the launch (128 qdrv, 128 rdrv), whole
-  length, equal to oracle_dds.
+  samples): every channel over its whole length equal to oracle_dds (in
+  chunks of 256 channels).
 
 oracle_fast / oracle_dds run with the job's CPU share (OMP_NUM_THREADS, 16
 on the GPU box)."""
@@ -103,7 +103,9 @@ def test_config3_shard_bit_exact(emu, rank, shape):
     assert abs(flip.mean() - 0.5) < 0.01
 
 
-def test_config5_full_launch_sampled_channels(emu):
+def config5_timelines(emu):
+    """the bench's config-5 inputs: 128 8-core RB timelines (depth 200) on the
+    device, the 2048-channel plan and the sample count"""
     import torch
     n_seq = 128
     ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
@@ -119,17 +121,27 @@ def test_config5_full_launch_sampled_channels(emu):
     chans = [(q, c, e) for q in range(n_seq) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
     plan = ChannelPlan(ps, cfg, 0, n_seq, chans, params)
     assert plan.n_channels == 2048 and n_samples > 200000
+    return cfg, ev, plan, n_samples
+
+
+def test_config5_full_launch_all_channels(emu):
+    import torch
+    cfg, ev, plan, n_samples = config5_timelines(emu)
     iq = emu.synthesize(plan, ev, n_samples)
     torch.cuda.synchronize()
-    pick = np.sort(np.concatenate([np.arange(0, plan.n_channels, 16), np.arange(1, plan.n_channels, 16)]))
-    got = iq[torch.from_numpy(pick).cuda()].cpu().numpy().view(np.uint32)
-    ref = oracle.dds(plan.desc[pick], ev['summary'].cpu().numpy(), ev['events'].cpu().numpy(), plan.env, plan.freq,
-                     n_samples, cfg.event_cap, threads=THREADS)
-    if not np.array_equal(got, ref):
-        bad = np.argwhere(got != ref)
-        raise AssertionError('{} mismatching samples, first at channel {} sample {}'.format(
-            len(bad), int(pick[bad[0][0]]), int(bad[0][1])))
-    assert (ref[0::2] != 0).any(axis=1).all() and (ref[1::2] != 0).any(axis=1).all()   # qdrv and rdrv play
+    summ, events = ev['summary'].cpu().numpy(), ev['events'].cpu().numpy()
+    plays = np.zeros(plan.n_channels, bool)
+    CH = 256
+    for c0 in range(0, plan.n_channels, CH):
+        got = iq[c0:c0 + CH].cpu().numpy().view(np.uint32)
+        ref = oracle.dds(plan.desc[c0:c0 + CH], summ, events, plan.env, plan.freq, n_samples, cfg.event_cap,
+                         threads=THREADS)
+        if not np.array_equal(got, ref):
+            bad = np.argwhere(got != ref)
+            raise AssertionError('{} mismatching samples, first at channel {} sample {}'.format(
+                len(bad), c0 + int(bad[0][0]), int(bad[0][1])))
+        plays[c0:c0 + CH] = (ref != 0).any(axis=1)
+    assert plays.all()                                   # every qdrv and rdrv channel plays
 
 
 @pytest.mark.parametrize('shape', [{}, BENCH_SHAPE], ids=['core_major', 'bench_shape'])

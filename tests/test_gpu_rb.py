@@ -3,16 +3,20 @@
 1.5 * 10^8 commands, a 2.4 GB device-resident program image), 10 shots per
 sequence = 10^6 shots = 2 * 10^6 (shot, core) lanes in one launch.
 
-* bit-exact: 2,000 shots in 50 windows spread over the whole program table,
-  compared with oracle_fast on every output array -- lanes of the full-size
-  launch (summaries, events, amplitudes, measurements, final registers) and
-  the same windows run as small launches with register traces;
+* bit-exact, the WHOLE launch: all 10^6 shots (2 * 10^6 lanes) compared
+  with oracle_fast on every output array -- summaries, event records,
+  measurements, final registers, the histogram -- in chunks of 50,000 shots
+  (device slices to host, the oracle on the same shot range);
+* 2,000 shots in 50 windows spread over the whole program table, run as
+  small launches with register traces, against oracle_fast;
 * full-size properties: every lane DONE, histogram total and per-sequence
   counts, sharding invariance (two half-size launches = the full launch).
 
 Programs are longer than hdl/proc.sv:12's 256-deep cmd_mem, within
 sim_modules/toplevel_sim.sv:5's 2^16 (SURVEY.md §7 hard part 6).
 """
+
+import os
 
 import numpy as np
 import pytest
@@ -56,21 +60,38 @@ def window_starts():
     return [int(x) for x in np.linspace(0, N_SHOTS - WIN, WINDOWS).astype(np.int64) + np.arange(WINDOWS) % 7]
 
 
-def test_full_table_windows_bit_exact(rb):
-    import torch
+CHUNK = 50000
+
+
+def test_full_launch_bit_exact(rb):
+    """every lane of the full-size launch against oracle_fast, chunk by chunk"""
     emu, ps, cfg, out = rb
-    assert emu.last_kernel()
-    for w0 in window_starts():
-        f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, w0, WIN,
-                            want=('summary', 'events', 'meas', 'regs'))
-        # the window's lanes of the full launch, core-major like the window run's
-        shots = torch.arange(w0, w0 + WIN, device='cuda')
-        lanes = torch.cat([shots, N_SHOTS + shots])
-        got = {'summary': out['summary'][lanes], 'events': out['events'][:, lanes],
-               'meas': out['meas'][:, lanes], 'regs': out['regs'][:, lanes]}
-        for k, v in got.items():
-            a = v.cpu().numpy().view(f[k].dtype)
-            assert np.array_equal(a, f[k]), 'shots [{}, {}) {}'.format(w0, w0 + WIN, k)
+    assert emu.last_kernel().startswith('macro_staged_kernel'), emu.last_kernel()
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or min(16, os.cpu_count() or 1)
+    want = ('summary', 'events', 'meas', 'regs')
+    for w0 in range(0, N_SHOTS, CHUNK):
+        n = min(CHUNK, N_SHOTS - w0)
+        f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, w0, n, threads=threads, want=want)
+        # core-major lanes: core c's shots [w0, w0 + n) are lanes c * N_SHOTS + [w0, w0 + n), which the
+        # chunk's oracle run holds at c * n + [0, n)
+        for c in range(2):
+            full = slice(c * N_SHOTS + w0, c * N_SHOTS + w0 + n)
+            part = slice(c * n, (c + 1) * n)
+            got = {'summary': out['summary'][full], 'events': out['events'][:, full],
+                   'meas': out['meas'][:, full], 'regs': out['regs'][:, full]}
+            ref = {'summary': f['summary'][part], 'events': f['events'][:, part],
+                   'meas': f['meas'][:, part], 'regs': f['regs'][:, part]}
+            for k in want:
+                a = got[k].cpu().numpy().view(ref[k].dtype)
+                if not np.array_equal(a, ref[k]):
+                    bad = np.argwhere(a != ref[k])
+                    raise AssertionError('shots [{}, {}) core {} {}: {} mismatches, first at {}'.format(
+                        w0, w0 + n, c, k, len(bad), bad[0].tolist()))
+        del f
+    # the histogram of the whole launch: one oracle pass, histogram only
+    f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, N_SHOTS, threads=threads,
+                        want=('hist',))
+    assert np.array_equal(out['hist'].cpu().numpy().view(f['hist'].dtype).reshape(f['hist'].shape), f['hist'])
 
 
 def test_full_table_windows_with_traces(rb):
