@@ -66,6 +66,26 @@ def _valu_peak():
 
 
 VALU_PEAK, VALU_CPI, VALU_PEAK_VARIANT = _valu_peak()
+
+
+def _kernel_valu_peaks():
+    """each bench kernel's own VALU issue peak: its opcode mix weighted by the
+    measured per-opcode issue costs (scripts/kernel_mixes.sh ->
+    profiles/<tag>_kernel_valu_peaks.json); {readable name: record}"""
+    path = os.path.join(REPO, 'profiles', '{}_kernel_valu_peaks.json'.format(PROFILE_TAG))
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return {k['name']: k for k in json.load(f)['kernels']}
+
+
+KERNEL_VALU_PEAKS = _kernel_valu_peaks()
+
+
+def kernel_key(name):
+    """'void dpemu::branch_kernel<11, 8>(dpemu::KParams)' -> 'branch_kernel<11,8>'"""
+    n = (name or '').split('(')[0].replace('void ', '').replace('dpemu::', '').replace(' ', '')
+    return n
 # where they are read from: the committed profiles/, or (DPEMU_BENCH_PROFILES)
 # the summaries of a profile pass just taken on the same box
 PROFILE_DIR = os.environ.get('DPEMU_BENCH_PROFILES') or os.path.join(REPO, 'profiles')
@@ -159,14 +179,23 @@ def valu_view(prof, kernel_ms=None, instrs=None):
     if not prof or not prof.get('SQ_INSTS_VALU'):
         return None
     n = float(prof['SQ_INSTS_VALU'])
-    v = {'bound': 'valu', 'unit': 'wave64 VALU instr/s', 'peak': VALU_PEAK, 'peak_cycles_per_inst': VALU_CPI,
-         'peak_source': 'profiles/r03_valu_peak_pmc.json ({})'.format(VALU_PEAK_VARIANT),
-         'valu_insts_per_launch': n}
+    # the kernel's OWN issue peak (its opcode mix at the measured per-opcode
+    # costs, at its clock in the PMC pass) when profiled; the uniform peak of
+    # the fastest integer mix beside it
+    own = KERNEL_VALU_PEAKS.get(kernel_key(prof.get('kernel')))
+    peak = own['peak_valu_insts_per_s'] if own else VALU_PEAK
+    v = {'bound': 'valu', 'unit': 'wave64 VALU instr/s', 'peak': peak,
+         'peak_cycles_per_inst': own['cycles_per_inst'] if own else VALU_CPI,
+         'peak_source': ('profiles/{}_kernel_valu_peaks.json (the kernel\'s own opcode mix at the measured '
+                         'per-opcode issue costs, {:.2f} GHz)'.format(PROFILE_TAG, own['clock_ghz']) if own else
+                         'profiles/r03_valu_peak_pmc.json ({})'.format(VALU_PEAK_VARIANT)),
+         'uniform_peak': VALU_PEAK, 'valu_insts_per_launch': n}
     if kernel_ms:
         v['achieved'] = n / (kernel_ms * 1e-3)
-        v['frac'] = v['achieved'] / VALU_PEAK
+        v['frac'] = v['achieved'] / peak
+        v['frac_uniform_peak'] = v['achieved'] / VALU_PEAK
     if prof.get('duration_ns'):
-        v['frac_rocprof'] = n / (prof['duration_ns'] * 1e-9) / VALU_PEAK
+        v['frac_rocprof'] = n / (prof['duration_ns'] * 1e-9) / peak
     if instrs:
         # VALU lane-ops per emulated instruction (the kernel's constant)
         v['valu_ops_per_instruction'] = n * 64 / instrs

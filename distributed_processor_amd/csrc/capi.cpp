@@ -887,10 +887,19 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.ev_lds = std::max<uint32_t>(8, (ch->event_cap + 7) & ~7u);
     p.env_lds = (env_max + 3) & ~3u;
     p.freq_lds = (freq_max + 3) & ~3u;
-    p.tiles = (p.n_samples + DDS_TILE - 1) / DDS_TILE;
-    p.stripes = std::max<uint32_t>(1, std::min<uint32_t>(p.tiles, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE));
+    if (DDS_XCD) {
+        // tile origins shifted by up to DDS_TILE - 16 samples (dds_tile_off): one more window
+        p.tiles = (p.n_samples + 2 * DDS_TILE - 16 - 1) / DDS_TILE;
+        p.stripes = DDS_XCD_K;
+        p.wg_tiles = (p.tiles + 8 * p.stripes - 1) / (8 * p.stripes);
+        if (DDS_XCD_BAL) p.wg_tiles = std::min(p.tiles, std::max(p.tiles / 8, 31u));   // residue M / the rest (< 32)
+    } else {
+        p.tiles = (p.n_samples + DDS_TILE - 1) / DDS_TILE;
+        p.stripes = std::max<uint32_t>(1, std::min<uint32_t>(p.tiles, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE));
+        p.wg_tiles = (p.tiles + p.stripes - 1) / p.stripes;
+    }
     {
-        const uint32_t fixed = dds_lds_bytes(0, DDS_TILES_PER_STRIPE, p.env_lds, p.freq_lds);
+        const uint32_t fixed = dds_lds_bytes(0, p.wg_tiles, p.env_lds, p.freq_lds);
         const uint32_t fit = fixed < DDS_WG_LDS_BUDGET ? (DDS_WG_LDS_BUDGET - fixed) / 20 & ~7u : 0u;
         p.rec_lds = std::min(p.ev_lds, std::max(fit, DDS_REC_LDS_MIN));
     }

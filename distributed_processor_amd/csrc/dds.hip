@@ -242,10 +242,14 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
         orr += (uint32_t)__popcll(br);
     }
     __syncthreads();
-    // window of tile c: from the latest record at or before its first cycle
+    // window of tile c (samples [c DDS_TILE - off, + DDS_TILE) of the channel,
+    // dds_tile_origin): from the latest record at or before its first cycle
     // (the first record when none is) to the latest at or before its last
-    for (uint32_t c = tid; c < p.tiles; c += BLOCK) {
-        const uint64_t j0 = (uint64_t)c * DDS_TILE, j1 = min(j0 + DDS_TILE, (uint64_t)p.n_samples) - 1;
+    const uint32_t off = dds_tile_off(p, ch);
+    const uint32_t n_tiles = (p.n_samples + off + DDS_TILE - 1) / DDS_TILE;
+    for (uint32_t c = tid; c < n_tiles; c += BLOCK) {
+        const uint64_t e = (uint64_t)c * DDS_TILE + DDS_TILE - off;
+        const uint64_t j0 = c ? (uint64_t)c * DDS_TILE - off : 0ull, j1 = min(e, (uint64_t)p.n_samples) - 1;
         const uint32_t n0 = (uint32_t)(j0 / spc), n1 = (uint32_t)(j1 / spc);
         const int a0 = last_le(s_st_t, (int)n_st, n0) + 1, a1 = last_le(s_st_t, (int)n_st, n1) + 1;
         const int b0 = last_le(s_rs_t, (int)n_rs, n0) + 1, b1 = last_le(s_rs_t, (int)n_rs, n1) + 1;
@@ -276,12 +280,69 @@ __device__ __forceinline__ int window_find_rec(const uint4 *rec, uint32_t lo, ui
     return a == 0 ? -1 : (int)(lo - base) + a - 1;
 }
 
-// local tile i of stripe `stripe`: the channel's tiles go round-robin over
-// its stripes, so at any time the stripes of a channel write adjacent tiles
-// (measured against contiguous runs per stripe: 0.317 vs 0.325 ms, config 5)
-__device__ __forceinline__ uint32_t stripe_tile(uint32_t stripe, uint32_t stripes, uint32_t i)
+// The tiles a workgroup sweeps: local tile i is the channel's tile
+// c_first + i * step, whose first sample is c * DDS_TILE - off (negative for
+// a first tile that begins before the channel: those samples are not made).
+//   XCD blocks (DDS_XCD): workgroup (ch, k, r) of a 1-D grid, linear id
+//     (ch K + k) 8 + r, takes the channel's tiles that lie in GLOBAL 4-KiB
+//     blocks B of the I/Q buffer with B % 8 == r (every K-th of them from
+//     k): workgroups are dealt round-robin over the 8 XCDs, so each XCD
+//     writes one residue of the buffer's blocks -- the torch-fill shape,
+//     which stores faster than every XCD writing every residue
+//     (profiles/r02_xcd_probe.jsonl, r04_dds_shape_probe.jsonl).  The tile
+//     origin off = ((ch N) mod DDS_TILE) rounded down to 16 samples puts
+//     every tile within 48 B of its block and on a clock boundary at 16
+//     samples per clock.
+//   stripes: grid (stripes, channels), stripe s takes tiles s, s + stripes,
+//     ... with off = 0 (round 3)
+struct TileMap {
+    uint32_t ch, c_first, step, n_t, off;
+    __device__ __forceinline__ uint32_t tile(uint32_t i) const { return c_first + i * step; }
+    __device__ __forceinline__ int32_t first(uint32_t i) const { return (int32_t)(tile(i) * DDS_TILE) - (int32_t)off; }
+};
+
+__device__ __forceinline__ TileMap tile_map(const DDSParams &p)
 {
-    return stripe + i * stripes;
+    TileMap m;
+    if (DDS_XCD_BAL) {
+        // residue workgroups g < 8 n_ch: (ch, r) takes the residue-r tiles
+        // c = c0 + 8 j, j < M, M = the channel's tiles / 8 rounded down to a
+        // multiple of 4 (every wave the same count: 4 waves x M / 4 rounds);
+        // channel workgroups g >= 8 n_ch: the contiguous rest [8 M, n_tiles)
+        const uint32_t g = blockIdx.x;
+        const bool rest = g >= 8u * p.n_channels;
+        m.ch = rest ? g - 8u * p.n_channels : g >> 3;
+        const uint64_t base = (uint64_t)m.ch * p.n_samples;
+        m.off = dds_tile_off(p, m.ch);
+        const uint32_t n_tiles = (p.n_samples + m.off + DDS_TILE - 1) / DDS_TILE;
+        const uint32_t M = (n_tiles / 8u) & ~3u;
+        if (rest) {
+            m.c_first = 8u * M;
+            m.step = 1u;
+            m.n_t = n_tiles - 8u * M;
+        } else {
+            m.c_first = ((g & 7u) - (uint32_t)(base / DDS_TILE)) & 7u;
+            m.step = 8u;
+            m.n_t = M;
+        }
+    } else if (DDS_XCD) {
+        const uint32_t K = p.stripes, g = blockIdx.x;
+        const uint32_t r = g & 7u, k = (g >> 3) % K;
+        m.ch = (g >> 3) / K;
+        const uint64_t base = (uint64_t)m.ch * p.n_samples;
+        m.off = dds_tile_off(p, m.ch);
+        const uint32_t n_tiles = (p.n_samples + m.off + DDS_TILE - 1) / DDS_TILE;
+        m.c_first = ((r - (uint32_t)(base / DDS_TILE)) & 7u) + 8u * k;
+        m.step = 8u * K;
+        m.n_t = m.c_first < n_tiles ? (n_tiles - 1u - m.c_first) / m.step + 1u : 0u;
+    } else {
+        m.ch = blockIdx.y;
+        m.off = 0;
+        m.c_first = blockIdx.x;
+        m.step = gridDim.x;
+        m.n_t = (p.tiles - blockIdx.x + gridDim.x - 1) / gridDim.x;
+    }
+    return m;
 }
 
 // the LDS-resident part of a tile workgroup
@@ -295,12 +356,12 @@ struct TileLds {
 // The sweep over a stripe's n_t tiles.  st / rs_t: the strobe records and
 // reset times, staged in LDS (base = the first staged index) or the global
 // index (base 0); inlined at both call sites so each keeps its address space.
-__device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L, const uint32_t *d, uint32_t stripe,
-                                           uint32_t stripes, uint32_t n_t, bool quad, const uint4 *st,
-                                           uint32_t st_lo, const uint32_t *rs_t, uint32_t rs_lo)
+__device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L, const uint32_t *d, const TileMap &M,
+                                           bool quad, const uint4 *st, uint32_t st_lo, const uint32_t *rs_t,
+                                           uint32_t rs_lo)
 {
     const uint32_t tid = threadIdx.x;
-    const uint32_t ch = blockIdx.y;
+    const uint32_t ch = M.ch, n_t = M.n_t;
     const uint32_t spc = d[2], interp = d[3] ? d[3] : 1u;
     const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
@@ -314,14 +375,15 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
         // are done once per 16 samples; wave w takes the stripe's tiles w, w + 4, ...
         const uint32_t wv = tid >> 6, ln = tid & 63u;
         for (uint32_t i = wv; i < n_t; i += BLOCK / 64) {
-            const uint32_t tile = stripe_tile(stripe, stripes, i);
-            const uint32_t n = tile * (DDS_TILE / 16) + ln;                  // this lane's cycle
-            const uint32_t j0 = 16 * n;
+            const int32_t tb = M.first(i);                                  // the tile's first sample (16 | tb)
+            const int32_t js = tb + 16 * (int32_t)ln;                       // this lane's cycle n = js / 16
+            const uint32_t n = (uint32_t)js >> 4;
             const uint4 w = L.win[i];
             uint32_t v[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) v[q] = 0u;
-            const int si = j0 < p.n_samples ? window_find_rec(st, w.x, w.y, st_lo, n) : -1;
+            bool live = false;                                              // this lane's cycle plays a pulse
+            const int si = js >= 0 && (uint32_t)js < p.n_samples ? window_find_rec(st, w.x, w.y, st_lo, n) : -1;
             if (si >= 0) {
                 const uint4 rec = st[si];                            // {t, env word, phase | freq << 17, amp}
                 const uint32_t A = rec.y & 0xFFFu, Lw = (rec.y >> 12) & 0xFFFu, fi = rec.z >> 17;
@@ -338,6 +400,7 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
                 }
                 const uint32_t d0 = 16 * (n - rec.x);                // samples since the strobe's first
                 if (16 * fi + 15 < freq_len && d0 < lim) {
+                    live = true;
                     const int ri = window_find(rs_t, w.z, w.w, rs_lo, n);
                     const uint32_t t_ref = ri >= 0 ? rs_t[ri] : 0u;
                     const uint32_t *frp = s_freq + 32 * fi;          // (R, R') pairs; pair 0 = (F0, 0)
@@ -392,8 +455,23 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
             // apart): round r, lanes 16 r .. 16 r + 15 put their 4 chunks
             // (lane l's chunk q at slot 4 (l & 15) + (q ^ (l >> 2 & 3)):
             // conflict-free both ways), every lane takes one chunk and stores
+            if (DDS_ZERO_TILES && !__any(live)) {
+                // no lane plays a pulse (most of a readout channel, the gaps of a
+                // drive channel): the tile is zeros, stored dense without the transpose
+                const uint32_t z[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int32_t jq = tb + 4 * (int32_t)(64u * r + ln);
+#ifdef DDS_PROBE_NOSTORE
+                    if (jq >= 0 && p.event_cap == 12345u)
+#else
+                    if (jq >= 0)
+#endif
+                        store4(out, (uint32_t)jq, p.n_samples, z);
+                }
+                continue;
+            }
             uint4 *xp = L.xpose + 64 * wv;
-            const uint32_t tb = tile * DDS_TILE;                      // the tile's first sample
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 if ((ln >> 4) == (uint32_t)r) {
@@ -408,17 +486,24 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
                 const uint32_t lc = ln >> 2;                            // source lane 16 r + lc
                 const uint4 x = xp[4 * lc + ((ln & 3u) ^ ((lc >> 2) & 3u))];
                 const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
-                store4(out, tb + 4 * (64u * r + ln), p.n_samples, w4);
+                const int32_t jq = tb + 4 * (int32_t)(64u * r + ln);
+#ifdef DDS_PROBE_NOSTORE                                        // A/B probe only: compute, no stores
+                if (jq >= 0 && (w4[0] ^ w4[1] ^ w4[2] ^ w4[3]) == 0x9E3779B9u && p.event_cap == 12345u)
+#else
+                if (jq >= 0)
+#endif
+                    store4(out, (uint32_t)jq, p.n_samples, w4);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the next writes
                 __builtin_amdgcn_wave_barrier();
             }
         }
         return;
     }
-    const uint32_t k0 = (4 * tid) & (spc - 1);     // sub-sample slot: fixed (the tile is a multiple of spc)
+    const uint32_t k0 = (4 * tid) & (spc - 1);     // sub-sample slot: fixed (tiles start at multiples of 16)
     for (uint32_t i = 0; i < n_t; i++) {
-        const uint32_t j0 = stripe_tile(stripe, stripes, i) * DDS_TILE + 4 * tid;
-        if (j0 >= p.n_samples) continue;
+        const int32_t js = M.first(i) + 4 * (int32_t)tid;
+        if (js < 0 || (uint32_t)js >= p.n_samples) continue;
+        const uint32_t j0 = (uint32_t)js;
         const uint4 w = L.win[i];
         uint32_t v[4] = {0u, 0u, 0u, 0u};
         if (quad) {
@@ -525,7 +610,12 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
 //   the mix sat16(E (x) a) as 2 v_dot2_i32_i16 + v_cvt_pk_i16_i32;
 //   else the generic per-sample sweep (X/Y form, tables read where they lie).
 // ===========================================================================
-__global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
+// 8 waves per SIMD: 64 VGPRs (and <= 20 KiB of LDS per workgroup, capi.cpp)
+#ifndef DDS_WAVES_PER_EU
+#define DDS_WAVES_PER_EU 8
+#endif
+#define DDS_TILE_ATTR __attribute__((amdgpu_waves_per_eu(DDS_WAVES_PER_EU)))
+__global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDSParams p)
 {
     // dynamic LDS (dds_lds_bytes): quarter sine table | strobe records |
     // reset times | tile windows | env | freq | store transpose
@@ -534,21 +624,22 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
     uint4 *s_st = reinterpret_cast<uint4 *>(s_dyn + DDS_LUT_BYTES);
     uint32_t *s_rs_t = reinterpret_cast<uint32_t *>(s_st + p.rec_lds);
     uint4 *s_win = reinterpret_cast<uint4 *>(s_rs_t + p.rec_lds);
-    uint32_t *s_env = reinterpret_cast<uint32_t *>(s_win + DDS_TILES_PER_STRIPE);
+    uint32_t *s_env = reinterpret_cast<uint32_t *>(s_win + p.wg_tiles);
     uint32_t *s_freq = s_env + p.env_lds;
     uint4 *s_xpose = reinterpret_cast<uint4 *>(s_freq + p.freq_lds);   // DDS_XPOSE_BYTES, 16-B aligned
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t ch = blockIdx.y, stripe = blockIdx.x, stripes = gridDim.x;
+    const TileMap M = tile_map(p);
+    if (M.n_t == 0) return;                          // (workgroup-uniform)
+    const uint32_t ch = M.ch, n_t = M.n_t;
     const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
     const uint32_t spc = d[2], interp = d[3] ? d[3] : 1u;
     const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
     const bool staged = (interp == 1 ? dds_env_pairs_words(env_len) : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds;
-    const uint32_t n_t = (p.tiles - stripe + stripes - 1) / stripes;   // this stripe's tiles (<= DDS_TILES_PER_STRIPE)
     const uint4 *gwin = p.win + (uint64_t)ch * p.tiles;
-    // the stripe's strobes / resets: from its first tile's window to its last's end
-    const uint4 w_first = gwin[stripe_tile(stripe, stripes, 0)], w_last = gwin[stripe_tile(stripe, stripes, n_t - 1)];
+    // the workgroup's strobes / resets: from its first tile's window to its last's end
+    const uint4 w_first = gwin[M.tile(0)], w_last = gwin[M.tile(n_t - 1)];
     const uint32_t st_lo = w_first.x, st_n = w_last.x + w_last.y - st_lo;
     const uint32_t rs_lo = w_first.z, rs_n = w_last.z + w_last.w - rs_lo;
     const bool fits = st_n <= p.rec_lds && rs_n <= p.rec_lds;    // workgroup-uniform
@@ -584,15 +675,19 @@ __global__ void __launch_bounds__(BLOCK) dds_tile_kernel(const DDSParams p)
         for (uint32_t i = tid; i < st_n; i += BLOCK) s_st[i] = xs[st_lo + i];
         for (uint32_t i = tid; i < rs_n; i += BLOCK) s_rs_t[i] = xr[rs_lo + i];
     }
-    if (tid < n_t) s_win[tid] = gwin[stripe_tile(stripe, stripes, tid)];
+    for (uint32_t i = tid; i < n_t; i += BLOCK) s_win[i] = gwin[M.tile(i)];
     bad = __syncthreads_or(bad);
+#ifdef DDS_PROBE_NOSWEEP                                            // A/B probe only: the prologue alone
+    if (p.event_cap == 12345u) p.iq[tid] = s_win[tid & 7].x ^ s_st[tid & 7].y ^ s_env[tid] ^ (uint32_t)s_lut[tid];
+    return;
+#endif
 
     const bool quad = staged && !bad && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
     const TileLds L{s_lut, s_win, s_env, s_freq, s_xpose};
     if (fits)
-        tile_sweep(p, L, d, stripe, stripes, n_t, quad, s_st, st_lo, s_rs_t, rs_lo);
+        tile_sweep(p, L, d, M, quad, s_st, st_lo, s_rs_t, rs_lo);
     else
-        tile_sweep(p, L, d, stripe, stripes, n_t, quad, xs, 0u, xr, 0u);
+        tile_sweep(p, L, d, M, quad, xs, 0u, xr, 0u);
 }
 
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
@@ -606,10 +701,12 @@ hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    const uint32_t lds = dds_lds_bytes(p.rec_lds, DDS_TILES_PER_STRIPE, p.env_lds, p.freq_lds);
+    const uint32_t lds = dds_lds_bytes(p.rec_lds, p.wg_tiles, p.env_lds, p.freq_lds);
     const hipError_t e = opt_in_dynamic_lds(reinterpret_cast<const void *>(dds_tile_kernel), lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(dds_tile_kernel, dim3(p.stripes, p.n_channels), dim3(BLOCK), lds, stream, p);
+    const dim3 grid = DDS_XCD_BAL ? dim3(p.n_channels * 9u)
+                    : DDS_XCD ? dim3(p.n_channels * 8u * p.stripes) : dim3(p.stripes, p.n_channels);
+    hipLaunchKernelGGL(dds_tile_kernel, grid, dim3(BLOCK), lds, stream, p);
     return hipGetLastError();
 }
 

@@ -220,8 +220,9 @@ struct DDSParams {
     uint32_t ev_lds;               // compacted-event slots per channel (>= event_cap, multiple of 8)
     uint32_t rec_lds;              // strobe records / reset times a tile workgroup stages in LDS (<= ev_lds)
     uint32_t env_lds, freq_lds;    // LDS staging capacity for a channel's env / freq table (words, as staged)
-    uint32_t tiles;                // sample tiles per channel (DDS_TILE samples each)
-    uint32_t stripes;              // workgroups per channel (gridDim.x)
+    uint32_t tiles;                // tile windows per channel (DDS_TILE samples each; dds_tile_off)
+    uint32_t stripes;              // DDS_XCD: workgroups per (channel, block residue); else per channel
+    uint32_t wg_tiles;             // most tiles one workgroup sweeps (its LDS window slots)
     // event index (dds_index_kernel -> dds_tile_kernel)
     uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
     uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
@@ -233,7 +234,30 @@ constexpr uint32_t DDS_TILE = 4 * BLOCK;      // samples per tile: 4 per thread,
 #ifndef DDS_TPS
 #define DDS_TPS 16
 #endif
-constexpr uint32_t DDS_TILES_PER_STRIPE = DDS_TPS;   // tiles per workgroup (build-time A/B: -DDDS_TPS=)
+constexpr uint32_t DDS_TILES_PER_STRIPE = DDS_TPS;   // stripes: tiles per workgroup (build-time A/B: -DDDS_TPS=)
+// XCD-block tile mapping (dds.hip TileMap), else round-3 stripes (A/B: -DDPEMU_DDS_XCD=0)
+#ifndef DPEMU_DDS_XCD
+#define DPEMU_DDS_XCD 1
+#endif
+constexpr bool DDS_XCD = DPEMU_DDS_XCD != 0;
+// 2: balanced -- residue workgroups take a multiple of 4 tiles (one per wave
+// and round), a workgroup per channel the contiguous rest (dds.hip tile_map)
+constexpr bool DDS_XCD_BAL = DPEMU_DDS_XCD == 2;
+#ifndef DPEMU_DDS_ZERO
+#define DPEMU_DDS_ZERO 1
+#endif
+constexpr bool DDS_ZERO_TILES = DPEMU_DDS_ZERO;   // all-zero wave tiles skip the transpose (A/B: -DDPEMU_DDS_ZERO=0)
+#ifndef DPEMU_DDS_K
+#define DPEMU_DDS_K 1
+#endif
+constexpr uint32_t DDS_XCD_K = DPEMU_DDS_K;   // workgroups per (channel, residue) (A/B: -DDPEMU_DDS_K=)
+// channel ch's tile origin: tile c holds samples [c DDS_TILE - off, + DDS_TILE);
+// XCD blocks: off = (ch N mod DDS_TILE) rounded down to 16 samples, so tile c
+// starts within 12 samples of global 4-KiB block (ch N) / DDS_TILE + c
+__host__ __device__ inline uint32_t dds_tile_off(const DDSParams &p, uint32_t ch)
+{
+    return DDS_XCD ? (uint32_t)(((uint64_t)ch * p.n_samples) % DDS_TILE) & ~15u : 0u;
+}
 constexpr uint32_t DDS_ENV_LDS_MAX = 8192;    // words: tables up to 32 KiB are staged in LDS
 constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;   // words: 64 freq entries as (R, R') pairs
 
@@ -251,7 +275,8 @@ __host__ __device__ inline uint32_t dds_lds_bytes(uint32_t rec_lds, uint32_t til
 // occupancy) share a CU's 160 KiB.  The record capacity is what is left of
 // it (at least DDS_REC_LDS_MIN); a stripe whose window holds more strobes or
 // resets than that reads them from the global index instead.
-constexpr uint32_t DDS_WG_LDS_BUDGET = 20 * 1024;
+// (less 512 B: the compiler's static LDS of the kernel, so 8 fit in 160 KiB)
+constexpr uint32_t DDS_WG_LDS_BUDGET = 20 * 1024 - 512;
 constexpr uint32_t DDS_REC_LDS_MIN = 64;
 
 // LDS words of an interp-1 envelope of n words staged as swizzled (E, E')

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 kernel-trace + PMC passes of the bench into per-kernel JSON.
 
-usage: python scripts/pmc_summary.py <prof root (e.g. gpurun_out/r01)> <tag> [dest dir] [key=substr|substr,...]
+usage: python scripts/pmc_summary.py <prof root (e.g. gpurun_out/r01)> <tag> [dest dir] [key=substr|substr[@grid],...]
 
 Reads <root>/prof_trace or <root>/trace (--kernel-trace --stats) and every
 other subdirectory's PMC pass (counter_collection.csv), groups dispatches by (kernel, grid size),
@@ -81,6 +81,9 @@ def main():
         GRIDS.clear()
         for item in sys.argv[4].split(','):
             k, subs = item.split('=')
+            if '@' in subs:            # key=substr@grid: only dispatches of that grid size (threads)
+                subs, g = subs.split('@')
+                GRIDS[k] = int(g)
             KERNELS[k] = tuple(subs.split('|'))
     os.makedirs(dest, exist_ok=True)
     # kernel trace: per (kernel, grid) durations

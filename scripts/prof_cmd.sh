@@ -20,5 +20,7 @@ run trace 300 --kernel-trace --stats || exit $?
 run fetch 300 --pmc FETCH_SIZE || exit $?
 run write 300 --pmc WRITE_SIZE || exit $?
 run sq1 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE || exit $?
-run sq2 300 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE || exit $?
+run sq2 300 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE || exit $?
+# the VALU stream's 32- / 64-bit integer split (the kernels' own VALU peak, scripts/kernel_valu_peak.py)
+run sq3 300 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_MUL_F32 GRBM_GUI_ACTIVE || exit $?
 find $out/trace -name "*kernel_stats.csv" -exec cat {} \;

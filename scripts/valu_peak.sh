@@ -10,4 +10,4 @@ timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $out/trace -o trace --outp
     -- ./scripts/micro/valu_peak > $out/trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
     -d $out/pmc -o pmc --output-format csv -- ./scripts/micro/valu_peak > $out/pmc.log 2>&1 || { echo "pmc pass failed"; exit 1; }
-python3 scripts/valu_peak_summary.py $out $out/r03_valu_peak_pmc.json
+python3 scripts/valu_peak_summary.py $out $out/valu_peak_pmc.json

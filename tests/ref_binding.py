@@ -34,7 +34,10 @@ _L = None
 
 
 def load(path='libdpemu.so'):
-    """bind the library once: entry points, ABI version, struct layouts"""
+    """bind the library once: entry points, ABI version, struct layouts.
+    A process that also uses PyTorch-ROCm imports torch first: libdpemu.so
+    then binds torch's HIP runtime, and both see the GPU (one runtime per
+    process)."""
     global _L
     if _L is not None:
         return _L

@@ -43,8 +43,15 @@ def test_integration_doc_holds_the_module_verbatim():
     assert any(b == src for b in blocks), 'INTEGRATION.md §3 must hold tests/ref_binding.py verbatim'
 
 
+def bind():
+    """the binding on the in-tree library; torch's HIP runtime first (the
+    GPU tests use torch in the same process, ref_binding.load)"""
+    _native.load_library()
+    return ref_binding.load(_native.LIB_PATH)
+
+
 def test_binding_layouts_match_library_and_mirror():
-    L = ref_binding.load(_native.LIB_PATH)
+    L = bind()
     sizes = (C.c_uint64 * 3)()
     L.dpemu_struct_sizes(sizes)
     assert sizes[0] == C.sizeof(ref_binding.DpemuConfig) == C.sizeof(_abi.Config)
@@ -89,6 +96,7 @@ def binding_config(C_, **kw):
 @pytest.mark.parametrize('which', ['golden', 'config1', 'restated'])
 def test_run_assembled_vs_oracle(which):
     import oracle
+    bind()
     asm = assembled_case(which)
     words, offsets, n_instr, table, C_ = ref_binding.pack_assembled(asm)
     n_shots = 20000
