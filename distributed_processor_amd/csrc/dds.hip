@@ -336,11 +336,27 @@ __device__ __forceinline__ TileMap tile_map(const DDSParams &p)
         m.step = 8u * K;
         m.n_t = m.c_first < n_tiles ? (n_tiles - 1u - m.c_first) / m.step + 1u : 0u;
     } else {
+#if DDS_STRIPE_ORDER == 1          // A/B: channels in a scrambled dispatch order (resident WGs far apart)
+        m.ch = (uint32_t)(((uint64_t)blockIdx.y * 1000003ull) % p.n_channels);
+        const uint32_t stripe = blockIdx.x, stripes = gridDim.x;
+#elif DDS_STRIPE_ORDER == 2        // A/B: grid (channels, stripes): every channel's stripe 0 first
+        m.ch = blockIdx.x;
+        const uint32_t stripe = blockIdx.y, stripes = gridDim.y;
+#else
         m.ch = blockIdx.y;
+        const uint32_t stripe = blockIdx.x, stripes = gridDim.x;
+#endif
         m.off = 0;
-        m.c_first = blockIdx.x;
-        m.step = gridDim.x;
-        m.n_t = (p.tiles - blockIdx.x + gridDim.x - 1) / gridDim.x;
+#if DDS_STRIPE_ORDER == 3          // A/B: contiguous stripes (a stripe's records are 1/stripes of the channel's)
+        const uint32_t per = (p.tiles + stripes - 1) / stripes;
+        m.c_first = stripe * per;
+        m.step = 1;
+        m.n_t = m.c_first < p.tiles ? min(per, p.tiles - m.c_first) : 0u;
+#else
+        m.c_first = stripe;
+        m.step = stripes;
+        m.n_t = (p.tiles - stripe + stripes - 1) / stripes;
+#endif
     }
     return m;
 }
@@ -610,11 +626,16 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
 //   the mix sat16(E (x) a) as 2 v_dot2_i32_i16 + v_cvt_pk_i16_i32;
 //   else the generic per-sample sweep (X/Y form, tables read where they lie).
 // ===========================================================================
-// 8 waves per SIMD: 64 VGPRs (and <= 20 KiB of LDS per workgroup, capi.cpp)
+// waves per SIMD the register allocation targets: 7 (69 VGPRs, spill-free);
+// forcing 8 (64 VGPRs) spills 10 VGPRs and measured 15 % slower
+// (profiles/r04_dds_variants_ab.json)
 #ifndef DDS_WAVES_PER_EU
-#define DDS_WAVES_PER_EU 8
+#define DDS_WAVES_PER_EU 7
 #endif
 #define DDS_TILE_ATTR __attribute__((amdgpu_waves_per_eu(DDS_WAVES_PER_EU)))
+#ifndef DDS_STRIPE_ORDER
+#define DDS_STRIPE_ORDER 0
+#endif
 __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDSParams p)
 {
     // dynamic LDS (dds_lds_bytes): quarter sine table | strobe records |
@@ -705,7 +726,8 @@ hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
     const hipError_t e = opt_in_dynamic_lds(reinterpret_cast<const void *>(dds_tile_kernel), lds);
     if (e != hipSuccess) return e;
     const dim3 grid = DDS_XCD_BAL ? dim3(p.n_channels * 9u)
-                    : DDS_XCD ? dim3(p.n_channels * 8u * p.stripes) : dim3(p.stripes, p.n_channels);
+                    : DDS_XCD ? dim3(p.n_channels * 8u * p.stripes)
+                    : DDS_STRIPE_ORDER == 2 ? dim3(p.n_channels, p.stripes) : dim3(p.stripes, p.n_channels);
     hipLaunchKernelGGL(dds_tile_kernel, grid, dim3(BLOCK), lds, stream, p);
     return hipGetLastError();
 }

@@ -237,14 +237,14 @@ constexpr uint32_t DDS_TILE = 4 * BLOCK;      // samples per tile: 4 per thread,
 constexpr uint32_t DDS_TILES_PER_STRIPE = DDS_TPS;   // stripes: tiles per workgroup (build-time A/B: -DDDS_TPS=)
 // XCD-block tile mapping (dds.hip TileMap), else round-3 stripes (A/B: -DDPEMU_DDS_XCD=0)
 #ifndef DPEMU_DDS_XCD
-#define DPEMU_DDS_XCD 1
+#define DPEMU_DDS_XCD 0
 #endif
 constexpr bool DDS_XCD = DPEMU_DDS_XCD != 0;
 // 2: balanced -- residue workgroups take a multiple of 4 tiles (one per wave
 // and round), a workgroup per channel the contiguous rest (dds.hip tile_map)
 constexpr bool DDS_XCD_BAL = DPEMU_DDS_XCD == 2;
 #ifndef DPEMU_DDS_ZERO
-#define DPEMU_DDS_ZERO 1
+#define DPEMU_DDS_ZERO 0
 #endif
 constexpr bool DDS_ZERO_TILES = DPEMU_DDS_ZERO;   // all-zero wave tiles skip the transpose (A/B: -DDPEMU_DDS_ZERO=0)
 #ifndef DPEMU_DDS_K
