@@ -39,6 +39,7 @@ hipError_t opt_in_dynamic_lds(const void *fn, size_t bytes)
 
 struct dpemu_ctx {
     int device = 0;
+    uint32_t n_cu = 256;                    // compute units of the device (hipDeviceAttributeMultiprocessorCount)
     std::string err;
     // programs
     uint4 *d_uops = nullptr;                // decode_cmd words, program-major (KParams::uops)
@@ -314,6 +315,9 @@ int dpemu_create(int device, dpemu_ctx **out)
     if (hipSetDevice(device) != hipSuccess) return DPEMU_E_DEVICE;
     dpemu_ctx *ctx = new dpemu_ctx();
     ctx->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        ctx->n_cu = (uint32_t)cus;
     std::vector<int16_t> lut(4096);
     dpemu_dds_sin_lut(lut.data());
     if (hipMalloc(&ctx->d_thr, DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
@@ -836,6 +840,19 @@ int dpemu_dds_sin_lut(int16_t *out)
 
 }  // extern "C"
 
+#ifdef DDS_PROBE_TIMES
+static unsigned long long *g_probe = nullptr;
+static uint64_t g_probe_n = 0, g_probe_used = 0;
+// the last synthesis's stamps {start, end, hw_id | xcc << 32 | channel << 40} per workgroup
+extern "C" uint64_t dpemu_probe_dds_times(unsigned long long *out, uint64_t n_max)
+{
+    if (hipDeviceSynchronize() != hipSuccess || !g_probe) return 0;
+    const uint64_t n = std::min(n_max, g_probe_used);
+    if (hipMemcpy(out, g_probe, n * 24, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return n;
+}
+#endif
+
 extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uint32_t *summary,
                          const uint32_t *events, const uint32_t *env_tables, const uint32_t *freq_tables,
                          int16_t *iq_out, void *stream)
@@ -864,6 +881,17 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, order_begin(ctx, s));
+    // the tile kernel's dispatch order: channels grouped by element (stable),
+    // so workgroups of one element's cost run together (DDS_ORDER_ELEM);
+    // appended to the descriptors
+    {
+        std::vector<uint32_t> order(ch->n_channels);
+        for (uint32_t i = 0; i < ch->n_channels; i++) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+            return desc[(size_t)a * DDS_CH_WORDS + 1] < desc[(size_t)b * DDS_CH_WORDS + 1];
+        });
+        desc.insert(desc.end(), order.begin(), order.end());
+    }
     if (desc != ctx->ch_cache) {            // descriptors change rarely: upload only then
         HIPCHK(ctx, hipStreamSynchronize(s));   // an earlier launch may still read d_ch
         if (desc.size() > ctx->ch_cap) {
@@ -881,6 +909,7 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.env = env_tables; p.freq = freq_tables;
     p.sin_lut = ctx->d_sin;
     p.ch = ctx->d_ch;
+    p.ch_order = ctx->d_ch + (size_t)ch->n_channels * DDS_CH_WORDS;
     p.iq = reinterpret_cast<uint32_t *>(iq_out);
     p.n_channels = ch->n_channels; p.n_lanes = ch->n_lanes; p.n_samples = ch->n_samples;
     p.event_cap = ch->event_cap;
@@ -897,6 +926,13 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
         p.tiles = (p.n_samples + DDS_TILE - 1) / DDS_TILE;
         p.stripes = std::max<uint32_t>(1, std::min<uint32_t>(p.tiles, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE));
         p.wg_tiles = (p.tiles + p.stripes - 1) / p.stripes;
+        if (DDS_TAIL) {
+            // one round of resident workgroups' worth of short stripes at the end:
+            // the device's CUs x 7 resident tile workgroups x DDS_TAIL_TILES tiles
+            p.tail_stripes = std::max<uint32_t>(p.stripes, (p.tiles + DDS_TAIL_TILES - 1) / DDS_TAIL_TILES);
+            const uint64_t tail_tiles = (uint64_t)ctx->n_cu * 7u * DDS_TAIL_TILES;
+            p.tail_ch = (uint32_t)std::min<uint64_t>(p.n_channels, (tail_tiles + p.tiles - 1) / p.tiles);
+        }
     }
     {
         const uint32_t fixed = dds_lds_bytes(0, p.wg_tiles, p.env_lds, p.freq_lds);
@@ -915,6 +951,21 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.xs = reinterpret_cast<uint4 *>(b);
     p.win = reinterpret_cast<uint4 *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
     p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16 + (uint64_t)p.n_channels * p.tiles * 16);
+#ifdef DDS_PROBE_TIMES                    // diagnostic build: per-workgroup stamps of the tile kernel
+    {
+        const uint64_t n_wg = DDS_XCD_BAL ? 9ull * p.n_channels : DDS_XCD ? 8ull * p.n_channels * p.stripes
+                              : DDS_TAIL ? (uint64_t)(p.n_channels - p.tail_ch) * p.stripes + (uint64_t)p.tail_ch * p.tail_stripes
+                                         : (uint64_t)p.stripes * p.n_channels;
+        if (n_wg > g_probe_n) {
+            (void)hipFree(g_probe);
+            HIPCHK(ctx, hipMalloc(&g_probe, n_wg * 24));
+            g_probe_n = n_wg;
+        }
+        HIPCHK(ctx, hipMemsetAsync(g_probe, 0, n_wg * 24, s));
+        p.probe = g_probe;
+        g_probe_used = n_wg;
+    }
+#endif
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, launch_dds_index(p, s));   // outside the timed bracket: it holds the synthesis kernel alone
     HIPCHK(ctx, timing_start(ctx, s, &ev_stop));

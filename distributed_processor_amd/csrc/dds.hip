@@ -312,6 +312,7 @@ __device__ __forceinline__ TileMap tile_map(const DDSParams &p)
         const uint32_t g = blockIdx.x;
         const bool rest = g >= 8u * p.n_channels;
         m.ch = rest ? g - 8u * p.n_channels : g >> 3;
+        if (DDS_ORDER_ELEM) m.ch = p.ch_order[m.ch];
         const uint64_t base = (uint64_t)m.ch * p.n_samples;
         m.off = dds_tile_off(p, m.ch);
         const uint32_t n_tiles = (p.n_samples + m.off + DDS_TILE - 1) / DDS_TILE;
@@ -329,12 +330,33 @@ __device__ __forceinline__ TileMap tile_map(const DDSParams &p)
         const uint32_t K = p.stripes, g = blockIdx.x;
         const uint32_t r = g & 7u, k = (g >> 3) % K;
         m.ch = (g >> 3) / K;
+        if (DDS_ORDER_ELEM) m.ch = p.ch_order[m.ch];
         const uint64_t base = (uint64_t)m.ch * p.n_samples;
         m.off = dds_tile_off(p, m.ch);
         const uint32_t n_tiles = (p.n_samples + m.off + DDS_TILE - 1) / DDS_TILE;
         m.c_first = ((r - (uint32_t)(base / DDS_TILE)) & 7u) + 8u * k;
         m.step = 8u * K;
         m.n_t = m.c_first < n_tiles ? (n_tiles - 1u - m.c_first) / m.step + 1u : 0u;
+    } else if (DDS_TAIL) {
+        // 1-D grid: channels [0, n - tail_ch) in p.stripes stripes each, then
+        // the last tail_ch channels in tail_stripes short stripes each
+        const uint32_t g = blockIdx.x, n_long = (p.n_channels - p.tail_ch) * p.stripes;
+        uint32_t stripe, stripes;
+        if (g < n_long) {
+            m.ch = g / p.stripes;
+            stripe = g - m.ch * p.stripes;
+            stripes = p.stripes;
+        } else {
+            const uint32_t g2 = g - n_long, q = g2 / p.tail_stripes;
+            m.ch = p.n_channels - p.tail_ch + q;
+            stripe = g2 - q * p.tail_stripes;
+            stripes = p.tail_stripes;
+        }
+        if (DDS_ORDER_ELEM) m.ch = p.ch_order[m.ch];
+        m.off = 0;
+        m.c_first = stripe;
+        m.step = stripes;
+        m.n_t = stripe < p.tiles ? (p.tiles - stripe + stripes - 1) / stripes : 0u;
     } else {
 #if DDS_STRIPE_ORDER == 1          // A/B: channels in a scrambled dispatch order (resident WGs far apart)
         m.ch = (uint32_t)(((uint64_t)blockIdx.y * 1000003ull) % p.n_channels);
@@ -343,7 +365,7 @@ __device__ __forceinline__ TileMap tile_map(const DDSParams &p)
         m.ch = blockIdx.x;
         const uint32_t stripe = blockIdx.y, stripes = gridDim.y;
 #else
-        m.ch = blockIdx.y;
+        m.ch = DDS_ORDER_ELEM ? p.ch_order[blockIdx.y] : blockIdx.y;
         const uint32_t stripe = blockIdx.x, stripes = gridDim.x;
 #endif
         m.off = 0;
@@ -650,6 +672,10 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
     uint4 *s_xpose = reinterpret_cast<uint4 *>(s_freq + p.freq_lds);   // DDS_XPOSE_BYTES, 16-B aligned
 
     const uint32_t tid = threadIdx.x;
+#ifdef DDS_PROBE_TIMES                                              // diagnostic build: workgroup timeline
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
     const TileMap M = tile_map(p);
     if (M.n_t == 0) return;                          // (workgroup-uniform)
     const uint32_t ch = M.ch, n_t = M.n_t;
@@ -709,6 +735,18 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
         tile_sweep(p, L, d, M, quad, s_st, st_lo, s_rs_t, rs_lo);
     else
         tile_sweep(p, L, d, M, quad, xs, 0u, xr, 0u);
+#ifdef DDS_PROBE_TIMES
+    __syncthreads();
+    if (tid == 0 && p.probe) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+        const uint64_t wg = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        p.probe[3 * wg] = t_start;
+        p.probe[3 * wg + 1] = t_end;
+        p.probe[3 * wg + 2] = (uint64_t)hw | ((uint64_t)xcc << 32) | ((uint64_t)ch << 40);
+    }
+#endif
 }
 
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
@@ -727,6 +765,7 @@ hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
     if (e != hipSuccess) return e;
     const dim3 grid = DDS_XCD_BAL ? dim3(p.n_channels * 9u)
                     : DDS_XCD ? dim3(p.n_channels * 8u * p.stripes)
+                    : DDS_TAIL ? dim3((p.n_channels - p.tail_ch) * p.stripes + p.tail_ch * p.tail_stripes)
                     : DDS_STRIPE_ORDER == 2 ? dim3(p.n_channels, p.stripes) : dim3(p.stripes, p.n_channels);
     hipLaunchKernelGGL(dds_tile_kernel, grid, dim3(BLOCK), lds, stream, p);
     return hipGetLastError();

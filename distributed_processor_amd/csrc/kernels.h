@@ -215,6 +215,7 @@ struct DDSParams {
     const uint32_t *env, *freq;
     const int16_t *sin_lut;        // Q15 sine table [4096]
     const uint32_t *ch;            // per-channel descriptors, DDS_CH_WORDS u32 each
+    const uint32_t *ch_order;      // the tile kernel's channel dispatch order (capi.cpp dds_channel_order)
     uint32_t *iq;                  // [n_channels][n_samples] packed {I16 low, Q16 high}
     uint32_t n_channels, n_lanes, n_samples, event_cap;
     uint32_t ev_lds;               // compacted-event slots per channel (>= event_cap, multiple of 8)
@@ -223,10 +224,12 @@ struct DDSParams {
     uint32_t tiles;                // tile windows per channel (DDS_TILE samples each; dds_tile_off)
     uint32_t stripes;              // DDS_XCD: workgroups per (channel, block residue); else per channel
     uint32_t wg_tiles;             // most tiles one workgroup sweeps (its LDS window slots)
+    uint32_t tail_ch, tail_stripes; // DDS_TAIL: the last tail_ch channels in tail_stripes short stripes
     // event index (dds_index_kernel -> dds_tile_kernel)
     uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
     uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
     uint4 *win;                    // [n_channels][tiles] {strobe lo, count, reset lo, count}
+    unsigned long long *probe;     // diagnostic builds only (DDS_PROBE_TIMES): per-workgroup stamps, else null
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
 constexpr uint32_t DDS_MAX_EVENTS = 1024;
@@ -247,6 +250,21 @@ constexpr bool DDS_XCD_BAL = DPEMU_DDS_XCD == 2;
 #define DPEMU_DDS_ZERO 0
 #endif
 constexpr bool DDS_ZERO_TILES = DPEMU_DDS_ZERO;   // all-zero wave tiles skip the transpose (A/B: -DDPEMU_DDS_ZERO=0)
+// dispatch channels grouped by element (ch_order) instead of in channel order (A/B: -DDPEMU_DDS_ORDER=0)
+#ifndef DPEMU_DDS_ORDER
+#define DPEMU_DDS_ORDER 0
+#endif
+constexpr bool DDS_ORDER_ELEM = DPEMU_DDS_ORDER;
+// stripes: the workgroups dispatched last are short (DDS_TAIL_TILES tiles),
+// so the launch's tail is one short workgroup long (A/B: -DDPEMU_DDS_TAIL=0)
+#ifndef DPEMU_DDS_TAIL
+#define DPEMU_DDS_TAIL 0
+#endif
+constexpr bool DDS_TAIL = DPEMU_DDS_TAIL && !DPEMU_DDS_XCD;
+#ifndef DPEMU_DDS_TAIL_TILES
+#define DPEMU_DDS_TAIL_TILES 4
+#endif
+constexpr uint32_t DDS_TAIL_TILES = DPEMU_DDS_TAIL_TILES;
 #ifndef DPEMU_DDS_K
 #define DPEMU_DDS_K 1
 #endif
