@@ -52,27 +52,30 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s
-PROFILE_TAG = 'r03'            # profiles/<tag>_*: rocprofv3 kernel stats and PMC passes of this bench
+PROFILE_TAG = 'r04'            # profiles/<tag>_*: rocprofv3 kernel stats and PMC passes of this bench
 
 
 def _valu_peak():
     """the measured wave64 integer-VALU issue peak (instructions/s, whole chip)
     and its cycles per instruction: scripts/micro/valu_peak.hip under
     rocprofv3 with SQ_INSTS_VALU + GRBM_GUI_ACTIVE in one pass
-    (profiles/r03_valu_peak_pmc.json, scripts/valu_peak_summary.py)"""
-    with open(os.path.join(REPO, 'profiles', 'r03_valu_peak_pmc.json')) as f:
+    (profiles/r04_valu_peak_pmc.json, scripts/valu_peak_summary.py)"""
+    with open(os.path.join(REPO, 'profiles', 'r04_valu_peak_pmc.json')) as f:
         v = json.load(f)
     return v['peak_valu_insts_per_s'], v['peak_cycles_per_inst'], v['peak_variant']
 
 
 VALU_PEAK, VALU_CPI, VALU_PEAK_VARIANT = _valu_peak()
+# where the profile summaries are read from: the committed profiles/, or
+# (DPEMU_BENCH_PROFILES) the summaries of a profile pass just taken on the same box
+PROFILE_DIR = os.environ.get('DPEMU_BENCH_PROFILES') or os.path.join(REPO, 'profiles')
 
 
 def _kernel_valu_peaks():
     """each bench kernel's own VALU issue peak: its opcode mix weighted by the
     measured per-opcode issue costs (scripts/kernel_mixes.sh ->
     profiles/<tag>_kernel_valu_peaks.json); {readable name: record}"""
-    path = os.path.join(REPO, 'profiles', '{}_kernel_valu_peaks.json'.format(PROFILE_TAG))
+    path = os.path.join(PROFILE_DIR, '{}_kernel_valu_peaks.json'.format(PROFILE_TAG))
     if not os.path.exists(path):
         return {}
     with open(path) as f:
@@ -86,9 +89,6 @@ def kernel_key(name):
     """'void dpemu::branch_kernel<11, 8>(dpemu::KParams)' -> 'branch_kernel<11,8>'"""
     n = (name or '').split('(')[0].replace('void ', '').replace('dpemu::', '').replace(' ', '')
     return n
-# where they are read from: the committed profiles/, or (DPEMU_BENCH_PROFILES)
-# the summaries of a profile pass just taken on the same box
-PROFILE_DIR = os.environ.get('DPEMU_BENCH_PROFILES') or os.path.join(REPO, 'profiles')
 
 
 # ---------------------------------------------------------------------------- helpers
@@ -188,7 +188,7 @@ def valu_view(prof, kernel_ms=None, instrs=None):
          'peak_cycles_per_inst': own['cycles_per_inst'] if own else VALU_CPI,
          'peak_source': ('profiles/{}_kernel_valu_peaks.json (the kernel\'s own opcode mix at the measured '
                          'per-opcode issue costs, {:.2f} GHz)'.format(PROFILE_TAG, own['clock_ghz']) if own else
-                         'profiles/r03_valu_peak_pmc.json ({})'.format(VALU_PEAK_VARIANT)),
+                         'profiles/r04_valu_peak_pmc.json ({})'.format(VALU_PEAK_VARIANT)),
          'uniform_peak': VALU_PEAK, 'valu_insts_per_launch': n}
     if kernel_ms:
         v['achieved'] = n / (kernel_ms * 1e-3)

@@ -20,7 +20,7 @@ writes <dest>/<tag>_<kernel>_pmc.json with per-launch means:
   puts GRBM_GUI_ACTIVE in both SQ passes), then averaged over dispatches:
     valu_issue_pct   SQ_INSTS_VALU x c / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs),
                      c = the measured cycles per wave64 integer-VALU
-                     instruction at the issue peak (profiles/r03_valu_peak_pmc.json)
+                     instruction at the issue peak (profiles/r04_valu_peak_pmc.json)
     (SQ_ACTIVE_INST_VALU equals SQ_INSTS_VALU on the peak microbenchmark, so
     a 'busy' ratio of it at an assumed 4 cycles per instruction overstates the
     VALU share wherever the kernel issues faster than 4; it is not reported)
@@ -53,7 +53,7 @@ def valu_peak():
     """the measured wave64 integer-VALU issue peak (instructions/s, whole chip)
     and its cycles per instruction per SIMD: scripts/micro/valu_peak.hip under
     rocprofv3, summarised by scripts/valu_peak_summary.py"""
-    with open(os.path.join(REPO, 'profiles', 'r03_valu_peak_pmc.json')) as f:
+    with open(os.path.join(REPO, 'profiles', 'r04_valu_peak_pmc.json')) as f:
         v = json.load(f)
     return v['peak_valu_insts_per_s'], v['peak_cycles_per_inst']
 
