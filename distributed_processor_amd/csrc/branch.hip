@@ -207,7 +207,12 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // draw the measurement.  Overflow flags come from the final counts.
     auto emit = [&](bool ok, uint32_t te, uint32_t kind) __attribute__((always_inline)) {
         if (ok) {
+#ifdef BRANCH_STORE_DIRECT                               // A/B: every record stored as it arises (no row holding)
+            if (n_ev < p.event_cap && p.events) ev_lane[(uint64_t)n_ev * n_lanes] = event_record(te, pe, pp, pa, kind);
+            if (false) {
+#else
             if (n_ev < p.event_cap && p.events) {
+#endif
                 const uint4 rec = event_record(te, pe, pp, pa, kind);
                 const bool full = n_ev - n_st == 2u;    // the oldest goes out now
                 if (full) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
@@ -283,6 +288,9 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 
     // store the pending rows every unfinished lane has passed (all: at the end)
     auto flush_rows = [&](bool all) __attribute__((always_inline)) {
+#ifdef BRANCH_STORE_DIRECT
+        return;
+#endif
         if (!p.events) return;
         const uint32_t ne = min(n_ev, p.event_cap);
         if (!__any(ne > n_st)) return;

@@ -689,7 +689,12 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
     const uint4 w_first = gwin[M.tile(0)], w_last = gwin[M.tile(n_t - 1)];
     const uint32_t st_lo = w_first.x, st_n = w_last.x + w_last.y - st_lo;
     const uint32_t rs_lo = w_first.z, rs_n = w_last.z + w_last.w - rs_lo;
+#ifdef DDS_PROBE_GLOBAL_RECORDS                                    // A/B: no record staging, the sweep reads the index
+    const bool fits = false;
+    (void)st_n; (void)rs_n;
+#else
     const bool fits = st_n <= p.rec_lds && rs_n <= p.rec_lds;    // workgroup-uniform
+#endif
 
     // prologue: every global load of the workgroup up front
     if (tid < DDS_LUT_BYTES / 16)                                      // entries 0..1031 (1024 needed)
