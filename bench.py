@@ -735,7 +735,9 @@ def main():
     ap.add_argument('--shots', type=int, default=10 ** 6, help='config-2 shots per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
-    ap.add_argument('--dds-depth', type=int, default=8, help='DDS batches in flight (dds.SynthesisPipeline)')
+    ap.add_argument('--dds-depth', type=int, default=8,
+                    help='DDS batches in flight (dds.SynthesisPipeline; streams beyond the 4 hardware queues '
+                         'share them, so at most 4 execute at once)')
     ap.add_argument('--rb-depth', type=int, default=2, help='config-4 batches in flight (emulator.RunPipeline)')
     ap.add_argument('--ar-shots', type=int, default=1250000, help='config-3 shots per GPU per step')
     ap.add_argument('--rb-seqs', type=int, default=100000, help='config-4 RB sequences')

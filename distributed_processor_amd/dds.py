@@ -112,6 +112,11 @@ class SynthesisPipeline:
     k % depth: batch k + 1's index kernel runs beside batch k's tile kernel
     (config 5 whole step 0.329 -> 0.317 ms, ``profiles/r03_dds_pipe.json``).
 
+    Streams beyond the process's hardware queues (``GPU_MAX_HW_QUEUES``, 4 by
+    default) share them: at most 4 batches execute at once, the others wait
+    on their queue behind one; depth 8 keeps every queue's
+    next batch ready.
+
     ``synthesize`` makes its stream wait for the caller's current stream (the
     producer of ``outputs``) and returns (iq, stream): iq is valid on that
     stream, and is overwritten by the call ``depth`` batches later, so a
