@@ -50,6 +50,15 @@ namespace {
 
 enum : uint32_t { B_RUN = 0, B_SYNC = 1, B_LUT = 2, B_FIN = 3 };
 
+// event records stored as they arise (1) or held as whole wave rows (0), per
+// back end (A/B knobs: -DDPEMU_BRANCH_DIRECT=, -DDPEMU_BRANCH_DIRECT_LUT=)
+#ifndef DPEMU_BRANCH_DIRECT
+#define DPEMU_BRANCH_DIRECT 0
+#endif
+#ifndef DPEMU_BRANCH_DIRECT_LUT
+#define DPEMU_BRANCH_DIRECT_LUT 1
+#endif
+
 // decode-to-decode latency per op4 past the command's base cycle (D, the
 // trigger cycle tT for pulse-with-trigger / idle, the fproc ready cycle R):
 // pulse 3, reg_alu / jump_i / inc_qclk / alu_fproc 4, jump_cond / jump_fproc 6
@@ -115,6 +124,13 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     constexpr bool REGS = (FEAT & FEAT_REGS) != 0;  // some command writes the reg_file (else it reads 0)
     constexpr bool PLDS = (FEAT & FEAT_PROG_LDS) != 0;   // the workgroup's programs staged in LDS
     constexpr int MT = XMEAS ? MEAS_LOOKUP : 1;
+    // event records stored as they arise (DIRECT) or held and stored as whole
+    // wave rows (below).  Measured per back end (same-process A/Bs, outputs
+    // identical; profiles/r04_branch_direct_ab.jsonl): config 3 (fproc_meas)
+    // 0.446 ms held vs 0.480 direct; config 3 through the LUT 0.564 held vs
+    // 0.494 direct -- the row bookkeeping's VALU costs more there than the
+    // scattered partial rows it avoids
+    constexpr bool DIRECT = LUT ? DPEMU_BRANCH_DIRECT_LUT != 0 : DPEMU_BRANCH_DIRECT != 0;
     constexpr int NF = LUT ? LUT_FIRE_CAP : 1;
 
     __shared__ uint32_t s_regs[REGS ? 16 : 1][REGS ? BLOCK : 1];
@@ -207,12 +223,9 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // draw the measurement.  Overflow flags come from the final counts.
     auto emit = [&](bool ok, uint32_t te, uint32_t kind) __attribute__((always_inline)) {
         if (ok) {
-#ifdef BRANCH_STORE_DIRECT                               // A/B: every record stored as it arises (no row holding)
-            if (n_ev < p.event_cap && p.events) ev_lane[(uint64_t)n_ev * n_lanes] = event_record(te, pe, pp, pa, kind);
-            if (false) {
-#else
-            if (n_ev < p.event_cap && p.events) {
-#endif
+            if (DIRECT && n_ev < p.event_cap && p.events)
+                ev_lane[(uint64_t)n_ev * n_lanes] = event_record(te, pe, pp, pa, kind);
+            if (!DIRECT && n_ev < p.event_cap && p.events) {
                 const uint4 rec = event_record(te, pe, pp, pa, kind);
                 const bool full = n_ev - n_st == 2u;    // the oldest goes out now
                 if (full) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
@@ -288,10 +301,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 
     // store the pending rows every unfinished lane has passed (all: at the end)
     auto flush_rows = [&](bool all) __attribute__((always_inline)) {
-#ifdef BRANCH_STORE_DIRECT
-        return;
-#endif
-        if (!p.events) return;
+        if (DIRECT || !p.events) return;
         const uint32_t ne = min(n_ev, p.event_cap);
         if (!__any(ne > n_st)) return;
         const uint32_t done = all ? INF32 : wave_min(mode == B_FIN ? INF32 : ne);
