@@ -305,14 +305,17 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         const uint32_t ne = min(n_ev, p.event_cap);
         if (!__any(ne > n_st)) return;
         const uint32_t done = all ? INF32 : wave_min(mode == B_FIN ? INF32 : ne);
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            const bool f = n_st < ne && n_st < done;
-            if (!__any(f)) break;                    // most iterations complete no row
-            if (f) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
-            pend0 = sel4(f, pend1, pend0);
-            n_st += f ? 1u : 0u;
+        // the held records [n_st, ne) are pend0, pend1: store the rows every
+        // unfinished lane has passed, then shift once (not once per row)
+        const bool f1 = n_st < ne && n_st < done;
+        if (!__any(f1)) return;                      // most iterations complete no row
+        const bool f2 = f1 && n_st + 1u < ne && n_st + 1u < done;
+        if (f1) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
+        if (__any(f2)) {
+            if (f2) ev_lane[(uint64_t)(n_st + 1u) * n_lanes] = pend1;
         }
+        pend0 = sel4(f1 && !f2, pend1, pend0);
+        n_st += (f1 ? 1u : 0u) + (f2 ? 1u : 0u);
     };
 
     // One lockstep iteration: every running lane retires at most one command.
