@@ -926,6 +926,9 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
         p.tiles = (p.n_samples + DDS_TILE - 1) / DDS_TILE;
         p.stripes = std::max<uint32_t>(1, std::min<uint32_t>(p.tiles, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE));
         p.wg_tiles = (p.tiles + p.stripes - 1) / p.stripes;
+        p.zw = std::max<uint32_t>(1u, ctx->n_cu * DPEMU_DDS_ZW_PER_CU);
+        if (DDS_ZFILL && (uint64_t)p.n_channels * p.tiles + (uint64_t)p.zw * DDS_ZB >= (1ull << 32))
+            return fail(ctx, DPEMU_E_INVALID, "DDS: channels x tiles too large");
         if (DDS_TAIL) {
             // one round of resident workgroups' worth of short stripes at the end:
             // the device's CUs x 7 resident tile workgroups x DDS_TAIL_TILES tiles

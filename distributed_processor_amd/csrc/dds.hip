@@ -189,10 +189,12 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
     __shared__ uint32_t s_cnt[2][BLOCK / 64];
     uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn);
     uint32_t *s_rs_t = s_st_t + p.ev_lds;
+    uint32_t *s_st_end = s_rs_t + p.ev_lds;          // DDS_ZFILL: a strobe's last playing sample + 1
     const uint32_t tid = threadIdx.x, wl = tid & 63u, wv = tid >> 6;
     const uint32_t ch = blockIdx.x;
     const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
     const uint32_t lane = d[0], elem = d[1] & 3u, spc = d[2];
+    const uint32_t interp = d[3] ? d[3] : 1u, env_len = d[5];
     const uint32_t n_ev = min(p.summary[8ull * lane + 2], p.event_cap);
     uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
     uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
@@ -232,6 +234,15 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
             const uint32_t i = os + (uint32_t)__popcll(bs & below);
             xs[i] = make_uint4(ev[k].x, ev[k].y & 0xFFFFFFu, ev[k].z, ev[k].w & 0xFFFFu);
             s_st_t[i] = ev[k].x;
+            if (DDS_ZFILL) {
+                // samples [t spc, end) can play: the pulse's envelope inside the
+                // table (the sweeps' lim), forever for a CW envelope (Lw = 0)
+                const uint32_t A = ev[k].y & 0xFFFu, Lw = (ev[k].y >> 12) & 0xFFFu;
+                const uint32_t room = env_len > 4 * A ? env_len - 4 * A : 0u;
+                const uint64_t lim = Lw ? (uint64_t)min(4 * Lw, room) * interp : (room ? ~0ull >> 1 : 0ull);
+                const uint64_t e64 = (uint64_t)ev[k].x * spc + lim;
+                s_st_end[i] = e64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)e64;
+            }
         }
         if (is_rs[k]) {
             const uint32_t i = orr + (uint32_t)__popcll(br & below);
@@ -254,7 +265,14 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
         const int a0 = last_le(s_st_t, (int)n_st, n0) + 1, a1 = last_le(s_st_t, (int)n_st, n1) + 1;
         const int b0 = last_le(s_rs_t, (int)n_rs, n0) + 1, b1 = last_le(s_rs_t, (int)n_rs, n1) + 1;
         const int sl = max(a0 - 1, 0), rl = max(b0 - 1, 0);
-        p.win[(uint64_t)ch * p.tiles + c] = make_uint4((uint32_t)sl, (uint32_t)(a1 - sl), (uint32_t)rl,
+        // DDS_ZFILL: the tile plays nothing unless one of its window's strobes
+        // can play a sample inside it (bit 31 of the count: live)
+        uint32_t live = DDS_ZFILL ? 0u : WIN_LIVE;
+        if (DDS_ZFILL) {
+            for (int k = sl; k < a1 && !live; k++)
+                live = ((uint64_t)s_st_t[k] * spc <= j1 && s_st_end[k] > j0) ? WIN_LIVE : 0u;
+        }
+        p.win[(uint64_t)ch * p.tiles + c] = make_uint4((uint32_t)sl, (uint32_t)(a1 - sl) | live, (uint32_t)rl,
                                                       (uint32_t)(b1 - rl));
     }
 }
@@ -301,9 +319,18 @@ struct TileMap {
     __device__ __forceinline__ int32_t first(uint32_t i) const { return (int32_t)(tile(i) * DDS_TILE) - (int32_t)off; }
 };
 
-__device__ __forceinline__ TileMap tile_map(const DDSParams &p)
+__device__ __forceinline__ TileMap tile_map(const DDSParams &p, uint32_t sidx)
 {
     TileMap m;
+    if (DDS_ZFILL) {                 // stripe workgroup sidx (channel-major) behind the zero workers
+        m.ch = sidx / p.stripes;
+        const uint32_t stripe = sidx - m.ch * p.stripes;
+        m.off = 0;
+        m.c_first = stripe;
+        m.step = p.stripes;
+        m.n_t = (p.tiles - stripe + p.stripes - 1) / p.stripes;
+        return m;
+    }
     if (DDS_XCD_BAL) {
         // residue workgroups g < 8 n_ch: (ch, r) takes the residue-r tiles
         // c = c0 + 8 j, j < M, M = the channel's tiles / 8 rounded down to a
@@ -383,6 +410,34 @@ __device__ __forceinline__ TileMap tile_map(const DDSParams &p)
     return m;
 }
 
+// DDS_ZFILL: zero worker z of zw writes the silent tiles g = z + k zw of
+// the flattened [channel][tile] order (the workers sweep the buffer front to
+// back together, the fill shape).  The silent flags of a batch of DDS_ZB
+// tiles are read into LDS first, so the store loop waits on no load (vmcnt
+// counts stores and loads in order: a load behind stores would wait for them).
+__device__ __forceinline__ void zero_tiles(const DDSParams &p, uint8_t *s_z, uint32_t z)
+{
+    const uint32_t n_g = p.n_channels * p.tiles, tid = threadIdx.x;    // (< 2^32: launch_dds)
+    const u32x4 zero = {0u, 0u, 0u, 0u};
+#pragma unroll 1
+    for (uint32_t g0 = z; g0 < n_g; g0 += p.zw * DDS_ZB) {
+        for (uint32_t i = tid; i < DDS_ZB; i += BLOCK) {
+            const uint32_t g = g0 + i * p.zw;
+            s_z[i] = g < n_g && !(p.win[g].y & WIN_LIVE);
+        }
+        __syncthreads();
+        uint32_t ch = g0 / p.tiles, c = g0 - ch * p.tiles;
+#pragma unroll 1
+        for (uint32_t i = 0; i < DDS_ZB && ch < p.n_channels; i++) {
+            const uint32_t j = c * DDS_TILE + 4 * tid;
+            if (s_z[i] && j < p.n_samples) *reinterpret_cast<u32x4 *>(p.iq + (uint64_t)ch * p.n_samples + j) = zero;
+            c += p.zw;
+            while (c >= p.tiles) { c -= p.tiles; ch++; }
+        }
+        __syncthreads();
+    }
+}
+
 // the LDS-resident part of a tile workgroup
 struct TileLds {
     const int16_t *lut;
@@ -416,7 +471,9 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
             const int32_t tb = M.first(i);                                  // the tile's first sample (16 | tb)
             const int32_t js = tb + 16 * (int32_t)ln;                       // this lane's cycle n = js / 16
             const uint32_t n = (uint32_t)js >> 4;
-            const uint4 w = L.win[i];
+            uint4 w = L.win[i];
+            if (DDS_ZFILL && !(w.y & WIN_LIVE)) continue;                   // a zero worker writes it
+            w.y &= ~WIN_LIVE;
             uint32_t v[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) v[q] = 0u;
@@ -542,7 +599,9 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
         const int32_t js = M.first(i) + 4 * (int32_t)tid;
         if (js < 0 || (uint32_t)js >= p.n_samples) continue;
         const uint32_t j0 = (uint32_t)js;
-        const uint4 w = L.win[i];
+        uint4 w = L.win[i];
+        if (DDS_ZFILL && !(w.y & WIN_LIVE)) continue;
+        w.y &= ~WIN_LIVE;
         uint32_t v[4] = {0u, 0u, 0u, 0u};
         if (quad) {
             const uint32_t n = j0 >> spc_sh;                         // the thread's 4 samples share cycle n
@@ -676,7 +735,22 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_waitcnt(0xC07F);
 #endif
-    const TileMap M = tile_map(p);
+    uint32_t sidx = blockIdx.x;
+    if (DDS_ZFILL) {
+        // the first zw workgroups in dispatch order are zero workers
+        // (zero_tiles): a few slots for the whole zero part
+        if (blockIdx.x < p.zw) {
+#ifndef DDS_PROBE_SONLY
+            zero_tiles(p, s_dyn, blockIdx.x);
+#endif
+            return;
+        }
+        sidx = blockIdx.x - p.zw;
+#ifdef DDS_PROBE_ZONLY
+        if (p.event_cap != 12345u) return;
+#endif
+    }
+    const TileMap M = tile_map(p, sidx);
     if (M.n_t == 0) return;                          // (workgroup-uniform)
     const uint32_t ch = M.ch, n_t = M.n_t;
     const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
@@ -686,7 +760,9 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
     const bool staged = (interp == 1 ? dds_env_pairs_words(env_len) : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds;
     const uint4 *gwin = p.win + (uint64_t)ch * p.tiles;
     // the workgroup's strobes / resets: from its first tile's window to its last's end
-    const uint4 w_first = gwin[M.tile(0)], w_last = gwin[M.tile(n_t - 1)];
+    uint4 w_first = gwin[M.tile(0)], w_last = gwin[M.tile(n_t - 1)];
+    w_first.y &= ~WIN_LIVE;
+    w_last.y &= ~WIN_LIVE;
     const uint32_t st_lo = w_first.x, st_n = w_last.x + w_last.y - st_lo;
     const uint32_t rs_lo = w_first.z, rs_n = w_last.z + w_last.w - rs_lo;
 #ifdef DDS_PROBE_GLOBAL_RECORDS                                    // A/B: no record staging, the sweep reads the index
@@ -727,7 +803,7 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
         for (uint32_t i = tid; i < st_n; i += BLOCK) s_st[i] = xs[st_lo + i];
         for (uint32_t i = tid; i < rs_n; i += BLOCK) s_rs_t[i] = xr[rs_lo + i];
     }
-    for (uint32_t i = tid; i < n_t; i += BLOCK) s_win[i] = gwin[M.tile(i)];
+    for (uint32_t i = tid; i < n_t; i += BLOCK) s_win[i] = gwin[M.tile(i)];   // (.y bit 31: live)
     bad = __syncthreads_or(bad);
 #ifdef DDS_PROBE_NOSWEEP                                            // A/B probe only: the prologue alone
     if (p.event_cap == 12345u) p.iq[tid] = s_win[tid & 7].x ^ s_st[tid & 7].y ^ s_env[tid] ^ (uint32_t)s_lut[tid];
@@ -746,7 +822,7 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         __builtin_amdgcn_s_waitcnt(0xC07F);
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
-        const uint64_t wg = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        const uint64_t wg = DDS_ZFILL ? (uint64_t)sidx : (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;   // < n_wg
         p.probe[3 * wg] = t_start;
         p.probe[3 * wg + 1] = t_end;
         p.probe[3 * wg + 2] = (uint64_t)hw | ((uint64_t)xcc << 32) | ((uint64_t)ch << 40);
@@ -757,8 +833,8 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    // the channel's strobe and reset times: 2 * ev_lds words <= 8 KiB
-    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), 2 * p.ev_lds * 4, stream, p);
+    // the channel's strobe and reset times (and strobe ends): 3 * ev_lds words <= 12 KiB
+    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), 3 * p.ev_lds * 4, stream, p);
     return hipGetLastError();
 }
 
@@ -768,7 +844,8 @@ hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
     const uint32_t lds = dds_lds_bytes(p.rec_lds, p.wg_tiles, p.env_lds, p.freq_lds);
     const hipError_t e = opt_in_dynamic_lds(reinterpret_cast<const void *>(dds_tile_kernel), lds);
     if (e != hipSuccess) return e;
-    const dim3 grid = DDS_XCD_BAL ? dim3(p.n_channels * 9u)
+    const dim3 grid = DDS_ZFILL ? dim3(p.zw + p.stripes * p.n_channels)
+                    : DDS_XCD_BAL ? dim3(p.n_channels * 9u)
                     : DDS_XCD ? dim3(p.n_channels * 8u * p.stripes)
                     : DDS_TAIL ? dim3((p.n_channels - p.tail_ch) * p.stripes + p.tail_ch * p.tail_stripes)
                     : DDS_STRIPE_ORDER == 2 ? dim3(p.n_channels, p.stripes) : dim3(p.stripes, p.n_channels);

@@ -225,6 +225,7 @@ struct DDSParams {
     uint32_t stripes;              // DDS_XCD: workgroups per (channel, block residue); else per channel
     uint32_t wg_tiles;             // most tiles one workgroup sweeps (its LDS window slots)
     uint32_t tail_ch, tail_stripes; // DDS_TAIL: the last tail_ch channels in tail_stripes short stripes
+    uint32_t zw;                    // DDS_ZFILL: zero worker workgroups (first in dispatch order)
     // event index (dds_index_kernel -> dds_tile_kernel)
     uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
     uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
@@ -265,6 +266,18 @@ constexpr bool DDS_TAIL = DPEMU_DDS_TAIL && !DPEMU_DDS_XCD;
 #define DPEMU_DDS_TAIL_TILES 4
 #endif
 constexpr uint32_t DDS_TAIL_TILES = DPEMU_DDS_TAIL_TILES;
+// A/B (build-time, -DDPEMU_DDS_ZFILL=1): the index marks each
+// tile live or silent, zw zero-worker workgroups (first in dispatch order)
+// write the silent tiles, the stripe workgroups only the live ones
+#ifndef DPEMU_DDS_ZFILL
+#define DPEMU_DDS_ZFILL 0
+#endif
+constexpr bool DDS_ZFILL = DPEMU_DDS_ZFILL && !DPEMU_DDS_XCD && !DPEMU_DDS_TAIL;
+#ifndef DPEMU_DDS_ZW_PER_CU
+#define DPEMU_DDS_ZW_PER_CU 1
+#endif
+constexpr uint32_t DDS_ZB = 1024;           // silent flags per zero-worker batch (LDS bytes <= DDS_LUT_BYTES)
+constexpr uint32_t WIN_LIVE = 0x80000000u;   // tile window .y bit 31: some sample of the tile can play
 #ifndef DPEMU_DDS_K
 #define DPEMU_DDS_K 1
 #endif
