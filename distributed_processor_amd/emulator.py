@@ -13,6 +13,7 @@ traces, measurements and outcome histograms.
 from __future__ import annotations
 
 import ctypes as C
+import math
 from typing import Dict, Iterable, List, Optional, Sequence, Union
 
 import numpy as np
@@ -412,13 +413,15 @@ def _check_tensor(name, t, spec, device):
         raise DpemuError('{}: expected a torch tensor'.format(name))
     if name in ('hist', 'hist_next') and len(shape) == 2 and shape[1] > 4096:
         raise DpemuError('{} needs cores_per_shot <= 12'.format(name))
-    if t.device.type != 'cuda' or (t.device.index if t.device.index is not None else 0) != device:
+    # (cheap attribute calls only: this runs for every output of every launch,
+    # and a bench step of config 1 is 27 us of GPU time)
+    if not t.is_cuda or t.get_device() != device:
         raise DpemuError('{}: tensor on {} but the emulator runs on cuda:{}'.format(name, t.device, device))
-    if t.element_size() != torch.empty((), dtype=dtype).element_size() or t.is_floating_point():
+    if t.element_size() != dtype.itemsize or t.is_floating_point():
         raise DpemuError('{}: dtype {} (want {})'.format(name, t.dtype, dtype))
     if not t.is_contiguous():
         raise DpemuError('{}: tensor must be contiguous'.format(name))
-    if t.numel() != int(np.prod(shape)):
+    if t.numel() != math.prod(shape):
         raise DpemuError('{}: {} elements, the run writes {} ({})'.format(name, t.numel(), int(np.prod(shape)),
                                                                         tuple(shape)))
 
