@@ -833,8 +833,8 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    // the channel's strobe and reset times (and strobe ends): 3 * ev_lds words <= 12 KiB
-    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), 3 * p.ev_lds * 4, stream, p);
+    // the channel's strobe and reset times (DDS_ZFILL: and strobe ends): 2 (3) * ev_lds words <= 8 (12) KiB
+    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), (DDS_ZFILL ? 3 : 2) * p.ev_lds * 4, stream, p);
     return hipGetLastError();
 }
 
