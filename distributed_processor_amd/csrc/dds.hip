@@ -391,6 +391,16 @@ __device__ __forceinline__ TileMap tile_map(const DDSParams &p, uint32_t sidx)
 #elif DDS_STRIPE_ORDER == 2        // A/B: grid (channels, stripes): every channel's stripe 0 first
         m.ch = blockIdx.x;
         const uint32_t stripe = blockIdx.y, stripes = gridDim.y;
+#elif DDS_STRIPE_ORDER == 4        // A/B: XCD regions -- XCD x (workgroups g = x mod 8) takes channels
+        // [x n / 8, (x + 1) n / 8), so each XCD writes one contiguous eighth of the I/Q buffer
+        const uint32_t stripes = gridDim.x, g = blockIdx.y * stripes + blockIdx.x;
+        uint32_t stripe = blockIdx.x;
+        m.ch = blockIdx.y;
+        if ((p.n_channels & 7u) == 0u) {
+            const uint32_t x = g & 7u, j = g >> 3, cl = j / stripes;
+            stripe = j - cl * stripes;
+            m.ch = x * (p.n_channels >> 3) + cl;
+        }
 #else
         m.ch = DDS_ORDER_ELEM ? p.ch_order[blockIdx.y] : blockIdx.y;
         const uint32_t stripe = blockIdx.x, stripes = gridDim.x;
