@@ -67,6 +67,77 @@ __global__ void __launch_bounds__(BLOCK) cur_k(uint32_t *iq, uint32_t stripes, u
     }
 }
 
+// (round 4, set "b") the stripes shape with the whole workgroup on each tile
+// (thread t writes 16 B at 4 t of the tile) instead of a wave per tile
+__global__ void __launch_bounds__(BLOCK) curG_k(uint32_t *iq, uint32_t stripes)
+{
+    const uint32_t ch = blockIdx.x / stripes, s = blockIdx.x % stripes;
+    const uint32_t tiles = (NS + 1023) / 1024;
+    uint32_t *out = iq + (uint64_t)ch * NS;
+    const uint32_t n_t = (tiles - s + stripes - 1) / stripes;
+    for (uint32_t i = 0; i < n_t; i++) {
+        const uint32_t j = (s + i * stripes) * 1024 + 4 * threadIdx.x;
+        if (j + 3 < NS) st16(out + j, j);
+    }
+}
+
+// (set "b") the stripes shape with each workgroup starting its tile loop at a
+// workgroup-dependent rotation (ROT: rot = (g * 7) mod n_t; 1: g mod n_t)
+__global__ void __launch_bounds__(BLOCK) curR_k(uint32_t *iq, uint32_t stripes, uint32_t mode)
+{
+    const uint32_t ch = blockIdx.x / stripes, s = blockIdx.x % stripes;
+    const uint32_t tiles = (NS + 1023) / 1024;
+    uint32_t *out = iq + (uint64_t)ch * NS;
+    const uint32_t n_t = (tiles - s + stripes - 1) / stripes;
+    const uint32_t rot = mode == 0 ? (blockIdx.x * 7u) % n_t : blockIdx.x % n_t;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    for (uint32_t i0 = wv; i0 < n_t; i0 += 4) {
+        const uint32_t i = (i0 + rot) % n_t;
+        const uint32_t t = s + i * stripes;
+        for (int r = 0; r < 4; r++) {
+            const uint32_t j = t * 1024 + 4 * (64 * r + ln);
+            if (j + 3 < NS) st16(out + j, j);
+        }
+    }
+}
+
+// (set "b") long-lived fill, rotated: WG b writes its N blocks starting at (b * 7) mod N
+__global__ void __launch_bounds__(BLOCK) blkR_k(uint32_t *iq, uint64_t total, uint32_t N)
+{
+    const uint64_t b0 = (uint64_t)blockIdx.x * N;
+    const uint32_t rot = (blockIdx.x * 7u) % N;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    for (uint32_t i0 = wv; i0 < N; i0 += 4) {
+        const uint32_t i = (i0 + rot) % N;
+        for (int q = 0; q < 4; q++) {
+            const uint64_t j = (b0 + i) * 1024 + 4 * (64 * q + ln);
+            if (j + 3 < total) st16(iq + j, (uint32_t)j);
+        }
+    }
+}
+
+// (set "b") long-lived fill: WG b writes N consecutive global 4-KiB blocks;
+// WAVE: wave w takes blocks w, w + 4, ... (4 x 1-KiB stores each), else the
+// whole workgroup writes each block in turn
+template <bool WAVE>
+__global__ void __launch_bounds__(BLOCK) blk_k(uint32_t *iq, uint64_t total, uint32_t N)
+{
+    const uint64_t b0 = (uint64_t)blockIdx.x * N;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    if (WAVE) {
+        for (uint32_t i = wv; i < N; i += 4)
+            for (int q = 0; q < 4; q++) {
+                const uint64_t j = (b0 + i) * 1024 + 4 * (64 * q + ln);
+                if (j + 3 < total) st16(iq + j, (uint32_t)j);
+            }
+    } else {
+        for (uint32_t i = 0; i < N; i++) {
+            const uint64_t j = (b0 + i) * 1024 + 4 * threadIdx.x;
+            if (j + 3 < total) st16(iq + j, (uint32_t)j);
+        }
+    }
+}
+
 // WG (ch, k, r): global blocks B of channel ch with B % 8 == res, list index i
 // (B = base8 + 8 i + res) with i % K == k (INTERLEAVE) or i in run k (contiguous)
 template <bool WAVE, bool INTERLEAVE>
@@ -145,10 +216,31 @@ static void check_xcc(uint32_t n_wg, void (*launch)(uint32_t *), const char *nam
     fflush(stdout);
 }
 
-int main()
+int main(int argc, char **argv)
 {
     const uint64_t total = (uint64_t)NCH * NS, bytes = total * 4;
     if (hipMalloc(&g_iq, bytes) != hipSuccess) { printf("alloc failed\n"); return 1; }
+    if (argc > 1 && argv[1][0] == 'b') {                 // round-4 set: per-tile granularity, WG lifetime
+        const uint32_t nblk = (uint32_t)((total + 1023) / 1024);
+        for (int rep = 0; rep < 2; rep++) {
+            bench("fill", [&] { fill_k<<<(uint32_t)(total / 4 / BLOCK), BLOCK>>>(g_iq, total); });
+            bench("cur", [&] { cur_k<<<NCH * 13, BLOCK>>>(g_iq, 13, nullptr); });
+            bench("curG", [&] { curG_k<<<NCH * 13, BLOCK>>>(g_iq, 13); });
+            bench("curR7", [&] { curR_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 0); });
+            bench("curR1", [&] { curR_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 1); });
+            bench("blk16R", [&] { blkR_k<<<(nblk + 15) / 16, BLOCK>>>(g_iq, total, 16); });
+            for (uint32_t N : {4u, 16u, 64u}) {
+                g_K = N;
+                char nm[32];
+                snprintf(nm, sizeof nm, "blk%uW", N);
+                bench(nm, [&] { blk_k<true><<<(nblk + g_K - 1) / g_K, BLOCK>>>(g_iq, total, g_K); });
+                snprintf(nm, sizeof nm, "blk%uG", N);
+                bench(nm, [&] { blk_k<false><<<(nblk + g_K - 1) / g_K, BLOCK>>>(g_iq, total, g_K); });
+            }
+        }
+        hipFree(g_iq);
+        return 0;
+    }
     check_xcc(NCH * 8, [](uint32_t *x) { cx_k<true, true><<<NCH * 8, BLOCK>>>(g_iq, 1, 0, x); }, "cx1W");
     check_xcc(NCH * 13, [](uint32_t *x) { cur_k<<<NCH * 13, BLOCK>>>(g_iq, 13, x); }, "cur");
     for (int rep = 0; rep < 2; rep++) {
