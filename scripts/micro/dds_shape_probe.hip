@@ -101,6 +101,29 @@ __global__ void __launch_bounds__(BLOCK) curR_k(uint32_t *iq, uint32_t stripes, 
     }
 }
 
+// (set "b") stripe items (ch, s) = item / 13, item % 13 (the cur shape's
+// workgroups) taken M at a time by one workgroup: WG g does items
+// g M .. g M + M - 1 (curM), or -- persistent, P workgroups -- items g, g + P, ...
+__global__ void __launch_bounds__(BLOCK) curM_k(uint32_t *iq, uint32_t M, uint32_t P)
+{
+    const uint32_t stripes = 13, tiles = (NS + 1023) / 1024, n_items = NCH * stripes;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    const uint32_t i_begin = P ? blockIdx.x : blockIdx.x * M, i_step = P ? P : 1u;
+    const uint32_t i_end = P ? n_items : min(n_items, blockIdx.x * M + M);
+    for (uint32_t it = i_begin; it < i_end; it += i_step) {
+        const uint32_t ch = it / stripes, s = it % stripes;
+        uint32_t *out = iq + (uint64_t)ch * NS;
+        const uint32_t n_t = (tiles - s + stripes - 1) / stripes;
+        for (uint32_t i = wv; i < n_t; i += 4) {
+            const uint32_t t = s + i * stripes;
+            for (int r = 0; r < 4; r++) {
+                const uint32_t j = t * 1024 + 4 * (64 * r + ln);
+                if (j + 3 < NS) st16(out + j, j);
+            }
+        }
+    }
+}
+
 // (set "b") long-lived fill, rotated: WG b writes its N blocks starting at (b * 7) mod N
 __global__ void __launch_bounds__(BLOCK) blkR_k(uint32_t *iq, uint64_t total, uint32_t N)
 {
@@ -226,6 +249,10 @@ int main(int argc, char **argv)
             bench("fill", [&] { fill_k<<<(uint32_t)(total / 4 / BLOCK), BLOCK>>>(g_iq, total); });
             bench("cur", [&] { cur_k<<<NCH * 13, BLOCK>>>(g_iq, 13, nullptr); });
             bench("curG", [&] { curG_k<<<NCH * 13, BLOCK>>>(g_iq, 13); });
+            bench("cur2", [&] { curM_k<<<(NCH * 13 + 1) / 2, BLOCK>>>(g_iq, 2, 0); });
+            bench("cur4", [&] { curM_k<<<(NCH * 13 + 3) / 4, BLOCK>>>(g_iq, 4, 0); });
+            bench("curP2048", [&] { curM_k<<<2048, BLOCK>>>(g_iq, 0, 2048); });
+            bench("curP4096", [&] { curM_k<<<4096, BLOCK>>>(g_iq, 0, 4096); });
             bench("curR7", [&] { curR_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 0); });
             bench("curR1", [&] { curR_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 1); });
             bench("blk16R", [&] { blkR_k<<<(nblk + 15) / 16, BLOCK>>>(g_iq, total, 16); });
