@@ -256,7 +256,7 @@ int main(int argc, char **argv)
             bench("curR7", [&] { curR_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 0); });
             bench("curR1", [&] { curR_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 1); });
             bench("blk16R", [&] { blkR_k<<<(nblk + 15) / 16, BLOCK>>>(g_iq, total, 16); });
-            for (uint32_t N : {4u, 16u, 64u}) {
+            for (uint32_t N : {2u, 4u, 8u, 16u, 32u, 64u, 128u, 256u}) {
                 g_K = N;
                 char nm[32];
                 snprintf(nm, sizeof nm, "blk%uW", N);
