@@ -926,6 +926,13 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
         p.tiles = (p.n_samples + DDS_TILE - 1) / DDS_TILE;
         p.stripes = std::max<uint32_t>(1, std::min<uint32_t>(p.tiles, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE));
         p.wg_tiles = (p.tiles + p.stripes - 1) / p.stripes;
+        if (DDS_PERSIST) {
+            p.wg_tiles = DDS_PB;
+            p.pipc = (p.tiles + DDS_PB - 1) / DDS_PB;
+            const uint64_t n_items = (uint64_t)p.pipc * p.n_channels;
+            if (n_items >= (1ull << 32)) return fail(ctx, DPEMU_E_INVALID, "DDS: too many tile items");
+            p.pgrid = (uint32_t)std::min<uint64_t>(n_items, (uint64_t)ctx->n_cu * DPEMU_DDS_PWG);
+        }
         p.zw = std::max<uint32_t>(1u, ctx->n_cu * DPEMU_DDS_ZW_PER_CU);
         if (DDS_ZFILL && (uint64_t)p.n_channels * p.tiles + (uint64_t)p.zw * DDS_ZB >= (1ull << 32))
             return fail(ctx, DPEMU_E_INVALID, "DDS: channels x tiles too large");

@@ -840,6 +840,95 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
 #endif
 }
 
+// DDS_PERSIST (A/B): the same sweep, persistent workgroups over items of
+// DDS_PB consecutive tiles of one channel, item q = g + k gridDim.x (the
+// resident workgroups work on consecutive items: one advancing front).  The
+// sine table is staged once per workgroup, the envelope / frequency tables
+// again only when an item's tables differ from the previous item's.
+__global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_persist_kernel(const DDSParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    int16_t *s_lut = reinterpret_cast<int16_t *>(s_dyn);
+    uint4 *s_st = reinterpret_cast<uint4 *>(s_dyn + DDS_LUT_BYTES);
+    uint32_t *s_rs_t = reinterpret_cast<uint32_t *>(s_st + p.rec_lds);
+    uint4 *s_win = reinterpret_cast<uint4 *>(s_rs_t + p.rec_lds);
+    uint32_t *s_env = reinterpret_cast<uint32_t *>(s_win + p.wg_tiles);
+    uint32_t *s_freq = s_env + p.env_lds;
+    uint4 *s_xpose = reinterpret_cast<uint4 *>(s_freq + p.freq_lds);
+
+    const uint32_t tid = threadIdx.x;
+    if (tid < DDS_LUT_BYTES / 16)
+        reinterpret_cast<uint4 *>(s_lut)[tid] = reinterpret_cast<const uint4 *>(p.sin_lut)[tid];
+    // the tables now in LDS (env_off, env_len, freq_off, freq_len, interp) and their Y-form flag
+    uint32_t c_eo = ~0u, c_el = 0, c_fo = ~0u, c_fl = 0, c_ip = 0;
+    bool c_bad = false;
+    const uint32_t n_items = p.n_channels * p.pipc;
+#pragma unroll 1
+    for (uint32_t q = blockIdx.x; q < n_items; q += gridDim.x) {
+        TileMap M;
+        M.ch = q / p.pipc;
+        M.c_first = (q - M.ch * p.pipc) * DDS_PB;
+        M.step = 1;
+        M.off = 0;
+        M.n_t = min(DDS_PB, p.tiles - M.c_first);
+        const uint32_t ch = M.ch, n_t = M.n_t;
+        const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
+        const uint32_t spc = d[2], interp = d[3] ? d[3] : 1u;
+        const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
+        const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
+        const bool staged = (interp == 1 ? dds_env_pairs_words(env_len) : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds;
+        const bool same = env_off == c_eo && env_len == c_el && freq_off == c_fo && freq_len == c_fl && interp == c_ip;
+        const uint4 *gwin = p.win + (uint64_t)ch * p.tiles;
+        uint4 w_first = gwin[M.tile(0)], w_last = gwin[M.tile(n_t - 1)];
+        w_first.y &= ~WIN_LIVE;                           // (.y bit 31: the live flag)
+        w_last.y &= ~WIN_LIVE;
+        const uint32_t st_lo = w_first.x, st_n = w_last.x + w_last.y - st_lo;
+        const uint32_t rs_lo = w_first.z, rs_n = w_last.z + w_last.w - rs_lo;
+        const bool fits = st_n <= p.rec_lds && rs_n <= p.rec_lds;
+        __syncthreads();                                  // the previous item's sweep is done with the LDS
+        bool bad = false;
+        if (staged && !same) {
+            if (interp == 1) {
+                for (uint32_t i = tid; i < env_len; i += BLOCK) {
+                    const uint32_t e = p.env[env_off + i];
+                    bad |= (e & 0xFFFFu) == 0x8000u;
+                    *reinterpret_cast<uint2 *>(s_env + env_pair(i)) = make_uint2(e, neg_swap(e));
+                }
+            } else {
+                for (uint32_t i = tid; i < env_len; i += BLOCK) {
+                    const uint32_t e = p.env[env_off + i];
+                    bad |= (e & 0xFFFFu) == 0x8000u;
+                    s_env[i] = e;
+                }
+            }
+            for (uint32_t i = tid; i < freq_len; i += BLOCK) {
+                const uint32_t w = p.freq[freq_off + i];
+                const bool rot = (i & 15u) != 0;
+                bad |= rot && (w & 0xFFFFu) == 0x8000u;
+                reinterpret_cast<uint2 *>(s_freq)[i] = make_uint2(w, rot ? neg_swap(w) : 0u);
+            }
+        }
+        const uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
+        const uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
+        if (fits) {
+            for (uint32_t i = tid; i < st_n; i += BLOCK) s_st[i] = xs[st_lo + i];
+            for (uint32_t i = tid; i < rs_n; i += BLOCK) s_rs_t[i] = xr[rs_lo + i];
+        }
+        for (uint32_t i = tid; i < n_t; i += BLOCK) s_win[i] = gwin[M.tile(i)];
+        bad = __syncthreads_or(bad);
+        if (staged) {
+            if (same) bad = c_bad;
+            c_eo = env_off; c_el = env_len; c_fo = freq_off; c_fl = freq_len; c_ip = interp; c_bad = bad;
+        }
+        const bool quad = staged && !bad && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
+        const TileLds L{s_lut, s_win, s_env, s_freq, s_xpose};
+        if (fits)
+            tile_sweep(p, L, d, M, quad, s_st, st_lo, s_rs_t, rs_lo);
+        else
+            tile_sweep(p, L, d, M, quad, xs, 0u, xr, 0u);
+    }
+}
+
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
@@ -852,6 +941,12 @@ hipError_t launch_dds(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
     const uint32_t lds = dds_lds_bytes(p.rec_lds, p.wg_tiles, p.env_lds, p.freq_lds);
+    if (DDS_PERSIST) {
+        const hipError_t e = opt_in_dynamic_lds(reinterpret_cast<const void *>(dds_tile_persist_kernel), lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(dds_tile_persist_kernel, dim3(p.pgrid), dim3(BLOCK), lds, stream, p);
+        return hipGetLastError();
+    }
     const hipError_t e = opt_in_dynamic_lds(reinterpret_cast<const void *>(dds_tile_kernel), lds);
     if (e != hipSuccess) return e;
     const dim3 grid = DDS_ZFILL ? dim3(p.zw + p.stripes * p.n_channels)

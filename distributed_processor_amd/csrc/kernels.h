@@ -226,6 +226,7 @@ struct DDSParams {
     uint32_t wg_tiles;             // most tiles one workgroup sweeps (its LDS window slots)
     uint32_t tail_ch, tail_stripes; // DDS_TAIL: the last tail_ch channels in tail_stripes short stripes
     uint32_t zw;                    // DDS_ZFILL: zero worker workgroups (first in dispatch order)
+    uint32_t pipc, pgrid;           // DDS_PERSIST: items (DDS_PB tiles) per channel, persistent workgroups
     // event index (dds_index_kernel -> dds_tile_kernel)
     uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
     uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
@@ -276,6 +277,21 @@ constexpr bool DDS_ZFILL = DPEMU_DDS_ZFILL && !DPEMU_DDS_XCD && !DPEMU_DDS_TAIL;
 #ifndef DPEMU_DDS_ZW_PER_CU
 #define DPEMU_DDS_ZW_PER_CU 1
 #endif
+// A/B (build-time, -DDPEMU_DDS_PERSIST=1): persistent tile workgroups taking
+// DDS_PB-tile items in channel order (item g + k grid), the sine table
+// staged once and the envelope / frequency tables kept across items of the
+// same tables (dds.hip dds_tile_persist_kernel)
+#ifndef DPEMU_DDS_PERSIST
+#define DPEMU_DDS_PERSIST 0
+#endif
+#ifndef DPEMU_DDS_PB
+#define DPEMU_DDS_PB 4
+#endif
+#ifndef DPEMU_DDS_PWG
+#define DPEMU_DDS_PWG 7
+#endif
+constexpr bool DDS_PERSIST = DPEMU_DDS_PERSIST && !DPEMU_DDS_XCD && !DPEMU_DDS_TAIL && !DPEMU_DDS_ZFILL;
+constexpr uint32_t DDS_PB = DPEMU_DDS_PB;
 constexpr uint32_t DDS_ZB = 1024;           // silent flags per zero-worker batch (LDS bytes <= DDS_LUT_BYTES)
 constexpr uint32_t WIN_LIVE = 0x80000000u;   // tile window .y bit 31: some sample of the tile can play
 #ifndef DPEMU_DDS_K
