@@ -845,7 +845,10 @@ __global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_kernel(const DDS
 // resident workgroups work on consecutive items: one advancing front).  The
 // sine table is staged once per workgroup, the envelope / frequency tables
 // again only when an item's tables differ from the previous item's.
-__global__ void __launch_bounds__(BLOCK) DDS_TILE_ATTR dds_tile_persist_kernel(const DDSParams p)
+#ifndef DDS_PERSIST_WAVES
+#define DDS_PERSIST_WAVES 5     // (7, the tile kernel's, spills 19 VGPRs here; 6 spills 13)
+#endif
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(DDS_PERSIST_WAVES))) dds_tile_persist_kernel(const DDSParams p)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     int16_t *s_lut = reinterpret_cast<int16_t *>(s_dyn);

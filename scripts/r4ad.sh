@@ -4,5 +4,5 @@ out=gpurun_out/r4ad
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p $out
 L=ab_build/libdpemu_
-timeout -k 10 300 python -u scripts/ab_dds.py --libs ${L}ddsS.so,${L}ddsP4w4.so,${L}ddsP4w6.so,${L}ddsP16w4.so,${L}ddsP16w6.so --reps 5 > $out/ab2.jsonl 2>&1 || { echo "ab failed"; tail $out/ab2.jsonl; exit 1; }
-tail -1 $out/ab2.jsonl
+timeout -k 10 300 python -u scripts/ab_dds.py --libs ${L}ddsS.so,${L}ddsP4.so,${L}ddsP8.so,${L}ddsP16.so --reps 5 > $out/ab3.jsonl 2>&1 || { echo "ab failed"; tail $out/ab3.jsonl; exit 1; }
+tail -1 $out/ab3.jsonl
