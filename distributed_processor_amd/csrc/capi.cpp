@@ -68,8 +68,6 @@ struct dpemu_ctx {
     uint32_t *d_ch = nullptr;
     uint32_t ch_cap = 0;
     std::vector<uint32_t> ch_cache;
-    void *d_dds_index = nullptr;            // event index of dds_index_kernel
-    uint64_t dds_index_cap = 0;
     std::string last_kernel;                // variant the last dpemu_run launched (dpemu_last_kernel)
     // kernel timing (dpemu_set_kernel_timing): event pairs recorded around main kernels
     bool timing = false;
@@ -105,7 +103,7 @@ static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...)
 
 // Work of one context runs in call order whatever the streams: a call on a
 // stream other than the previous call's first waits for the previous call's
-// work (the scratch buffers -- histogram replicas, DDS index, thresholds, LUT
+// work (the scratch buffers -- histogram replicas, thresholds, LUT
 // table, channel descriptors -- are shared by the context's calls).
 static hipError_t order_begin(dpemu_ctx *ctx, hipStream_t s)
 {
@@ -339,7 +337,6 @@ int dpemu_destroy(dpemu_ctx *ctx)
     if (ctx->ord_valid) (void)hipEventSynchronize(ctx->ord_ev);   // the context's work is done with its buffers
     free_programs(ctx);
     (void)hipFree(ctx->d_thr); (void)hipFree(ctx->d_lut); (void)hipFree(ctx->d_sin); (void)hipFree(ctx->d_ch);
-    (void)hipFree(ctx->d_dds_index);
     (void)hipFree(ctx->d_hist_rep);
     for (auto *v : {&ctx->ev_used, &ctx->ev_free})
         for (auto &e : *v) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -840,19 +837,6 @@ int dpemu_dds_sin_lut(int16_t *out)
 
 }  // extern "C"
 
-#ifdef DDS_PROBE_TIMES
-static unsigned long long *g_probe = nullptr;
-static uint64_t g_probe_n = 0, g_probe_used = 0;
-// the last synthesis's stamps {start, end, hw_id | xcc << 32 | channel << 40} per workgroup
-extern "C" uint64_t dpemu_probe_dds_times(unsigned long long *out, uint64_t n_max)
-{
-    if (hipDeviceSynchronize() != hipSuccess || !g_probe) return 0;
-    const uint64_t n = std::min(n_max, g_probe_used);
-    if (hipMemcpy(out, g_probe, n * 24, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    return n;
-}
-#endif
-
 extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uint32_t *summary,
                          const uint32_t *events, const uint32_t *env_tables, const uint32_t *freq_tables,
                          int16_t *iq_out, void *stream)
@@ -881,17 +865,6 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, order_begin(ctx, s));
-    // the tile kernel's dispatch order: channels grouped by element (stable),
-    // so workgroups of one element's cost run together (DDS_ORDER_ELEM);
-    // appended to the descriptors
-    {
-        std::vector<uint32_t> order(ch->n_channels);
-        for (uint32_t i = 0; i < ch->n_channels; i++) order[i] = i;
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-            return desc[(size_t)a * DDS_CH_WORDS + 1] < desc[(size_t)b * DDS_CH_WORDS + 1];
-        });
-        desc.insert(desc.end(), order.begin(), order.end());
-    }
     if (desc != ctx->ch_cache) {            // descriptors change rarely: upload only then
         HIPCHK(ctx, hipStreamSynchronize(s));   // an earlier launch may still read d_ch
         if (desc.size() > ctx->ch_cap) {
@@ -909,75 +882,24 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.env = env_tables; p.freq = freq_tables;
     p.sin_lut = ctx->d_sin;
     p.ch = ctx->d_ch;
-    p.ch_order = ctx->d_ch + (size_t)ch->n_channels * DDS_CH_WORDS;
     p.iq = reinterpret_cast<uint32_t *>(iq_out);
     p.n_channels = ch->n_channels; p.n_lanes = ch->n_lanes; p.n_samples = ch->n_samples;
     p.event_cap = ch->event_cap;
-    p.ev_lds = std::max<uint32_t>(8, (ch->event_cap + 7) & ~7u);
     p.env_lds = (env_max + 3) & ~3u;
     p.freq_lds = (freq_max + 3) & ~3u;
-    if (DDS_XCD) {
-        // tile origins shifted by up to DDS_TILE - 16 samples (dds_tile_off): one more window
-        p.tiles = (p.n_samples + 2 * DDS_TILE - 16 - 1) / DDS_TILE;
-        p.stripes = DDS_XCD_K;
-        p.wg_tiles = (p.tiles + 8 * p.stripes - 1) / (8 * p.stripes);
-        if (DDS_XCD_BAL) p.wg_tiles = std::min(p.tiles, std::max(p.tiles / 8, 31u));   // residue M / the rest (< 32)
-    } else {
-        p.tiles = (p.n_samples + DDS_TILE - 1) / DDS_TILE;
-        p.stripes = std::max<uint32_t>(1, std::min<uint32_t>(p.tiles, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE));
-        p.wg_tiles = (p.tiles + p.stripes - 1) / p.stripes;
-        if (DDS_PERSIST) {
-            p.wg_tiles = DDS_PB;
-            p.pipc = (p.tiles + DDS_PB - 1) / DDS_PB;
-            const uint64_t n_items = (uint64_t)p.pipc * p.n_channels;
-            if (n_items >= (1ull << 32)) return fail(ctx, DPEMU_E_INVALID, "DDS: too many tile items");
-            p.pgrid = (uint32_t)std::min<uint64_t>(n_items, (uint64_t)ctx->n_cu * DPEMU_DDS_PWG);
-        }
-        p.zw = std::max<uint32_t>(1u, ctx->n_cu * DPEMU_DDS_ZW_PER_CU);
-        if (DDS_ZFILL && (uint64_t)p.n_channels * p.tiles + (uint64_t)p.zw * DDS_ZB >= (1ull << 32))
-            return fail(ctx, DPEMU_E_INVALID, "DDS: channels x tiles too large");
-        if (DDS_TAIL) {
-            // one round of resident workgroups' worth of short stripes at the end:
-            // the device's CUs x 7 resident tile workgroups x DDS_TAIL_TILES tiles
-            p.tail_stripes = std::max<uint32_t>(p.stripes, (p.tiles + DDS_TAIL_TILES - 1) / DDS_TAIL_TILES);
-            const uint64_t tail_tiles = (uint64_t)ctx->n_cu * 7u * DDS_TAIL_TILES;
-            p.tail_ch = (uint32_t)std::min<uint64_t>(p.n_channels, (tail_tiles + p.tiles - 1) / p.tiles);
-        }
-    }
+    p.tiles = (uint32_t)(((uint64_t)p.n_samples + DDS_TILE - 1) / DDS_TILE);
+    p.seg_tiles = std::min(p.tiles, DDS_SEG);
+    p.segs = (p.tiles + p.seg_tiles - 1) / p.seg_tiles;
+    if ((uint64_t)p.segs * p.n_channels >= (1ull << 31)) return fail(ctx, DPEMU_E_INVALID, "DDS: too many tiles");
     {
-        const uint32_t fixed = dds_lds_bytes(0, p.wg_tiles, p.env_lds, p.freq_lds);
-        const uint32_t fit = fixed < DDS_WG_LDS_BUDGET ? (DDS_WG_LDS_BUDGET - fixed) / 20 & ~7u : 0u;
-        p.rec_lds = std::min(p.ev_lds, std::max(fit, DDS_REC_LDS_MIN));
+        // the record area: every record of a lane (16 B x event_cap) when that fits the
+        // budget (dds_synth_kernel<false>), else what fits, in passes (<true>)
+        const uint32_t fixed = dds_lds_bytes(0, p.env_lds, p.freq_lds);
+        const uint32_t fit = fixed < DDS_WG_LDS_BUDGET ? (DDS_WG_LDS_BUDGET - fixed) & ~15u : 0u;
+        const uint32_t all = 16 * std::max<uint32_t>(1, ch->event_cap);
+        p.rec_bytes = all <= fit ? all : std::max(fit, 20 * DDS_REC_MIN);
     }
-    const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds, p.tiles);
-    if (need > ctx->dds_index_cap) {         // the event index (grown, never shrunk)
-        HIPCHK(ctx, hipStreamSynchronize(s));   // an earlier launch may still use it
-        (void)hipFree(ctx->d_dds_index);
-        ctx->d_dds_index = nullptr; ctx->dds_index_cap = 0;
-        HIPCHK(ctx, hipMalloc(&ctx->d_dds_index, need));
-        ctx->dds_index_cap = need;
-    }
-    uint8_t *b = static_cast<uint8_t *>(ctx->d_dds_index);
-    p.xs = reinterpret_cast<uint4 *>(b);
-    p.win = reinterpret_cast<uint4 *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
-    p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16 + (uint64_t)p.n_channels * p.tiles * 16);
-#ifdef DDS_PROBE_TIMES                    // diagnostic build: per-workgroup stamps of the tile kernel
-    {
-        const uint64_t n_wg = DDS_XCD_BAL ? 9ull * p.n_channels : DDS_XCD ? 8ull * p.n_channels * p.stripes
-                              : DDS_TAIL ? (uint64_t)(p.n_channels - p.tail_ch) * p.stripes + (uint64_t)p.tail_ch * p.tail_stripes
-                                         : (uint64_t)p.stripes * p.n_channels;
-        if (n_wg > g_probe_n) {
-            (void)hipFree(g_probe);
-            HIPCHK(ctx, hipMalloc(&g_probe, n_wg * 24));
-            g_probe_n = n_wg;
-        }
-        HIPCHK(ctx, hipMemsetAsync(g_probe, 0, n_wg * 24, s));
-        p.probe = g_probe;
-        g_probe_used = n_wg;
-    }
-#endif
     hipEvent_t ev_stop = nullptr;
-    HIPCHK(ctx, launch_dds_index(p, s));   // outside the timed bracket: it holds the synthesis kernel alone
     HIPCHK(ctx, timing_start(ctx, s, &ev_stop));
     HIPCHK(ctx, launch_dds(p, s));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, s));

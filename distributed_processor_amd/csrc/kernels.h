@@ -204,139 +204,53 @@ constexpr uint32_t MACRO_CHUNK_MIXED = 0xFFFFFFFFu;   // macro_chunk: not every 
 constexpr bool MACRO_CHUNK_LEAN = DPEMU_MACRO_CHUNK_LEAN;   // one wave test per chunk (A/B: -DDPEMU_MACRO_CHUNK_LEAN=0)
 
 // ---- DDS ------------------------------------------------------------------
-// Two launches per synthesis (dds.hip): dds_index_kernel compacts each
-// channel's strobes and pulse resets once and writes every sample tile's
-// window of them; dds_tile_kernel, grid (DDS stripes, channels), sweeps the
-// tiles of a channel round-robin over its stripe workgroups, so the
-// workgroups of a channel write adjacent tiles at the same time.
+// One launch per synthesis (dds.hip dds_synth_kernel): workgroup (channel,
+// segment of seg_tiles tiles) stages the channel's tables, scans the lane's
+// events for the strobes / resets its segment can see, and sweeps its tiles.
 struct DDSParams {
     const uint32_t *summary;
     const uint4 *events;           // dpemu_run event records, slot-major
     const uint32_t *env, *freq;
     const int16_t *sin_lut;        // Q15 sine table [4096]
     const uint32_t *ch;            // per-channel descriptors, DDS_CH_WORDS u32 each
-    const uint32_t *ch_order;      // the tile kernel's channel dispatch order (capi.cpp dds_channel_order)
     uint32_t *iq;                  // [n_channels][n_samples] packed {I16 low, Q16 high}
     uint32_t n_channels, n_lanes, n_samples, event_cap;
-    uint32_t ev_lds;               // compacted-event slots per channel (>= event_cap, multiple of 8)
-    uint32_t rec_lds;              // strobe records / reset times a tile workgroup stages in LDS (<= ev_lds)
+    uint32_t tiles;                // DDS_TILE-sample tiles per channel
+    uint32_t seg_tiles, segs;      // tiles per workgroup; workgroups (segments) per channel
+    uint32_t rec_bytes;            // a workgroup's record staging area (dds.hip stage; multiple of 16)
     uint32_t env_lds, freq_lds;    // LDS staging capacity for a channel's env / freq table (words, as staged)
-    uint32_t tiles;                // tile windows per channel (DDS_TILE samples each; dds_tile_off)
-    uint32_t stripes;              // DDS_XCD: workgroups per (channel, block residue); else per channel
-    uint32_t wg_tiles;             // most tiles one workgroup sweeps (its LDS window slots)
-    uint32_t tail_ch, tail_stripes; // DDS_TAIL: the last tail_ch channels in tail_stripes short stripes
-    uint32_t zw;                    // DDS_ZFILL: zero worker workgroups (first in dispatch order)
-    uint32_t pipc, pgrid;           // DDS_PERSIST: items (DDS_PB tiles) per channel, persistent workgroups
-    // event index (dds_index_kernel -> dds_tile_kernel)
-    uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
-    uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
-    uint4 *win;                    // [n_channels][tiles] {strobe lo, count, reset lo, count}
-    unsigned long long *probe;     // diagnostic builds only (DDS_PROBE_TIMES): per-workgroup stamps, else null
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
-constexpr uint32_t DDS_MAX_EVENTS = 1024;
-constexpr uint32_t DDS_TILE = 4 * BLOCK;      // samples per tile: 4 per thread, one 16-B store each
-#ifndef DDS_TPS
-#define DDS_TPS 16
-#endif
-constexpr uint32_t DDS_TILES_PER_STRIPE = DDS_TPS;   // stripes: tiles per workgroup (build-time A/B: -DDDS_TPS=)
-// XCD-block tile mapping (dds.hip TileMap), else round-3 stripes (A/B: -DDPEMU_DDS_XCD=0)
-#ifndef DPEMU_DDS_XCD
-#define DPEMU_DDS_XCD 0
-#endif
-constexpr bool DDS_XCD = DPEMU_DDS_XCD != 0;
-// 2: balanced -- residue workgroups take a multiple of 4 tiles (one per wave
-// and round), a workgroup per channel the contiguous rest (dds.hip tile_map)
-constexpr bool DDS_XCD_BAL = DPEMU_DDS_XCD == 2;
-#ifndef DPEMU_DDS_ZERO
-#define DPEMU_DDS_ZERO 0
-#endif
-constexpr bool DDS_ZERO_TILES = DPEMU_DDS_ZERO;   // all-zero wave tiles skip the transpose (A/B: -DDPEMU_DDS_ZERO=0)
-// dispatch channels grouped by element (ch_order) instead of in channel order (A/B: -DDPEMU_DDS_ORDER=0)
-#ifndef DPEMU_DDS_ORDER
-#define DPEMU_DDS_ORDER 0
-#endif
-constexpr bool DDS_ORDER_ELEM = DPEMU_DDS_ORDER;
-// stripes: the workgroups dispatched last are short (DDS_TAIL_TILES tiles),
-// so the launch's tail is one short workgroup long (A/B: -DDPEMU_DDS_TAIL=0)
-#ifndef DPEMU_DDS_TAIL
-#define DPEMU_DDS_TAIL 0
-#endif
-constexpr bool DDS_TAIL = DPEMU_DDS_TAIL && !DPEMU_DDS_XCD;
-#ifndef DPEMU_DDS_TAIL_TILES
-#define DPEMU_DDS_TAIL_TILES 4
-#endif
-constexpr uint32_t DDS_TAIL_TILES = DPEMU_DDS_TAIL_TILES;
-// A/B (build-time, -DDPEMU_DDS_ZFILL=1): the index marks each
-// tile live or silent, zw zero-worker workgroups (first in dispatch order)
-// write the silent tiles, the stripe workgroups only the live ones
-#ifndef DPEMU_DDS_ZFILL
-#define DPEMU_DDS_ZFILL 0
-#endif
-constexpr bool DDS_ZFILL = DPEMU_DDS_ZFILL && !DPEMU_DDS_XCD && !DPEMU_DDS_TAIL;
-#ifndef DPEMU_DDS_ZW_PER_CU
-#define DPEMU_DDS_ZW_PER_CU 1
-#endif
-// A/B (build-time, -DDPEMU_DDS_PERSIST=1): persistent tile workgroups taking
-// DDS_PB-tile items in channel order (item g + k grid), the sine table
-// staged once and the envelope / frequency tables kept across items of the
-// same tables (dds.hip dds_tile_persist_kernel)
-#ifndef DPEMU_DDS_PERSIST
-#define DPEMU_DDS_PERSIST 0
-#endif
-#ifndef DPEMU_DDS_PB
-#define DPEMU_DDS_PB 4
-#endif
-#ifndef DPEMU_DDS_PWG
-#define DPEMU_DDS_PWG 7
-#endif
-constexpr bool DDS_PERSIST = DPEMU_DDS_PERSIST && !DPEMU_DDS_XCD && !DPEMU_DDS_TAIL && !DPEMU_DDS_ZFILL;
-constexpr uint32_t DDS_PB = DPEMU_DDS_PB;
-constexpr uint32_t DDS_ZB = 1024;           // silent flags per zero-worker batch (LDS bytes <= DDS_LUT_BYTES)
-constexpr uint32_t WIN_LIVE = 0x80000000u;   // tile window .y bit 31: some sample of the tile can play
-#ifndef DPEMU_DDS_K
-#define DPEMU_DDS_K 1
-#endif
-constexpr uint32_t DDS_XCD_K = DPEMU_DDS_K;   // workgroups per (channel, residue) (A/B: -DDPEMU_DDS_K=)
-// channel ch's tile origin: tile c holds samples [c DDS_TILE - off, + DDS_TILE);
-// XCD blocks: off = (ch N mod DDS_TILE) rounded down to 16 samples, so tile c
-// starts within 12 samples of global 4-KiB block (ch N) / DDS_TILE + c
-__host__ __device__ inline uint32_t dds_tile_off(const DDSParams &p, uint32_t ch)
-{
-    return DDS_XCD ? (uint32_t)(((uint64_t)ch * p.n_samples) % DDS_TILE) & ~15u : 0u;
-}
+constexpr uint32_t DDS_MAX_EVENTS = 1024;     // event_cap bound: 4 records per thread in the event scan
+constexpr uint32_t DDS_TILE = 4 * BLOCK;      // samples per tile (one wave's 4 KiB)
 constexpr uint32_t DDS_ENV_LDS_MAX = 8192;    // words: tables up to 32 KiB are staged in LDS
 constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;   // words: 64 freq entries as (R, R') pairs
 
-// dynamic LDS bytes of dds_tile_kernel: quarter sine table (entries
-// 0..1031) | strobe records (16 B) | reset times | tile windows | env | freq |
+// dynamic LDS bytes of dds_synth_kernel: quarter sine table (entries
+// 0..1031) | record area (16-B strobe records, 4-B reset times) | env | freq |
 // the cycle sweep's per-wave store transpose (1 KiB per wave)
 constexpr uint32_t DDS_LUT_BYTES = 1032 * 2;
 constexpr uint32_t DDS_XPOSE_BYTES = (BLOCK / 64) * 1024;
-__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t rec_lds, uint32_t tiles_per_stripe, uint32_t env_lds,
-                                                  uint32_t freq_lds)
+__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t rec_bytes, uint32_t env_lds, uint32_t freq_lds)
 {
-    return DDS_LUT_BYTES + rec_lds * 20 + tiles_per_stripe * 16 + (env_lds + freq_lds) * 4 + DDS_XPOSE_BYTES;
+    return DDS_LUT_BYTES + rec_bytes + (env_lds + freq_lds) * 4 + DDS_XPOSE_BYTES;
 }
-// LDS budget of a tile workgroup: 8 workgroups (32 waves, the VGPR-bound
-// occupancy) share a CU's 160 KiB.  The record capacity is what is left of
-// it (at least DDS_REC_LDS_MIN); a stripe whose window holds more strobes or
-// resets than that reads them from the global index instead.
+// LDS budget of a workgroup: 8 workgroups (32 waves) share a CU's 160 KiB.
+// The record area is 16 B x event_cap when that fits (every record of a lane
+// fits: one staging per workgroup), else what is left of the budget (at least
+// DDS_REC_MIN records of each kind) and the multi-pass kernel.
 // (less 512 B: the compiler's static LDS of the kernel, so 8 fit in 160 KiB)
 constexpr uint32_t DDS_WG_LDS_BUDGET = 20 * 1024 - 512;
-constexpr uint32_t DDS_REC_LDS_MIN = 64;
+constexpr uint32_t DDS_REC_MIN = 64;
+#ifndef DDS_SEG_TILES
+#define DDS_SEG_TILES 52
+#endif
+constexpr uint32_t DDS_SEG = DDS_SEG_TILES;   // tiles per workgroup (A/B: -DDDS_SEG_TILES=)
 
 // LDS words of an interp-1 envelope of n words staged as swizzled (E, E')
 // pairs (dds.hip env_pair): whole groups of 8 16-B chunks
 __host__ __device__ inline uint32_t dds_env_pairs_words(uint32_t n) { return (2 * n + 31) & ~31u; }
 
-// bytes of the event index (xs, xr, win)
-inline uint64_t dds_index_bytes(uint32_t n_channels, uint32_t ev_lds, uint32_t tiles)
-{
-    return (uint64_t)n_channels * ev_lds * 20 + (uint64_t)n_channels * tiles * 16;
-}
-
-hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream);
 hipError_t launch_dds(const DDSParams &p, hipStream_t stream);
 
 }  // namespace dpemu

@@ -274,6 +274,46 @@ def test_global_record_fallback(emu):
     assert (ref != 0).sum() > 10000
 
 
+def test_dense_tile_raw_event_lookup(emu):
+    """a 32-KiB envelope leaves the multi-pass kernel room for only
+    DDS_REC_MIN (64) records of each kind; lanes with 150 strobes and 120
+    resets packed into one 1,024-sample tile (repeated times: hand-built
+    events, not dpemu_run's) make that tile look its records up in the raw
+    events, next to tiles swept from staged records; against oracle_dds"""
+    import torch
+    rng = np.random.default_rng(29)
+    cap, n_lanes, n_cycles = 400, 3, 1200
+    env_tab = pack_iq16(np.exp(1j * rng.uniform(0, 2 * np.pi, 4000)) * rng.uniform(0, 1, 4000))
+    freq_tab = np.concatenate([DDSElementConfig(samples_per_clk=16).get_freq_buffer([f])
+                               for f in (91.7e6, -13.1e6, 250e6)])
+    summary, ev = synthetic_timelines(rng, n_lanes, cap, n_cycles, 4000, 3)
+    for L in (1, 2):
+        # 270 events between cycles 300 and 340 (tile 4 at 16 samples / clk
+        # holds cycles 256..319, tile 5 320..383), the rest spread after them
+        n = 270
+        t = np.sort(np.concatenate([300 + rng.integers(0, 20, 150), 320 + rng.integers(0, 20, 120)])).astype(np.uint32)
+        kind = np.zeros(n, np.uint32)
+        kind[rng.permutation(n)[:120]] = 1
+        ev[:n, L, 0] = t
+        ev[:n, L, 1] = (ev[:n, L, 1] & ~np.uint32(0xF3000000)) | (kind << 28)   # element 0 strobes / resets
+        rest = np.sort(rng.integers(400, n_cycles, cap - n)).astype(np.uint32)
+        ev[n:, L, 0] = rest
+        summary[L, 2] = cap
+    desc = []
+    for L in range(n_lanes):
+        for e, (spc, interp) in enumerate(((16, 1), (16, 4), (8, 1), (16, 3))):
+            desc.append((L, e, spc, interp, 0, 4000, 0, len(freq_tab)))
+    desc = np.array(desc, np.uint32)
+    n_samples = 16 * n_cycles + 4 * 5
+    ref = oracle.dds(desc, summary, ev, env_tab, freq_tab, n_samples, cap)
+    dev = {'summary': torch.from_numpy(summary.view(np.int32)).cuda(),
+           'events': torch.from_numpy(ev.view(np.int32)).cuda()}
+    iq = emu.synthesize(plan_from(desc, env_tab, freq_tab, n_lanes, cap), dev, n_samples)
+    torch.cuda.synchronize()
+    check_equal(host(iq), ref, 'dense tile')
+    assert (ref[4 * 1:4 * 3, 16 * 300:16 * 340] != 0).sum() > 1000
+
+
 @pytest.mark.parametrize('depth', [2, 8])
 def test_synthesis_pipeline_batches(emu, depth):
     """dds.SynthesisPipeline (`depth` contexts / streams, batch k + 1's index
