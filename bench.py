@@ -16,15 +16,17 @@ Sub-objects on the same line, each with its own roofline and CPU baselines:
                   (test_linear_compile_globalasm core 0) at 10^6 shots, beside
                   oracle_rtl (the per-clock stand-in for the Verilator testbench)
   "dds"           config 5: RB timelines (8 cores, depth 200) synthesised to
-                  int16 I/Q on 16 channels per sequence at 16 samples/clk,
-                  --dds-depth batches in flight (dds.SynthesisPipeline)
+                  int16 I/Q on 16 channels per sequence at 16 samples/clk;
+                  one synthesis per step on one stream (--dds-depth > 1 also
+                  measures batches in flight, dds.SynthesisPipeline)
   "active_reset"  config 3: fproc_meas branching + sync barriers, 1.25*10^6
                   shots per GPU (10^7 over 8 GPUs)
   "lut"           config 3's circuit through the fproc_lut back end: every
                   core waits on a syndrome LUT over the 8 measurements
   "rb"            config 4 at its stated size: 10^5 distinct 2-core depth-200
-                  RB sequences x 10 shots per GPU, --rb-depth batches in
-                  flight (emulator.RunPipeline)
+                  RB sequences x 10 shots per GPU, one batch per step
+                  (--rb-depth > 1 also measures batches in flight,
+                  emulator.RunPipeline)
 
 CPU baselines (rank 0, one GPU): the reference's Verilator/cocotb testbench
 cannot run here or on the box, so each leg reports
@@ -126,8 +128,13 @@ def median_rate(run, units_per_n, n0, target_s=0.8, reps=5):
     return n * units_per_n / float(np.median(times)), n, times
 
 
-def cpu_baselines(ps, cfg, horizon, what):
-    """oracle_fast (all cores) and oracle_rtl (1 thread, all cores) on the leg's workload"""
+def cpu_baselines(ps, cfg, horizon, what, all_cores=False):
+    """oracle_fast (the job's threads) and oracle_rtl (1 thread, the job's
+    threads) on the leg's workload.  all_cores: also oracle_fast at one
+    thread, and the whole host's rate (BASELINE.md:46 asks for all host
+    cores) extrapolated from the job's share -- not run at nproc threads: the
+    harness grants a one-GPU job OMP_NUM_THREADS of the host's CPUs and asks
+    it to keep its worker pools within that share."""
     import oracle
     threads, info = host_cores()
     C = cfg.cores_per_shot
@@ -137,18 +144,30 @@ def cpu_baselines(ps, cfg, horizon, what):
     f_rate, f_n, f_t = median_rate(fast(threads), C, 2000)
     r1_rate, r1_n, r1_t = median_rate(rtl(1), C, 20)
     ra_rate, ra_n, ra_t = median_rate(rtl(threads), C, 20 * threads)
-    return dict(value=f_rate, unit='core-shots/s', cores=threads, kind='port', **info,
-                per_core=f_rate / threads, share_note=share_note(threads, info),
-                method='median of 5 timed runs of a fixed sample after one warm-up run',
-                sample='{}: {} shots x {} cores per oracle_fast run (event-driven C restatement, OpenMP over '
-                       'shots, {} threads)'.format(what, f_n, C, threads),
-                oracle_fast={'value': f_rate, 'threads': threads, 'shots_per_run': f_n,
-                             'run_s': [round(x, 4) for x in f_t]},
-                oracle_rtl={'value_1_thread': r1_rate, 'value_all_cores': ra_rate, 'threads': threads,
-                            'shots_per_run': [r1_n, ra_n],
-                            'note': 'per-clock restatement of hdl/ (one evaluation per clock, the closest '
-                                    'stand-in for the Verilator testbench of cocotb/proc/Makefile:1-14, '
-                                    'which cannot run here)'})
+    res = dict(value=f_rate, unit='core-shots/s', cores=threads, kind='port', **info,
+               per_core=f_rate / threads, share_note=share_note(threads, info),
+               method='median of 5 timed runs of a fixed sample after one warm-up run',
+               sample='{}: {} shots x {} cores per oracle_fast run (event-driven C restatement, OpenMP over '
+                      'shots, {} threads)'.format(what, f_n, C, threads),
+               oracle_fast={'value': f_rate, 'threads': threads, 'shots_per_run': f_n,
+                            'run_s': [round(x, 4) for x in f_t]},
+               oracle_rtl={'value_1_thread': r1_rate, 'value_all_cores': ra_rate, 'threads': threads,
+                           'shots_per_run': [r1_n, ra_n],
+                           'note': 'per-clock restatement of hdl/ (one evaluation per clock, the closest '
+                                   'stand-in for the Verilator testbench of cocotb/proc/Makefile:1-14, '
+                                   'which cannot run here)'})
+    if all_cores:
+        f1_rate, f1_n, _ = median_rate(fast(1), C, 200)
+        nproc = info['nproc']
+        res['oracle_fast']['value_1_thread'] = f1_rate
+        res['all_cores'] = {
+            'value': f_rate * nproc / threads, 'unit': 'core-shots/s', 'threads': nproc, 'kind': 'extrapolated',
+            'scaling_1_to_{}_threads'.format(threads): f_rate / (f1_rate * threads),
+            'note': 'oracle_fast on all {} host CPUs, extrapolated linearly from the measured {}-thread rate '
+                    '(shots are independent; the 1 -> {} thread scaling measured beside it is the efficiency '
+                    'shown); not run at {} threads because the harness grants this job {} of them'.format(
+                        nproc, threads, threads, nproc, threads)}
+    return res
 
 
 def pmc(name):
@@ -179,21 +198,24 @@ def valu_view(prof, kernel_ms=None, instrs=None):
     if not prof or not prof.get('SQ_INSTS_VALU'):
         return None
     n = float(prof['SQ_INSTS_VALU'])
-    # the kernel's OWN issue peak (its opcode mix at the measured per-opcode
-    # costs, at its clock in the PMC pass) when profiled; the uniform peak of
-    # the fastest integer mix beside it
+    # graded against the measured wave64 integer-VALU issue peak (the fastest
+    # add / shift / xor mix, profiles/r04_valu_peak_pmc.json); the kernel's
+    # static opcode mix weighted by single-opcode chain costs
+    # (profiles/<tag>_kernel_valu_peaks.json) is reported beside it as
+    # frac_own_mix -- that table does not predict a mixed kernel's issue rate
+    # (DESIGN.md §6), so it is not the grading peak
     own = KERNEL_VALU_PEAKS.get(kernel_key(prof.get('kernel')))
-    peak = own['peak_valu_insts_per_s'] if own else VALU_PEAK
-    v = {'bound': 'valu', 'unit': 'wave64 VALU instr/s', 'peak': peak,
-         'peak_cycles_per_inst': own['cycles_per_inst'] if own else VALU_CPI,
-         'peak_source': ('profiles/{}_kernel_valu_peaks.json (the kernel\'s own opcode mix at the measured '
-                         'per-opcode issue costs, {:.2f} GHz)'.format(PROFILE_TAG, own['clock_ghz']) if own else
-                         'profiles/r04_valu_peak_pmc.json ({})'.format(VALU_PEAK_VARIANT)),
-         'uniform_peak': VALU_PEAK, 'valu_insts_per_launch': n}
+    peak = VALU_PEAK
+    v = {'bound': 'valu', 'unit': 'wave64 VALU instr/s', 'peak': peak, 'peak_cycles_per_inst': VALU_CPI,
+         'peak_source': 'profiles/r04_valu_peak_pmc.json ({})'.format(VALU_PEAK_VARIANT),
+         'valu_insts_per_launch': n}
+    if own:
+        v['own_mix_peak'] = own['peak_valu_insts_per_s']
     if kernel_ms:
         v['achieved'] = n / (kernel_ms * 1e-3)
         v['frac'] = v['achieved'] / peak
-        v['frac_uniform_peak'] = v['achieved'] / VALU_PEAK
+        if own:
+            v['frac_own_mix'] = v['achieved'] / own['peak_valu_insts_per_s']
     if prof.get('duration_ns'):
         v['frac_rocprof'] = n / (prof['duration_ns'] * 1e-9) / peak
     if instrs:
@@ -373,8 +395,12 @@ def compact_leg(res):
         c['step_frac'] = _sig(res['step_roofline_frac'], 3)
     if 'serial_ms_per_step' in res:
         c['serial_ms'] = _sig(res['serial_ms_per_step'])
+    if 'pipelined_ms_per_step' in res:
+        c['pipe_ms'] = _sig(res['pipelined_ms_per_step'])
     if 'cpu_baseline' in res:
         c['cpu'] = _sig(res['cpu_baseline']['value'], 3)
+        if 'all_cores' in res['cpu_baseline']:
+            c['cpu_all'] = _sig(res['cpu_baseline']['all_cores']['value'], 3)
     return c
 
 
@@ -433,7 +459,7 @@ def leg_ramsey(emu, args, world, rank, stream):
                       'lane_order': LANE_ORDER_NAMES[cfg.lane_order],
                       'global_shots_per_step': n * world, 'parallelism': 'shots sharded, {} GPU(s)'.format(world)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res['cpu_baseline'] = cpu_baselines(ps, cfg, 4096, 'config 2 Ramsey')
+        res['cpu_baseline'] = cpu_baselines(ps, cfg, 4096, 'config 2 Ramsey', all_cores=True)
     del out
     torch.cuda.empty_cache()
     return res
@@ -518,47 +544,54 @@ def leg_dds(emu, args, world, rank, stream):
     chans = [(shot0 + q, c, e) for q in range(n) for c in range(8) for e in (workloads.QDRV, workloads.RDRV)]
     plan = ChannelPlan(ps, cfg, shot0, n, chans, params)
     iq = torch.empty((plan.n_channels, n_samples), dtype=torch.int32, device='cuda')
-    # a step is one batch's whole synthesis (index + tiles); `dds_depth`
-    # batches in flight on as many contexts / streams (dds.SynthesisPipeline):
-    # batch k + 1's index kernel runs beside batch k's tiles, and the tile
-    # kernels of several batches share the GPU
-    pipe = SynthesisPipeline(torch.cuda.current_device(), depth=max(1, args.dds_depth), streams=args.pipe_streams)
-    last = {}
-
-    def step():
-        last['iq'] = pipe.synthesize(plan, ev, n_samples)[0]
-    dt = timed(step, pipe.drain, args.steps, args.warmup, world)
-    pipe.drain()
-    iq_pipe = last['iq'].clone()
-    pipe.close()
+    # a step is one batch's whole synthesis (dds_index_kernel + dds_tile_kernel)
+    # on one context and stream, in call order
     serial = lambda: emu.synthesize(plan, ev, n_samples, iq, stream)
     dt_serial = timed(serial, lambda: None, args.steps, args.warmup, world)
     kernel_ms = kernel_pass(emu, args.steps, serial, lambda: None)
     torch.cuda.synchronize()
-    # the pipelined batches and the serial ones must produce the same I/Q (a
-    # cross-stream ordering bug would still yield a throughput number)
-    assert torch.equal(iq_pipe, iq), 'config 5: pipelined and serial I/Q differ'
-    del iq_pipe
+    dt, mode = dt_serial, 'serial'
+    pipe_ms = None
+    if args.dds_depth > 1:
+        # opt-in: `dds_depth` batches in flight on as many contexts / streams
+        # (dds.SynthesisPipeline); the leg reports whichever of the two
+        # measured faster, both on the line
+        pipe = SynthesisPipeline(torch.cuda.current_device(), depth=args.dds_depth, streams=args.pipe_streams)
+        last = {}
+
+        def step():
+            last['iq'] = pipe.synthesize(plan, ev, n_samples)[0]
+        dt_pipe = timed(step, pipe.drain, args.steps, args.warmup, world)
+        pipe.drain()
+        # the pipelined batches and the serial ones must produce the same I/Q
+        # (a cross-stream ordering bug would still yield a throughput number)
+        assert torch.equal(last['iq'], iq), 'config 5: pipelined and serial I/Q differ'
+        pipe.close()
+        pipe_ms = dt_pipe / args.steps * 1e3
+        if dt_pipe < dt_serial:
+            dt, mode = dt_pipe, 'pipelined'
     samples = plan.n_channels * n_samples
     ms_step = dt / args.steps * 1e3
     prof = pmc('dds') if args.dds_seqs == 128 else None
-    # the kernel's own roofline: capped at the one-context step, not at the
-    # pipelined step (batches overlap, so that is shorter than one kernel)
+    # the tile kernel's own roofline, capped at the one-context step
     roof = hbm_roofline(samples * 4, kernel_ms, dt_serial / args.steps * 1e3, 'dpemu::dds_tile_kernel', prof,
                         'dds_tile_kernel')
     res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
            'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s', 'ms_per_step': ms_step,
            'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
-           'step': 'dds_index_kernel (per-channel event index + tile windows) + dds_tile_kernel per batch, '
-                   '{} batches in flight (dds.SynthesisPipeline: contexts and streams); kernel_ms and the '
-                   'roofline hold dds_tile_kernel alone (one context, one stream), value and ms_per_step the '
-                   'whole step'.format(args.dds_depth),
-           'batches_in_flight': args.dds_depth,
+           'step': 'dds_index_kernel (per-channel event index + tile windows) + dds_tile_kernel per batch on one '
+                   'stream ({}); kernel_ms and the roofline hold dds_tile_kernel alone, value and ms_per_step the '
+                   'whole step'.format('serial' if args.dds_depth <= 1 else
+                                       'serial and {} batches in flight measured, the faster reported'.format(
+                                           args.dds_depth)),
+           'step_mode': mode, 'batches_in_flight': args.dds_depth if mode == 'pipelined' else 1,
            'step_roofline_frac': samples * 4 / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
            'serial_ms_per_step': dt_serial / args.steps * 1e3,
            'config': {'workload': 'config5_dds_rb8', 'sequences_per_gpu': n, 'channels_per_gpu': plan.n_channels,
                       'samples_per_channel': n_samples, 'rb_depth': 200},
            'roofline': roof}
+    if pipe_ms is not None:
+        res['pipelined_ms_per_step'] = pipe_ms
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle
         threads, info = host_cores()
@@ -659,25 +692,7 @@ def leg_rb(emu, args, world, rank, stream):
     shot0, n = sharding.weak_shard(args.rb_seqs * args.rb_spg, rank)
     want = ('summary', 'events', 'meas', 'hist')
     steps = max(1, args.steps)
-    # a step is one batch (10^6 shots), `rb_depth` batches in flight on as many
-    # contexts / streams (emulator.RunPipeline): the next batch's waves fill
-    # the CUs this batch's tail of long sequences leaves idle
-    depth = max(1, args.rb_depth)
-    rp = RunPipeline(ps, cfg, n, want=want, depth=depth, device=torch.cuda.current_device(), first=emu,
-                     streams=args.pipe_streams)
-    hp = sharding.HistogramPipeline(rp.outputs[0]['hist'], n_buffers=max(2, depth))
-
-    def step():
-        with torch.cuda.stream(rp.streams[rp.k % depth]):
-            hp.step(lambda h: rp.launch(cfg, n, shot0, hist=h))
-    dt = timed(step, hp.drain, steps, min(args.warmup, 2), world)
-    hp.drain()
-    rp.drain()
-    assert int(hp.result().sum().item()) == n * world
-    s_pipe = rp.outputs[(rp.k - 1) % depth]['summary'].cpu().numpy()
-    rp.close()
-    del rp
-    # the same batches one at a time on one context: the kernel's own time
+    # a step is one batch (10^6 shots) on one context, in call order
     out = alloc_device_outputs(cfg, n, want=want)
     pipe = sharding.HistogramPipeline(out['hist'])
 
@@ -688,8 +703,33 @@ def leg_rb(emu, args, world, rank, stream):
     dt_serial = timed(serial, pipe.drain, steps, min(args.warmup, 2), world)
     kernel = emu.last_kernel()
     kernel_ms, kernel_ms_blk = interp_kernel_ms(emu, cfg, n, shot0, out, stream, steps, serial, pipe.drain)
+    dt, mode, pipe_ms, s_pipe = dt_serial, 'serial', None, None
+    depth = max(1, args.rb_depth)
+    if depth > 1:
+        # opt-in: `rb_depth` batches in flight on as many contexts / streams
+        # (emulator.RunPipeline: the next batch's waves fill the CUs this
+        # batch's tail of long sequences leaves idle); the faster of the two
+        # is the leg's value, both on the line
+        rp = RunPipeline(ps, cfg, n, want=want, depth=depth, device=torch.cuda.current_device(), first=emu,
+                         streams=args.pipe_streams)
+        hp = sharding.HistogramPipeline(rp.outputs[0]['hist'], n_buffers=max(2, depth))
+
+        def step():
+            with torch.cuda.stream(rp.streams[rp.k % depth]):
+                hp.step(lambda h: rp.launch(cfg, n, shot0, hist=h))
+        dt_pipe = timed(step, hp.drain, steps, min(args.warmup, 2), world)
+        hp.drain()
+        rp.drain()
+        assert int(hp.result().sum().item()) == n * world
+        s_pipe = rp.outputs[(rp.k - 1) % depth]['summary'].cpu().numpy()
+        rp.close()
+        del rp
+        pipe_ms = dt_pipe / steps * 1e3
+        if dt_pipe < dt_serial:
+            dt, mode = dt_pipe, 'pipelined'
     summ = out['summary'].cpu().numpy().view(np.uint32)
-    assert np.array_equal(summ, s_pipe.view(np.uint32)), 'config 4: pipelined and serial batches differ'
+    if s_pipe is not None:
+        assert np.array_equal(summ, s_pipe.view(np.uint32)), 'config 4: pipelined and serial batches differ'
     s = _abi.unpack_summary(summ)
     assert (s['status'] == _abi.ST_DONE).all(), 'config 4: not every lane reached DONE'
     assert int(pipe.result().sum().item()) == n * world
@@ -711,7 +751,8 @@ def leg_rb(emu, args, world, rank, stream):
     res = {'metric': 'emulated core-shots/s (config 4: 2-qubit RB, 1e5 sequences x depth 200, 10 shots each)',
            'value': n * 2 * world * steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * steps / dt,
            'ms_per_step': ms_step, 'kernel_ms': kernel_ms, 'steps': steps,
-           'serial_ms_per_step': dt_serial / steps * 1e3, 'batches_in_flight': depth,
+           'serial_ms_per_step': dt_serial / steps * 1e3, 'step_mode': mode,
+           'batches_in_flight': depth if mode == 'pipelined' else 1,
            'instructions_per_s': instrs * world * steps / dt,
            'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * steps / dt,
            'config': {'workload': 'config4_rb_2core_1e5seq_depth200', 'sequences': args.rb_seqs,
@@ -720,8 +761,10 @@ def leg_rb(emu, args, world, rank, stream):
                       'program_image_bytes': int(ps.words.nbytes), 'event_cap': cfg.event_cap,
                       'generate_s': gen_s, 'load_s': load_s},
            'roofline': roof}
+    if pipe_ms is not None:
+        res['pipelined_ms_per_step'] = pipe_ms
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res['cpu_baseline'] = cpu_baselines(ps, cfg, 1 << 20, 'config 4 RB')
+        res['cpu_baseline'] = cpu_baselines(ps, cfg, 1 << 20, 'config 4 RB', all_cores=True)
     del out
     torch.cuda.empty_cache()
     return res
@@ -735,10 +778,12 @@ def main():
     ap.add_argument('--shots', type=int, default=10 ** 6, help='config-2 shots per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
-    ap.add_argument('--dds-depth', type=int, default=8,
-                    help='DDS batches in flight (dds.SynthesisPipeline; streams beyond the 4 hardware queues '
-                         'share them, so at most 4 execute at once)')
-    ap.add_argument('--rb-depth', type=int, default=2, help='config-4 batches in flight (emulator.RunPipeline)')
+    ap.add_argument('--dds-depth', type=int, default=1,
+                    help='DDS batches in flight (opt-in, > 1: dds.SynthesisPipeline, measured beside the serial '
+                         'step and reported only when faster; streams beyond the 4 hardware queues share them)')
+    ap.add_argument('--rb-depth', type=int, default=1,
+                    help='config-4 batches in flight (opt-in, > 1: emulator.RunPipeline, measured beside the '
+                         'serial step and reported only when faster)')
     ap.add_argument('--ar-shots', type=int, default=1250000, help='config-3 shots per GPU per step')
     ap.add_argument('--rb-seqs', type=int, default=100000, help='config-4 RB sequences')
     ap.add_argument('--rb-spg', type=int, default=10, help='config-4 shots per sequence')

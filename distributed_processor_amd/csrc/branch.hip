@@ -50,14 +50,6 @@ namespace {
 
 enum : uint32_t { B_RUN = 0, B_SYNC = 1, B_LUT = 2, B_FIN = 3 };
 
-// event records stored as they arise (1) or held as whole wave rows (0), per
-// back end (A/B knobs: -DDPEMU_BRANCH_DIRECT=, -DDPEMU_BRANCH_DIRECT_LUT=)
-#ifndef DPEMU_BRANCH_DIRECT
-#define DPEMU_BRANCH_DIRECT 0
-#endif
-#ifndef DPEMU_BRANCH_DIRECT_LUT
-#define DPEMU_BRANCH_DIRECT_LUT 1
-#endif
 
 // decode-to-decode latency per op4 past the command's base cycle (D, the
 // trigger cycle tT for pulse-with-trigger / idle, the fproc ready cycle R):
@@ -110,27 +102,7 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v)
     return min(min(a, b), min(c, d));
 }
 
-#ifdef BRANCH_PROBE_COUNTS   // diagnostic build: per-wave execution counts of the loop's sections
-__device__ unsigned long long g_branch_cnt[16];
-#define PCNT(i) do { if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(&g_branch_cnt[i], 1ull); } while (0)
-#else
-#define PCNT(i) do { } while (0)
-#endif
-
 }  // namespace
-
-#ifdef BRANCH_PROBE_COUNTS
-extern "C" int dpemu_probe_branch_counts(unsigned long long *out, int reset)
-{
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_branch_cnt), sizeof(g_branch_cnt)) != hipSuccess) return -1;
-    if (reset) {
-        static const unsigned long long z[16] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_branch_cnt), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 16;
-}
-#endif
 
 // CT: the cores per shot when fixed at compile time (8: the BASELINE
 // configs), so group reductions and lane arithmetic are straight-line; 0 = p.C
@@ -150,7 +122,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // 0.446 ms held vs 0.480 direct; config 3 through the LUT 0.564 held vs
     // 0.494 direct -- the row bookkeeping's VALU costs more there than the
     // scattered partial rows it avoids
-    constexpr bool DIRECT = LUT ? DPEMU_BRANCH_DIRECT_LUT != 0 : DPEMU_BRANCH_DIRECT != 0;
+    constexpr bool DIRECT = LUT;
     constexpr int NF = LUT ? LUT_FIRE_CAP : 1;
 
     __shared__ uint32_t s_regs[REGS ? 16 : 1][REGS ? BLOCK : 1];
@@ -243,7 +215,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // draw the measurement.  Overflow flags come from the final counts.
     auto emit = [&](bool ok, uint32_t te, uint32_t kind) __attribute__((always_inline)) {
         if (ok) {
-            PCNT(3);
             if (DIRECT && n_ev < p.event_cap && p.events)
                 ev_lane[(uint64_t)n_ev * n_lanes] = event_record(te, pe, pp, pa, kind);
             if (!DIRECT && n_ev < p.event_cap && p.events) {
@@ -258,7 +229,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             }
             n_ev++;
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {   // meas_elem 0xFF: none
-                PCNT(4);
                 const uint32_t bit = meas_bit(p, shot, core, n_meas, thr_core, pa, pe);
                 const uint32_t tv = te + p.meas_latency;
                 if constexpr (XMEAS) {
@@ -326,17 +296,14 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         if (DIRECT || !p.events) return;
         const uint32_t ne = min(n_ev, p.event_cap);
         if (!__any(ne > n_st)) return;
-        PCNT(8);
         const uint32_t done = all ? INF32 : wave_min(mode == B_FIN ? INF32 : ne);
         // the held records [n_st, ne) are pend0, pend1: store the rows every
         // unfinished lane has passed, then shift once (not once per row)
         const bool f1 = n_st < ne && n_st < done;
         if (!__any(f1)) return;                      // most iterations complete no row
-        PCNT(9);
         const bool f2 = f1 && n_st + 1u < ne && n_st + 1u < done;
         if (f1) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
         if (__any(f2)) {
-            PCNT(10);
             if (f2) ev_lane[(uint64_t)(n_st + 1u) * n_lanes] = pend1;
         }
         pend0 = sel4(f1 && !f2, pend1, pend0);
@@ -351,7 +318,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         // max_cycles at decode
         finish(mode == B_RUN && t > max_cycles, ST_MAX_CYCLES, t);
         const bool run = mode == B_RUN;
-        PCNT(0);
         const uint4 u = PLDS ? s_prog[fetch_off + min(ip, k_max)]
                              : p.fetch[(uint64_t)min(ip, k_max) * p.fetch_stride + fetch_off];
         const uint32_t op = u.y >> 28;
@@ -362,7 +328,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         if constexpr (FPROC) {
             const bool fp = run && (op == 4u || op == 5u);
             if (__any(fp)) {
-                PCNT(1);
                 uint32_t bound = run ? t + 2u : INF32;
                 if constexpr (SYNC) {
                     if (__any(mode == B_SYNC)) {
@@ -410,7 +375,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             // immediates, then reg[rs0] into register-sourced fields
             // (only 8 / 9 write: skipped in iterations where no lane has one)
             if (__any(cont && ((0x300u >> op) & 1u))) {
-                PCNT(2);
                 uint32_t pe2 = pe, pp2 = pp, pa2 = pa;
                 pulse_write(u, pe2, pp2, pa2);
                 if (cont && (u.w & UOP_ANY_RS)) {
@@ -435,7 +399,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             }
             flags |= (pg && late) ? F_LATE : 0u;
             if (__any(pg && !cont && !to_sync)) {
-                PCNT(7);
                 finish(pg && !cont && !to_sync, over ? ST_MAX_CYCLES : op >= 0xDu ? ST_HUNG_OPCODE : ST_DONE, D);
             }
             wait_d = to_sync ? D : wait_d;
@@ -445,7 +408,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         }
         // ---- reg_alu, jump_cond, alu_fproc / jump_fproc, inc_qclk (1, 3-6) ----
         if (__any(go && !pcls)) {
-            PCNT(5);
             const bool sg = go && !pcls;
             const bool is_fp = op == 4u || op == 5u;
             const uint32_t reg0 = reg(u.w >> 20);
@@ -455,7 +417,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
             bool lut_wait = false, no_meas = false;
             if constexpr (FPROC) {
                 if (__any(sg && is_fp)) {
-                    PCNT(6);
                     if (sg && is_fp) data = meas_lookup(leader_tid + (((u.z >> 16) & 0xFFu) & (C - 1u)), D);
                 }
             }
@@ -512,7 +473,6 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         // last arrival releases it in the same iteration ----
         if constexpr (SYNC) {
             if (__any(mode == B_SYNC)) {
-                PCNT(11);
                 const uint32_t maxkey = sync_maxkey();
                 const uint64_t b = __ballot(is_part && mode == B_SYNC);
                 const uint64_t pm = __ballot(is_part);

@@ -68,6 +68,8 @@ struct dpemu_ctx {
     uint32_t *d_ch = nullptr;
     uint32_t ch_cap = 0;
     std::vector<uint32_t> ch_cache;
+    void *d_dds_index = nullptr;            // event index of dds_index_kernel
+    uint64_t dds_index_cap = 0;
     std::string last_kernel;                // variant the last dpemu_run launched (dpemu_last_kernel)
     // kernel timing (dpemu_set_kernel_timing): event pairs recorded around main kernels
     bool timing = false;
@@ -103,7 +105,7 @@ static int fail(dpemu_ctx *ctx, int code, const char *fmt, ...)
 
 // Work of one context runs in call order whatever the streams: a call on a
 // stream other than the previous call's first waits for the previous call's
-// work (the scratch buffers -- histogram replicas, thresholds, LUT
+// work (the scratch buffers -- histogram replicas, DDS index, thresholds, LUT
 // table, channel descriptors -- are shared by the context's calls).
 static hipError_t order_begin(dpemu_ctx *ctx, hipStream_t s)
 {
@@ -337,6 +339,7 @@ int dpemu_destroy(dpemu_ctx *ctx)
     if (ctx->ord_valid) (void)hipEventSynchronize(ctx->ord_ev);   // the context's work is done with its buffers
     free_programs(ctx);
     (void)hipFree(ctx->d_thr); (void)hipFree(ctx->d_lut); (void)hipFree(ctx->d_sin); (void)hipFree(ctx->d_ch);
+    (void)hipFree(ctx->d_dds_index);
     (void)hipFree(ctx->d_hist_rep);
     for (auto *v : {&ctx->ev_used, &ctx->ev_free})
         for (auto &e : *v) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -885,21 +888,31 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.iq = reinterpret_cast<uint32_t *>(iq_out);
     p.n_channels = ch->n_channels; p.n_lanes = ch->n_lanes; p.n_samples = ch->n_samples;
     p.event_cap = ch->event_cap;
+    p.ev_lds = std::max<uint32_t>(8, (ch->event_cap + 7) & ~7u);
     p.env_lds = (env_max + 3) & ~3u;
     p.freq_lds = (freq_max + 3) & ~3u;
     p.tiles = (uint32_t)(((uint64_t)p.n_samples + DDS_TILE - 1) / DDS_TILE);
-    p.seg_tiles = std::min(p.tiles, DDS_SEG);
-    p.segs = (p.tiles + p.seg_tiles - 1) / p.seg_tiles;
-    if ((uint64_t)p.segs * p.n_channels >= (1ull << 31)) return fail(ctx, DPEMU_E_INVALID, "DDS: too many tiles");
+    p.stripes = std::max<uint32_t>(1, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE);
+    p.wg_tiles = (p.tiles + p.stripes - 1) / p.stripes;
     {
-        // the record area: every record of a lane (16 B x event_cap) when that fits the
-        // budget (dds_synth_kernel<false>), else what fits, in passes (<true>)
-        const uint32_t fixed = dds_lds_bytes(0, p.env_lds, p.freq_lds);
-        const uint32_t fit = fixed < DDS_WG_LDS_BUDGET ? (DDS_WG_LDS_BUDGET - fixed) & ~15u : 0u;
-        const uint32_t all = 16 * std::max<uint32_t>(1, ch->event_cap);
-        p.rec_bytes = all <= fit ? all : std::max(fit, 20 * DDS_REC_MIN);
+        const uint32_t fixed = dds_lds_bytes(0, p.wg_tiles, p.env_lds, p.freq_lds);
+        const uint32_t fit = fixed < DDS_WG_LDS_BUDGET ? (DDS_WG_LDS_BUDGET - fixed) / 20 & ~7u : 0u;
+        p.rec_lds = std::min(p.ev_lds, std::max(fit, DDS_REC_LDS_MIN));
     }
+    const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds, p.tiles);
+    if (need > ctx->dds_index_cap) {         // the event index (grown, never shrunk)
+        HIPCHK(ctx, hipStreamSynchronize(s));   // an earlier launch may still use it
+        (void)hipFree(ctx->d_dds_index);
+        ctx->d_dds_index = nullptr; ctx->dds_index_cap = 0;
+        HIPCHK(ctx, hipMalloc(&ctx->d_dds_index, need));
+        ctx->dds_index_cap = need;
+    }
+    uint8_t *b = static_cast<uint8_t *>(ctx->d_dds_index);
+    p.xs = reinterpret_cast<uint4 *>(b);
+    p.win = reinterpret_cast<uint4 *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
+    p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16 + (uint64_t)p.n_channels * p.tiles * 16);
     hipEvent_t ev_stop = nullptr;
+    HIPCHK(ctx, launch_dds_index(p, s));   // outside the timed bracket: it holds the synthesis kernel alone
     HIPCHK(ctx, timing_start(ctx, s, &ev_stop));
     HIPCHK(ctx, launch_dds(p, s));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, s));

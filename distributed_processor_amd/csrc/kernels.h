@@ -181,16 +181,9 @@ hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream);
 // register slots the macro image names: 2, else 16 in LDS), else
 // macro_kernel (staged = false)
 constexpr uint32_t MACRO_SLOTS = 8;     // distinct programs per wave whose macros are staged in LDS
-#ifndef DPEMU_MACRO_CHUNK
-#define DPEMU_MACRO_CHUNK 16
-#endif
-constexpr uint32_t MACRO_CHUNK = DPEMU_MACRO_CHUNK;   // macros per program per staged chunk (A/B: -DDPEMU_MACRO_CHUNK=)
+constexpr uint32_t MACRO_CHUNK = 16;    // macros per program per staged chunk (8: 3.84-4.12 vs 3.60 ms)
 // addid: every ALU slot of the image is reg_alu id0 / add (RB phase updates)
 hipError_t launch_macro(const KParams &p, bool staged, int nr, bool addid, hipStream_t stream);
-#ifndef DPEMU_MACRO_RING
-#define DPEMU_MACRO_RING 4
-#endif
-constexpr uint32_t MACRO_RING = DPEMU_MACRO_RING;     // event rows a staged wave holds in LDS (power of two >= 4; 0: A/B only)
 constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no command; ALU ctl bit 31: present
 // pulse slot w bit 30 (capi.cpp mark_simple_macros): not a program's first
 // macro, its ALU slots are reg_alu (no inc_qclk) and its pulse slot is a
@@ -198,15 +191,13 @@ constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no comm
 // lean path (runtime conditions permitting)
 constexpr uint32_t MACRO_SIMPLE = 0x40000000u;
 constexpr uint32_t MACRO_CHUNK_MIXED = 0xFFFFFFFFu;   // macro_chunk: not every macro MACRO_SIMPLE
-#ifndef DPEMU_MACRO_CHUNK_LEAN
-#define DPEMU_MACRO_CHUNK_LEAN 1
-#endif
-constexpr bool MACRO_CHUNK_LEAN = DPEMU_MACRO_CHUNK_LEAN;   // one wave test per chunk (A/B: -DDPEMU_MACRO_CHUNK_LEAN=0)
 
 // ---- DDS ------------------------------------------------------------------
-// One launch per synthesis (dds.hip dds_synth_kernel): workgroup (channel,
-// segment of seg_tiles tiles) stages the channel's tables, scans the lane's
-// events for the strobes / resets its segment can see, and sweeps its tiles.
+// Two launches per synthesis (dds.hip): dds_index_kernel compacts each
+// channel's strobes and pulse resets once and writes every sample tile's
+// window of them; dds_tile_kernel, grid (DDS stripes, channels), sweeps the
+// tiles of a channel round-robin over its stripe workgroups, so the
+// workgroups of a channel write adjacent tiles at the same time.
 struct DDSParams {
     const uint32_t *summary;
     const uint4 *events;           // dpemu_run event records, slot-major
@@ -215,42 +206,55 @@ struct DDSParams {
     const uint32_t *ch;            // per-channel descriptors, DDS_CH_WORDS u32 each
     uint32_t *iq;                  // [n_channels][n_samples] packed {I16 low, Q16 high}
     uint32_t n_channels, n_lanes, n_samples, event_cap;
-    uint32_t tiles;                // DDS_TILE-sample tiles per channel
-    uint32_t seg_tiles, segs;      // tiles per workgroup; workgroups (segments) per channel
-    uint32_t rec_bytes;            // a workgroup's record staging area (dds.hip stage; multiple of 16)
+    uint32_t ev_lds;               // compacted-event slots per channel (>= event_cap, multiple of 8)
+    uint32_t rec_lds;              // strobe records / reset times a tile workgroup stages in LDS (<= ev_lds)
     uint32_t env_lds, freq_lds;    // LDS staging capacity for a channel's env / freq table (words, as staged)
+    uint32_t tiles;                // tile windows per channel (DDS_TILE samples each)
+    uint32_t stripes;              // tile workgroups per channel
+    uint32_t wg_tiles;             // most tiles one workgroup sweeps (its LDS window slots)
+    // event index (dds_index_kernel -> dds_tile_kernel)
+    uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
+    uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
+    uint4 *win;                    // [n_channels][tiles] {strobe lo, count, reset lo, count}
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
-constexpr uint32_t DDS_MAX_EVENTS = 1024;     // event_cap bound: 4 records per thread in the event scan
-constexpr uint32_t DDS_TILE = 4 * BLOCK;      // samples per tile (one wave's 4 KiB)
+constexpr uint32_t DDS_MAX_EVENTS = 1024;
+constexpr uint32_t DDS_TILE = 4 * BLOCK;      // samples per tile: 4 per thread, one 16-B store each
+// tiles per stripe workgroup: 8 / 12 / 20 / 24 / 32 measured 0.419 / 0.346 /
+// 0.315 / 0.325 / 0.345 ms against 0.313 for 16 (config 5)
+constexpr uint32_t DDS_TILES_PER_STRIPE = 16;
 constexpr uint32_t DDS_ENV_LDS_MAX = 8192;    // words: tables up to 32 KiB are staged in LDS
 constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;   // words: 64 freq entries as (R, R') pairs
 
-// dynamic LDS bytes of dds_synth_kernel: quarter sine table (entries
-// 0..1031) | record area (16-B strobe records, 4-B reset times) | env | freq |
+// dynamic LDS bytes of dds_tile_kernel: quarter sine table (entries
+// 0..1031) | strobe records (16 B) | reset times | tile windows | env | freq |
 // the cycle sweep's per-wave store transpose (1 KiB per wave)
 constexpr uint32_t DDS_LUT_BYTES = 1032 * 2;
 constexpr uint32_t DDS_XPOSE_BYTES = (BLOCK / 64) * 1024;
-__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t rec_bytes, uint32_t env_lds, uint32_t freq_lds)
+__host__ __device__ inline uint32_t dds_lds_bytes(uint32_t rec_lds, uint32_t tiles_per_stripe, uint32_t env_lds,
+                                                  uint32_t freq_lds)
 {
-    return DDS_LUT_BYTES + rec_bytes + (env_lds + freq_lds) * 4 + DDS_XPOSE_BYTES;
+    return DDS_LUT_BYTES + rec_lds * 20 + tiles_per_stripe * 16 + (env_lds + freq_lds) * 4 + DDS_XPOSE_BYTES;
 }
-// LDS budget of a workgroup: 8 workgroups (32 waves) share a CU's 160 KiB.
-// The record area is 16 B x event_cap when that fits (every record of a lane
-// fits: one staging per workgroup), else what is left of the budget (at least
-// DDS_REC_MIN records of each kind) and the multi-pass kernel.
+// LDS budget of a tile workgroup: 8 workgroups (32 waves, the VGPR-bound
+// occupancy) share a CU's 160 KiB.  The record capacity is what is left of
+// it (at least DDS_REC_LDS_MIN); a stripe whose window holds more strobes or
+// resets than that reads them from the global index instead.
 // (less 512 B: the compiler's static LDS of the kernel, so 8 fit in 160 KiB)
 constexpr uint32_t DDS_WG_LDS_BUDGET = 20 * 1024 - 512;
-constexpr uint32_t DDS_REC_MIN = 64;
-#ifndef DDS_SEG_TILES
-#define DDS_SEG_TILES 52
-#endif
-constexpr uint32_t DDS_SEG = DDS_SEG_TILES;   // tiles per workgroup (A/B: -DDDS_SEG_TILES=)
+constexpr uint32_t DDS_REC_LDS_MIN = 64;
 
 // LDS words of an interp-1 envelope of n words staged as swizzled (E, E')
 // pairs (dds.hip env_pair): whole groups of 8 16-B chunks
 __host__ __device__ inline uint32_t dds_env_pairs_words(uint32_t n) { return (2 * n + 31) & ~31u; }
 
+// bytes of the event index (xs, xr, win)
+inline uint64_t dds_index_bytes(uint32_t n_channels, uint32_t ev_lds, uint32_t tiles)
+{
+    return (uint64_t)n_channels * ev_lds * 20 + (uint64_t)n_channels * tiles * 16;
+}
+
+hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream);
 hipError_t launch_dds(const DDSParams &p, hipStream_t stream);
 
 }  // namespace dpemu

@@ -53,9 +53,6 @@ __device__ __forceinline__ uint3 philox3(uint64_t seed, uint64_t shot, uint32_t 
 {
     uint32_t c0 = (uint32_t)shot, c1 = (uint32_t)(shot >> 32), c2 = core, c3 = m;
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#ifdef LANE_PROBE_NORNG                     // A/B probe only: the generator's cost (wrong outcomes)
-    if (k0 != 12345u) return make_uint3(c0 * 0x9E3779B9u ^ c3 * 0x85EBCA6Bu ^ c2, c0 ^ c3, c2 + c3);
-#endif
 #pragma unroll
     for (int r = 0; r < 10; r++) {
         const uint64_t p0 = mul_wide(c0, 0xD2511F53u), p1 = mul_wide(c2, 0xCD9E8D57u);

@@ -113,11 +113,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
     // come from the final counts.
     auto emit = [&](bool ok, uint32_t te, uint32_t kind, uint32_t reps) __attribute__((always_inline)) {
         for (uint32_t r = 0; r < (ok ? reps : 0u); r++) {
-#ifdef MACRO_PROBE_NOSTORE                              // A/B probe only (scripts/ab_libs.sh): no event stores
-            if (n_ev == 0xFFFFFFFFu)
-#else
             if (n_ev < p.event_cap && p.events)
-#endif
                 p.events[(uint64_t)n_ev * n_lanes + lane] = event_record(te + r, pe, pp, pa, kind);
             n_ev++;
             const bool is_meas = kind == 0u && ((pe >> 24) & 3u) == p.meas_elem;   // meas_elem 0xFF: none
@@ -272,11 +268,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
     // macro m of this lane's program (ALU slots, pulse slot); in bounds: the
     // terminal macro repeats
     const uint4 *mbase = p.macros;
-#ifdef MACRO_PROBE_NOFETCH                              // A/B probe only: every fetch hits macro 0..1 (L1)
-    auto addr = [&](uint32_t m) __attribute__((always_inline)) -> const uint4 * { return mbase + 2ull * min(mb + (m & 1u), ml); };
-#else
     auto addr = [&](uint32_t m) __attribute__((always_inline)) -> const uint4 * { return mbase + 2ull * min(mb + m, ml); };
-#endif
 
     // one macro ahead: macro m + 1 is in flight while macro m executes
     uint4 an = addr(0u)[0], un = addr(0u)[1];
@@ -345,7 +337,6 @@ struct MacroLane {
     uint32_t t, pe, pp, pa, qa_t, qa_q;
     uint32_t flags, n_ev, n_meas, meas_bits, last_bit, n_tr, k, st;
     uint4 *evp;                            // event slot n_ev of this lane
-    uint32_t it = 0;                       // (A/B probe MACRO_PROBE_ITERSLOT only)
     bool tr_on, ev_on;
     static constexpr uint32_t ST_TOP = 0x100u;
 
@@ -392,16 +383,8 @@ struct MacroLane {
     __device__ __forceinline__ void emit1(bool ok, uint32_t te, uint32_t kind)
     {
         if (ok) {
-#ifdef MACRO_PROBE_NOSTORE                              // A/B probe only: no event stores
-            if (n_ev == 0xFFFFFFFFu)
-#else
             if (n_ev < p.event_cap && ev_on)
-#endif
-#ifdef MACRO_PROBE_ITERSLOT                             // A/B probe only: record at slot = macro iteration
-                p.events[(uint64_t)min(it, p.event_cap - 1u) * p.n_lanes + lane] = event_record(te, pe, pp, pa, kind);
-#else
                 *evp = event_record(te, pe, pp, pa, kind);
-#endif
             evp += p.n_lanes;
             n_ev++;
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {        // meas_elem 0xFF: none
@@ -605,12 +588,17 @@ struct MacroLane {
     // B + 11 m, B = max(t, Tmax + qa_t - qa_q): B + 11 (CH - 1) + 8 <=
     // max_cycles keeps every macro's decodes inside max_cycles -- lean_ok at
     // every macro, without testing it.  (A late pulse stops its lane, which
-    // the lean pulse slot handles.)
+    // the lean pulse slot handles.)  The argument holds while qclk cannot
+    // wrap before max_cycles (qa_q + max_cycles - qa_t < 2^32): then a
+    // cmd_time below qclk(D) waits past max_cycles and stops the lane; after a
+    // wrap (an inc_qclk by a negative value) a small cmd_time would fire
+    // later than B, so such lanes take the per-macro tests.
     __device__ __forceinline__ bool lean_chunk_ok(uint32_t info) const
     {
         const uint64_t tc = (uint64_t)info + qa_t;                       // Tmax's cycle + qa_q
         const uint64_t b = max((uint64_t)t, tc > qa_q ? tc - qa_q + 3u : 0ull);
-        const bool ok = info != MACRO_CHUNK_MIXED && b + 12ull * MACRO_CHUNK + 8u <= p.max_cycles;
+        const bool no_wrap = (uint64_t)qa_q + p.max_cycles < (1ull << 32) + qa_t;
+        const bool ok = info != MACRO_CHUNK_MIXED && no_wrap && b + 12ull * MACRO_CHUNK + 8u <= p.max_cycles;
         return !tr_on && !__ballot(st == 0u && !ok);
     }
     static __device__ __forceinline__ uint32_t bmask(uint32_t v, int b)     // bit b of v as 0 / ~0
@@ -675,11 +663,8 @@ struct MacroLane {
     }
 };
 
-#ifndef MACRO_STAGED_WAVES
-#define MACRO_STAGED_WAVES 4
-#endif
 template <int NR, bool ADDID>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR == 16 ? 3 : MACRO_STAGED_WAVES))) macro_staged_kernel(const KParams p)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR == 16 ? 3 : 4))) macro_staged_kernel(const KParams p)
 {
     constexpr uint32_t NW = BLOCK / 64, CH = MACRO_CHUNK, NS = MACRO_SLOTS;
     constexpr uint32_t PIECES = NS * CH * 2;          // 16-B pieces of a chunk
@@ -710,7 +695,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
         prog = p.prog_table[(uint64_t)grp * C + core];
         mb = p.macro_off[prog];
         ml = p.macro_off[prog + 1] - 1u;
-        if constexpr (NR == 2 && MACRO_CHUNK_LEAN) cb = p.macro_coff[prog];
+        if constexpr (NR == 2) cb = p.macro_coff[prog];
     }
     if (p.hist_lds) {
         for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
@@ -770,7 +755,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
                 __builtin_amdgcn_global_load_lds(mbase + 2ull * min(b0 + m, l0) + ph, buf + r * 64u, 16, 0, 0);
             }
         }
-        if constexpr (NR == 2 && MACRO_CHUNK_LEAN) {
+        if constexpr (NR == 2) {
             if (wl < min(nslots, NS)) {
                 const uint32_t ci = min(c, (s_sml[wv][wl] - s_smb[wv][wl]) / CH);
                 __builtin_amdgcn_global_load_lds(p.macro_chunk + s_scb[wv][wl] + ci, info, 4, 0, 0);
@@ -786,7 +771,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
     // is waited for (vmcnt(0)) once per phase
     auto phase = [&](const uint4 *buf, const uint32_t *info) __attribute__((always_inline)) {
         const uint4 *const cur = buf + moff;
-        if constexpr (NR == 2 && MACRO_CHUNK_LEAN) {
+        if constexpr (NR == 2) {
             // one wave test for the whole chunk, then CH macros with no test
             // and no branch between them but the stores' own
             if (L.lean_chunk_ok(info[slot])) {
@@ -804,9 +789,6 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
 #pragma unroll 1
         for (uint32_t i = 0; i < CH; i++) {
             const uint4 a = cur[2 * i], u = cur[2 * i + 1];
-#ifdef MACRO_PROBE_ITERSLOT
-            L.it++;
-#endif
             if constexpr (NR == 2) {
                 if (L.lean_ok(u)) {
                     const uint32_t run = L.st == 0u ? ~0u : 0u;

@@ -33,15 +33,33 @@ class DpemuOutputs(C.Structure):                   # dpemu_outputs
 _L = None
 
 
+def hip_runtimes():
+    """paths of the HIP runtimes (libamdhip64) mapped into this process"""
+    try:
+        with open('/proc/self/maps') as f:
+            return sorted({ln.split()[-1] for ln in f if 'libamdhip64' in ln})
+    except OSError:
+        return []
+
+
 def load(path='libdpemu.so'):
     """bind the library once: entry points, ABI version, struct layouts.
-    A process that also uses PyTorch-ROCm imports torch first: libdpemu.so
-    then binds torch's HIP runtime, and both see the GPU (one runtime per
-    process)."""
+    One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64, and
+    a torch imported AFTER libdpemu.so bound /opt/rocm's would start a second
+    runtime that sees no GPU.  So when torch is installed it is imported
+    first (libdpemu.so then binds torch's runtime), and two runtimes already
+    mapped raise here instead of failing later."""
     global _L
     if _L is not None:
         return _L
+    try:
+        import torch  # noqa: F401  (its HIP runtime, before libdpemu.so's dependency resolves)
+    except ImportError:
+        pass
     L = C.CDLL(path)
+    if len(hip_runtimes()) > 1:
+        raise RuntimeError('two HIP runtimes in one process ({}): load torch before other HIP '
+                           'libraries'.format(', '.join(hip_runtimes())))
     L.dpemu_abi_version.restype = C.c_int
     if L.dpemu_abi_version() != ABI_VERSION:
         raise RuntimeError('libdpemu ABI {} != {}'.format(L.dpemu_abi_version(), ABI_VERSION))

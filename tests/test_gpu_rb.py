@@ -23,7 +23,7 @@ import pytest
 
 import oracle
 from distributed_processor_amd import _abi, isa, workloads
-from distributed_processor_amd.emulator import Emulator, alloc_device_outputs
+from distributed_processor_amd.emulator import Emulator, ProgramSet, alloc_device_outputs
 
 pytestmark = pytest.mark.gpu
 
@@ -161,3 +161,34 @@ def test_rb_lean_path_edges(max_cycles):
                 # shot-major waves span 5 sequences x 2 cores > MACRO_SLOTS: the per-lane macro_kernel
                 want = 'macro_staged_kernel<2,addid>' if order == _abi.LANES_CORE_MAJOR else 'macro_kernel'
                 assert emu.last_kernel() == want, emu.last_kernel()
+
+
+@pytest.mark.parametrize('max_cycles', [1400, 1500, 1560, 1620, 4000])
+def test_lean_chunk_after_qclk_wrap(max_cycles):
+    """an inc_qclk by a negative value puts qclk just below 2^32, so the next
+    pulses' small cmd_times fire only after qclk wraps (~1000 cycles later):
+    the lean-chunk bound (macro.hip lean_chunk_ok) must not take those chunks
+    as inside max_cycles.  40 reg_alu + pulse macros after the wrap (whole
+    16-macro chunks of MACRO_SIMPLE macros), max_cycles inside and past them;
+    every output against oracle_fast"""
+    from tests.test_gpu_parity import compare_all, run_pair
+
+    def core(w, step):
+        words = [isa.pulse_reset(), isa.reg_alu_i(0, 'id0', 0, 1), isa.inc_qclk_i(-w)]
+        for k in range(40):
+            words.append(isa.reg_alu_i(5, 'add', 1, 1))
+            words.append(isa.pulse_i(freq_word=3, phase_word=0, amp_word=100, env_word=1 | (4 << 12),
+                                     cfg_word=0, cmd_time=10 + step * k))
+        words.append(isa.done_cmd())
+        return isa.words_to_bytes(words)
+    ps = ProgramSet([{0: core(1000, 20), 1: core(1100, 17)}])
+    cfg = _abi.make_config(2, n_groups=1, max_cycles=max_cycles, event_cap=48, trace_cap=0, meas_cap=2,
+                           meas_latency=64, seed=7, p1=0.5)
+    with Emulator(0) as emu:
+        g, f = run_pair(emu, ps, cfg, 256)
+        compare_all(g, f, 'qclk wrap, max_cycles {}'.format(max_cycles))
+        emu.run(3, 0, cfg=cfg)
+        assert emu.last_kernel() == 'macro_staged_kernel<2,addid>', emu.last_kernel()
+    status = _abi.unpack_summary(np.asarray(g['summary']).view(np.uint32))['status']
+    if max_cycles < 1600:
+        assert (status == _abi.ST_MAX_CYCLES).all()

@@ -44,9 +44,8 @@ def test_integration_doc_holds_the_module_verbatim():
 
 
 def bind():
-    """the binding on the in-tree library; torch's HIP runtime first (the
-    GPU tests use torch in the same process, ref_binding.load)"""
-    _native.load_library()
+    """the binding on the in-tree library, loaded the way a distproc user
+    would load it (ref_binding.load brings in torch's HIP runtime itself)"""
     return ref_binding.load(_native.LIB_PATH)
 
 
@@ -115,3 +114,44 @@ def test_run_assembled_vs_oracle(which):
         # the reference's golden core 0: pulse_reset at 0, cstrobes at 8 / 24 / 324
         # (test_gpu_parity.test_config1_golden_program; lane = core * n_shots + shot)
         assert [int(e[0]) for e in ev[:4, 0]] == [0, 8, 24, 324]
+
+
+CHILD = r'''
+import sys
+sys.path.insert(0, {repo!r})
+from tests import ref_binding
+L = ref_binding.load({lib!r})                  # the binding first, as a distproc user would
+import torch                                    # then PyTorch
+assert torch.cuda.device_count() > 0, 'torch sees no GPU after the binding loaded'
+runtimes = ref_binding.hip_runtimes()
+assert len(runtimes) == 1, runtimes
+x = torch.arange(1024, device='cuda', dtype=torch.int32)
+assert int(x.sum().item()) == 1023 * 1024 // 2
+cfg = ref_binding.DpemuConfig()
+cfg.max_cycles, cfg.event_cap, cfg.meas_cap, cfg.meas_latency, cfg.sync_latency = 4000, 8, 2, 64, 1
+for i in range(64):
+    cfg.p1_threshold[i] = 1 << 31
+golden = {golden!r}
+asm = {{k: {{'cmd_buf': bytes.fromhex(v), 'env_buffers': [], 'freq_buffers': []}} for k, v in golden.items()}}
+summary, ev, meas, hist = ref_binding.run_assembled(asm, 1000, cfg, path={lib!r})
+assert [int(e[0]) for e in ev[:4, 0]] == [0, 8, 24, 324], ev[:4, 0]
+print('ok', torch.cuda.device_count(), runtimes[0])
+'''
+
+
+@pytest.mark.gpu
+@pytest.mark.fresh_process
+def test_binding_first_then_torch_in_a_fresh_process():
+    """INTEGRATION.md §3 as a distproc user runs it: a fresh Python loads the
+    binding BEFORE importing torch, then uses torch on the GPU and runs the
+    reference's golden cmd_buf through the binding -- one HIP runtime, torch
+    sees the device.  (Runs first in the session, before this process touches
+    the GPU: tests/conftest.py orders fresh_process tests.)"""
+    import subprocess
+    import sys
+    with open(os.path.join(HERE, 'golden', 'cmd_buf_golden.json')) as f:
+        gold = {k: v['cmd_buf'] for k, v in json.load(f)['cores'].items()}
+    src = CHILD.format(repo=REPO, lib=_native.LIB_PATH, golden=gold)
+    r = subprocess.run([sys.executable, '-c', src], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.startswith('ok'), r.stdout
