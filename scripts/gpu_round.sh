@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round evidence on one GPU box: full -m gpu suite, smoke, then the same-box
 # rocprofv3 + PMC passes and the bench line (scripts/evidence.sh).
-# usage (on the box): bash scripts/gpu_round.sh gpurun_out/<dir>
+# usage (on the box): bash scripts/gpu_round.sh gpurun_out/<dir> [tag]
 set -o pipefail
 out=$1
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
@@ -12,4 +12,4 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 tail -2 $out/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { echo "smoke failed"; tail $out/smoke.log; exit 1; }
 tail -1 $out/smoke.log
-bash scripts/evidence.sh $out || exit 1
+bash scripts/evidence.sh $out $2 || exit 1

@@ -127,10 +127,10 @@ runtimes = ref_binding.hip_runtimes()
 assert len(runtimes) == 1, runtimes
 x = torch.arange(1024, device='cuda', dtype=torch.int32)
 assert int(x.sum().item()) == 1023 * 1024 // 2
-cfg = ref_binding.DpemuConfig()
-cfg.max_cycles, cfg.event_cap, cfg.meas_cap, cfg.meas_latency, cfg.sync_latency = 4000, 8, 2, 64, 1
-for i in range(64):
-    cfg.p1_threshold[i] = 1 << 31
+import ctypes
+cfg = ref_binding.DpemuConfig()                 # filled by the parent (make_config), byte for byte
+raw = bytes.fromhex({cfg_hex!r})
+ctypes.memmove(ctypes.addressof(cfg), raw, len(raw))
 golden = {golden!r}
 asm = {{k: {{'cmd_buf': bytes.fromhex(v), 'env_buffers': [], 'freq_buffers': []}} for k, v in golden.items()}}
 summary, ev, meas, hist = ref_binding.run_assembled(asm, 1000, cfg, path={lib!r})
@@ -151,7 +151,8 @@ def test_binding_first_then_torch_in_a_fresh_process():
     import sys
     with open(os.path.join(HERE, 'golden', 'cmd_buf_golden.json')) as f:
         gold = {k: v['cmd_buf'] for k, v in json.load(f)['cores'].items()}
-    src = CHILD.format(repo=REPO, lib=_native.LIB_PATH, golden=gold)
+    cfg, _ = binding_config(2, max_cycles=4000, event_cap=8, meas_cap=2, meas_latency=64, p1=0.5)
+    src = CHILD.format(repo=REPO, lib=_native.LIB_PATH, golden=gold, cfg_hex=bytes(cfg).hex())
     r = subprocess.run([sys.executable, '-c', src], capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert r.stdout.startswith('ok'), r.stdout
