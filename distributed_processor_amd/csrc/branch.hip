@@ -86,12 +86,6 @@ __device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t C)
     return v;
 }
 
-// per-component select (keeps the pending event records in registers)
-__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b)
-{
-    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
-}
-
 // minimum over the whole wave (all lanes converged): DPP within each row of
 // 16, then the four rows' minima by readlane
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)

@@ -53,6 +53,7 @@ struct dpemu_ctx {
     // register slots of the macro image (remap_macro_regs): 2 or 4 in VGPRs, else 16 (identity map)
     int macro_nr = 16;
     bool macro_addid = false;               // every ALU slot of the macro image is id0 / add
+    bool macro_w3 = false;                  // the macro image has three ALU slots (kernels.h MACRO_W3)
     uint32_t macro_rs = 0;                  // UOP_RS_* fields its pulse slots register-source
     uint64_t reg_map = 0xFEDCBA9876543210ull, reg_inv = 0xFEDCBA9876543210ull;
     uint32_t reg_used = 0xFFFFu;
@@ -144,20 +145,22 @@ static hipError_t timing_start(dpemu_ctx *ctx, hipStream_t stream, hipEvent_t *s
 
 // Macro image of a branch-free program (macro.hip): from its decoded
 // commands u[0, n) (and the zero = DONE guard past the end), macros of up to
-// two consecutive reg_alu / inc_qclk commands followed by the next other
+// `max_alu` consecutive reg_alu / inc_qclk commands followed by the next other
 // command, until the first terminal command (done / 0000 / hang) -- the
 // program's last macro, which the kernel re-reads once a lane has finished.
-// Per macro 8 u32: {imm0, ctl0, imm1, ctl1} then the pulse slot's decode_cmd
-// word (w bit 31 = no command).  ctl = present[31] inc_qclk[30] rs0[15:12]
-// rd[11:8] rs1[7:4] in0_reg[3] alu_op[2:0].
-static void build_macros(const uint32_t *u, uint32_t n, std::vector<uint32_t> &out)
+// Built WIDE, MACRO_WIDE u32 per macro: {imm, ctl} x 3 ALU slots then the
+// pulse slot's decode_cmd word (w bit 31 = no command); ctl = present[31]
+// inc_qclk[30] rs0[15:12] rd[11:8] rs1[7:4] in0_reg[3] alu_op[2:0].
+// pack_macros turns it into the 32-B device image (kernels.h MACRO_W3).
+constexpr uint32_t MACRO_WIDE = 10;
+static void build_macros(const uint32_t *u, uint32_t n, uint32_t max_alu, std::vector<uint32_t> &out)
 {
     static const uint32_t zero[4] = {0, 0, 0, 0};
     uint32_t k = 0;
     for (;;) {
-        uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, MACRO_ABSENT};
+        uint32_t m[MACRO_WIDE] = {0, 0, 0, 0, 0, 0, 0, 0, 0, MACRO_ABSENT};
         const uint32_t *c = k < n ? u + 4ull * k : zero;
-        for (int a = 0; a < 2; a++) {
+        for (uint32_t a = 0; a < max_alu; a++) {
             const uint32_t op4 = c[1] >> 28;
             if (op4 != 0x1 && op4 != 0x6) break;
             m[2 * a] = c[0];
@@ -166,12 +169,41 @@ static void build_macros(const uint32_t *u, uint32_t n, std::vector<uint32_t> &o
             c = k < n ? u + 4ull * k : zero;
         }
         const uint32_t op4 = c[1] >> 28;
-        if (op4 != 0x1 && op4 != 0x6) {        // the slot's command (else: a third ALU command opens the next macro)
-            memcpy(m + 4, c, 16);
+        if (op4 != 0x1 && op4 != 0x6) {        // the slot's command (else: another ALU command opens the next macro)
+            memcpy(m + 6, c, 16);
             k++;
         }
-        out.insert(out.end(), m, m + 8);
+        out.insert(out.end(), m, m + MACRO_WIDE);
         if (op4 == 0x0 || op4 == 0xA || op4 >= 0xD) return;
+    }
+}
+
+// ALU slot k's ctl of a packed macro (8 u32, macro.hip): legacy {imm0, ctl0,
+// imm1, ctl1, pulse}, or MACRO_W3 {imm0, packed ctl, imm1, imm2, pulse}
+static uint32_t macro_ctl(const uint32_t *m, int k, bool w3)
+{
+    if (!w3) return k < 2 ? m[2 * k + 1] : 0u;
+    return w3_ctl(m[1], k);
+}
+
+// The 32-B device image from the wide one: MACRO_W3 packs three ALU slots
+// (their ctl fields with 1-bit register slots, kernels.h w3_pack) when the
+// image names at most 2 registers; else two slots, legacy layout.
+static void pack_macros(const std::vector<uint32_t> &wide, bool w3, std::vector<uint32_t> &mac)
+{
+    const size_t n = wide.size() / MACRO_WIDE;
+    mac.resize(8 * n);
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t *w = &wide[MACRO_WIDE * i];
+        uint32_t *m = &mac[8 * i];
+        if (w3) {
+            uint32_t pk = 0;
+            for (int k = 0; k < 3; k++) pk |= w3_pack(w[2 * k + 1]) << (10 * k);
+            m[0] = w[0]; m[1] = pk; m[2] = w[2]; m[3] = w[4];
+        } else {
+            m[0] = w[0]; m[1] = w[1]; m[2] = w[2]; m[3] = w[3];
+        }
+        memcpy(m + 4, w + 6, 16);
     }
 }
 
@@ -187,8 +219,8 @@ static void build_macros(const uint32_t *u, uint32_t n, std::vector<uint32_t> &o
 static int remap_macro_regs(std::vector<uint32_t> &mac, uint64_t &map, uint64_t &inv, uint32_t &used)
 {
     used = 0;
-    for (size_t i = 0; i < mac.size(); i += 8) {
-        for (int a = 0; a < 2; a++) {
+    for (size_t i = 0; i < mac.size(); i += MACRO_WIDE) {
+        for (int a = 0; a < 3; a++) {
             const uint32_t ctl = mac[i + 2 * a + 1];
             if (!(ctl >> 31)) continue;
             const uint32_t op = ctl & 7u;                       // alu.v: 0 id0, 6 id1, 7 zero
@@ -198,7 +230,7 @@ static int remap_macro_regs(std::vector<uint32_t> &mac, uint64_t &map, uint64_t 
                 if (op != 0u && op != 7u) used |= 1u << ((ctl >> 4) & 15u);
             }
         }
-        const uint32_t w = mac[i + 7];
+        const uint32_t w = mac[i + 9];
         if (!(w >> 31) && (w & UOP_ANY_RS)) used |= 1u << ((w >> 20) & 15u);
     }
     const int n = __builtin_popcount(used);
@@ -212,12 +244,12 @@ static int remap_macro_regs(std::vector<uint32_t> &mac, uint64_t &map, uint64_t 
     for (uint32_t r = 0, k = 0; r < 16; r++)
         if ((used >> r) & 1u) { slot[r] = k; map |= (uint64_t)k << (4 * r); inv |= (uint64_t)r << (4 * k); k++; }
     auto re = [&](uint32_t v, int sh) { return (v & ~(15u << sh)) | (slot[(v >> sh) & 15u] << sh); };
-    for (size_t i = 0; i < mac.size(); i += 8) {
-        for (int a = 0; a < 2; a++) {
+    for (size_t i = 0; i < mac.size(); i += MACRO_WIDE) {
+        for (int a = 0; a < 3; a++) {
             uint32_t &ctl = mac[i + 2 * a + 1];
             if (ctl >> 31) ctl = re(re(re(ctl, 12), 8), 4);
         }
-        uint32_t &w = mac[i + 7];
+        uint32_t &w = mac[i + 9];
         if (!(w >> 31) && (w & UOP_ANY_RS)) w = re(w, 20);
     }
     return 2;
@@ -226,7 +258,7 @@ static int remap_macro_regs(std::vector<uint32_t> &mac, uint64_t &map, uint64_t 
 // Mark every macro of the lean-path shape (MACRO_SIMPLE, kernels.h) in the
 // image's pulse slots, and return whether every ALU slot is reg_alu id0 / add
 // (alu.v ops 0 / 1) and which pulse fields are register-sourced
-static bool mark_simple_macros(std::vector<uint32_t> &mac, const std::vector<uint32_t> &moff, uint32_t &rs)
+static bool mark_simple_macros(std::vector<uint32_t> &mac, const std::vector<uint32_t> &moff, bool w3, uint32_t &rs)
 {
     bool addid = true;
     rs = 0;
@@ -235,8 +267,8 @@ static bool mark_simple_macros(std::vector<uint32_t> &mac, const std::vector<uin
         while (prog + 1 < moff.size() && moff[prog + 1] <= m) prog++;
         const bool first = moff[prog] == m;
         bool simple = !first;
-        for (int a = 0; a < 2; a++) {
-            const uint32_t ctl = mac[i + 2 * a + 1];
+        for (int a = 0; a < 3; a++) {
+            const uint32_t ctl = macro_ctl(&mac[i], a, w3);
             if (!(ctl >> 31)) continue;
             if ((ctl >> 30) & 1u) simple = false;               // inc_qclk
             if ((ctl & 7u) > 1u) addid = false;
@@ -440,16 +472,30 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, 
     }
     // ... and the macro image of branch-free programs with register commands
     if (linear && !straight && max_len < 65536u) {
-        std::vector<uint32_t> mac, moff(n_programs + 1);
-        mac.reserve(tot * 4 + 8ull * n_programs);
-        for (uint32_t pr = 0; pr < n_programs; pr++) {
-            moff[pr] = (uint32_t)(mac.size() / 8);
-            build_macros(&uops[4ull * goff[pr]], n_instr[pr], mac);
-            if (mac.size() / 8 >= (1ull << 32)) return fail(ctx, DPEMU_E_INVALID, "macro image exceeds 2^32 macros");
+        // three ALU slots per macro when the image names at most 2 registers
+        // (MACRO_W3: RB-like programs then have almost no macro without a
+        // pulse, so a wave's programs stay on the same event slot and its
+        // stores are whole rows), else two
+        std::vector<uint32_t> wide, mac, moff(n_programs + 1);
+        bool w3 = true;
+        for (int attempt = 0; attempt < 2; attempt++) {
+            wide.clear();
+            wide.reserve((tot * 4 + 8ull * n_programs) / 8 * MACRO_WIDE);
+            for (uint32_t pr = 0; pr < n_programs; pr++) {
+                moff[pr] = (uint32_t)(wide.size() / MACRO_WIDE);
+                build_macros(&uops[4ull * goff[pr]], n_instr[pr], w3 ? 3u : 2u, wide);
+                if (wide.size() / MACRO_WIDE >= (1ull << 32))
+                    return fail(ctx, DPEMU_E_INVALID, "macro image exceeds 2^32 macros");
+            }
+            moff[n_programs] = (uint32_t)(wide.size() / MACRO_WIDE);
+            ctx->macro_nr = remap_macro_regs(wide, ctx->reg_map, ctx->reg_inv, ctx->reg_used);
+            if (ctx->macro_nr == 2 || !w3) break;
+            w3 = false;                               // 16 registers: the two-slot layout
         }
-        moff[n_programs] = (uint32_t)(mac.size() / 8);
-        ctx->macro_nr = remap_macro_regs(mac, ctx->reg_map, ctx->reg_inv, ctx->reg_used);
-        ctx->macro_addid = mark_simple_macros(mac, moff, ctx->macro_rs);
+        ctx->macro_w3 = w3;
+        pack_macros(wide, w3, mac);
+        std::vector<uint32_t>().swap(wide);
+        ctx->macro_addid = mark_simple_macros(mac, moff, w3, ctx->macro_rs);
         HIPCHK(ctx, hipMalloc(&ctx->d_macro, mac.size() * 4));
         HIPCHK(ctx, hipMemcpy(ctx->d_macro, mac.data(), mac.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(ctx, hipMalloc(&ctx->d_moff, moff.size() * 4));
@@ -544,6 +590,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.macro_chunk = ctx->d_mchunk; p.macro_coff = ctx->d_mcoff;
     p.reg_map = ctx->reg_map; p.reg_inv = ctx->reg_inv; p.reg_used = ctx->reg_used;
     p.macro_rs = ctx->macro_rs;
+    p.macro_w3 = ctx->macro_w3 ? 1u : 0u;
     p.p1_thr = ctx->d_thr; p.lut_table = ctx->d_lut;
     p.summary = out->summary;
     p.events = reinterpret_cast<uint4 *>(out->events);

@@ -130,6 +130,7 @@ struct KParams {
     uint64_t reg_inv;             //   for r in the reg_used mask (others are never named: they read 0);
     uint32_t reg_used;            //   slot s holds register (reg_inv >> 4 s) & 15 (trace addresses)
     uint32_t macro_rs;            // UOP_RS_* fields some pulse slot of the macro image register-sources
+    uint32_t macro_w3;            // the macro image is MACRO_W3 (three ALU slots; always with 2 register slots)
     const uint32_t *p1_thr;
     const uint64_t *lut_table;
     // outputs (device, nullable); lane L = core * n_shots + shot (core-major)
@@ -191,6 +192,26 @@ constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no comm
 // lean path (runtime conditions permitting)
 constexpr uint32_t MACRO_SIMPLE = 0x40000000u;
 constexpr uint32_t MACRO_CHUNK_MIXED = 0xFFFFFFFFu;   // macro_chunk: not every macro MACRO_SIMPLE
+// MACRO_W3 image (KParams::macro_w3; the image names at most 2 registers):
+// THREE ALU slots in the same 32 B, {imm0, packed ctl, imm1, imm2} + pulse
+// slot.  Slot k's ctl is the 9-bit field at bit 10 k: op[2:0] in0_reg[3]
+// rs1[4] rd[5] rs0[6] inc_qclk[7] present[8] (register fields are slots 0 /
+// 1 after capi.cpp remap_macro_regs).  w3_ctl expands a field to the legacy
+// ctl layout (present[31] inc_qclk[30] rs0[15:12] rd[11:8] rs1[7:4]
+// in0_reg[3] op[2:0]); w3_pack is its inverse on 1-bit register fields.
+constexpr uint32_t W3_OP = 0, W3_IN0 = 3, W3_RS1 = 4, W3_RD = 5, W3_RS0 = 6, W3_INC = 7, W3_PRES = 8;
+__host__ __device__ inline uint32_t w3_ctl(uint32_t packed, int k)
+{
+    const uint32_t f = packed >> (10 * k);
+    return (f & 0x1Fu) | (((f >> W3_RD) & 1u) << 8) | (((f >> W3_RS0) & 1u) << 12) | (((f >> W3_INC) & 1u) << 30) |
+           (((f >> W3_PRES) & 1u) << 31);
+}
+__host__ __device__ inline uint32_t w3_pack(uint32_t ctl)
+{
+    if (!(ctl >> 31)) return 0u;
+    return (ctl & 0x1Fu) | (((ctl >> 8) & 1u) << W3_RD) | (((ctl >> 12) & 1u) << W3_RS0) |
+           (((ctl >> 30) & 1u) << W3_INC) | (1u << W3_PRES);
+}
 
 // ---- DDS ------------------------------------------------------------------
 // Two launches per synthesis (dds.hip): dds_index_kernel compacts each

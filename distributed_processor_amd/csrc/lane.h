@@ -6,6 +6,13 @@
 
 namespace dpemu {
 
+// per-component select (keeps the pending event records in registers)
+__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b)
+{
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+
 #define INF32 0xFFFFFFFFu
 
 // pulse_reg.sv:59-97 for a pre-decoded pulse command (decode_cmd): each field

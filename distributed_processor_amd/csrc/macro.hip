@@ -7,10 +7,12 @@
 // program into MACROS of one fixed shape (capi.cpp build_macros):
 //
 //     [ALU slot 0][ALU slot 1][pulse slot]          32 B
+//     [imm0][ctl 0-2 packed][imm1][imm2][pulse slot]   32 B (MACRO_W3)
 //
-// up to two consecutive reg_alu / inc_qclk commands followed by the next
-// other command (pulse write / trigger, idle, pulse reset, done, hang),
-// each slot marked present or absent.  Every lane still running in loop
+// up to two (three: MACRO_W3, images that name at most 2 registers)
+// consecutive reg_alu / inc_qclk commands followed by the next other command
+// (pulse write / trigger, idle, pulse reset, done, hang), each slot marked
+// present or absent.  Every lane still running in loop
 // iteration m executes macro m of its own program, so a wave of lanes with
 // DIFFERENT programs (a depth-200 RB table: ~7 sequences per wave) runs one
 // code path per iteration -- two ALU slots, one pulse slot, selects for the
@@ -279,8 +281,14 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
             an = q[0];
             un = q[1];
         }
-        alu_step(a.x, a.y);
-        alu_step(a.z, a.w);
+        if (p.macro_w3) {                               // (uniform) three ALU slots, ctl packed in a.y
+            alu_step(a.x, w3_ctl(a.y, 0));
+            alu_step(a.z, w3_ctl(a.y, 1));
+            alu_step(a.w, w3_ctl(a.y, 2));
+        } else {
+            alu_step(a.x, a.y);
+            alu_step(a.z, a.w);
+        }
         pulse_step(u);
     }
     flags |= (n_ev > p.event_cap ? F_EVENT_OVF : 0u) | (n_meas > min(p.meas_cap, MEAS_LOOKUP) ? F_MEAS_OVF : 0u) |
@@ -330,6 +338,11 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
 
 template <int NR, bool ADDID>
 struct MacroLane {
+    // NR == 2 images are MACRO_W3 (capi.cpp: three ALU slots whenever the
+    // image names at most 2 registers); their last ALU slot decodes at t + 8,
+    // the pulse slot at t + 12 (t + 4 / t + 8 with two slots)
+    static constexpr bool W3 = NR == 2;
+    static constexpr uint32_t SPAN = W3 ? 12u : 8u;
     const KParams &p;
     uint32_t *s_regs_lane;                 // NR == 16: &s_regs[0][tid], stride BLOCK
     uint32_t lane, sl, core;
@@ -554,8 +567,11 @@ struct MacroLane {
     // ballots and the uniform-op switch (a chain of scalar branches).
     __device__ __forceinline__ bool simple_ok(const uint4 a, const uint4 u) const
     {
-        const bool bad = ((int32_t)a.y < 0 && (a.y & 0x40000000u)) || ((int32_t)a.w < 0 && (a.w & 0x40000000u)) ||
-                         ((int32_t)u.w >= 0 && (u.y >> 28) != 0x9u) || t < qa_t || t + 8u > p.max_cycles;
+        // an inc_qclk in a present ALU slot (W3: present and inc_qclk bits of the three packed fields)
+        constexpr uint32_t PRES3 = (1u << W3_PRES) | (1u << (10 + W3_PRES)) | (1u << (20 + W3_PRES));
+        const bool inc = W3 ? ((a.y & (a.y << (W3_PRES - W3_INC)) & PRES3) != 0u)
+                            : (((int32_t)a.y < 0 && (a.y & 0x40000000u)) || ((int32_t)a.w < 0 && (a.w & 0x40000000u)));
+        const bool bad = inc || ((int32_t)u.w >= 0 && (u.y >> 28) != 0x9u) || t < qa_t || t + SPAN > p.max_cycles;
         return !tr_on && !__ballot(st == 0u && bad);
     }
     __device__ __forceinline__ void alu_simple(uint32_t imm, uint32_t ctl)
@@ -571,13 +587,13 @@ struct MacroLane {
     // ---- the lean path (NR == 2, registers r0 / r1 in VGPRs): the macro
     // carries MACRO_SIMPLE (capi.cpp: not a program's first, so past the
     // reset hold; reg_alu ALU slots; a PULSE_WRITE_TRIG or no pulse slot) and
-    // every running lane is 8 cycles or more inside max_cycles, no trace.  The
+    // every running lane is SPAN (12) cycles or more inside max_cycles, no trace.  The
     // remapped register fields are one bit each (slot 0 / 1), so operand
     // selection and the register write are v_bfe_i32 masks and v_bitop3
     // selects, and the counters advance by masks (k - pm: +1 where present)
     __device__ __forceinline__ bool lean_ok(const uint4 u) const
     {
-        return !tr_on && !__ballot(st == 0u && (!(u.w & MACRO_SIMPLE) || t + 8u > p.max_cycles));
+        return !tr_on && !__ballot(st == 0u && (!(u.w & MACRO_SIMPLE) || t + SPAN > p.max_cycles));
     }
     // ---- the lean CHUNK (NR == 2): one wave-uniform test for MACRO_CHUNK
     // macros.  `info` is the lane's chunk marker (capi.cpp mark_lean_chunks):
@@ -586,7 +602,8 @@ struct MacroLane {
     // that does not stop the lane ends at Tc + 3 with Tc = its cmd_time +
     // qa_t - qa_q >= its decode, so by induction macro m starts at or before
     // B + 11 m, B = max(t, Tmax + qa_t - qa_q): B + 11 (CH - 1) + 8 <=
-    // max_cycles keeps every macro's decodes inside max_cycles -- lean_ok at
+    // max_cycles keeps every macro's decodes inside max_cycles (W3: 15 m and
+    // B + 15 (CH - 1) + 12; 16 CH + 8 bounds both) -- lean_ok at
     // every macro, without testing it.  (A late pulse stops its lane, which
     // the lean pulse slot handles.)  The argument holds while qclk cannot
     // wrap before max_cycles (qa_q + max_cycles - qa_t < 2^32): then a
@@ -598,25 +615,39 @@ struct MacroLane {
         const uint64_t tc = (uint64_t)info + qa_t;                       // Tmax's cycle + qa_q
         const uint64_t b = max((uint64_t)t, tc > qa_q ? tc - qa_q + 3u : 0ull);
         const bool no_wrap = (uint64_t)qa_q + p.max_cycles < (1ull << 32) + qa_t;
-        const bool ok = info != MACRO_CHUNK_MIXED && no_wrap && b + 12ull * MACRO_CHUNK + 8u <= p.max_cycles;
+        const bool ok = info != MACRO_CHUNK_MIXED && no_wrap && b + (W3 ? 16ull : 12ull) * MACRO_CHUNK + 8u <= p.max_cycles;
         return !tr_on && !__ballot(st == 0u && !ok);
     }
     static __device__ __forceinline__ uint32_t bmask(uint32_t v, int b)     // bit b of v as 0 / ~0
     {
         return (uint32_t)(((int32_t)(v << (31 - b))) >> 31);
     }
-    __device__ __forceinline__ void alu_lean(uint32_t run, uint32_t imm, uint32_t ctl)
+    // ALU slot K of a MACRO_W3 macro (its packed ctl field at bit 10 K)
+    template <int K>
+    __device__ __forceinline__ void alu_lean_w3(uint32_t run, uint32_t imm, uint32_t pk)
     {
-        const uint32_t pm = run & (uint32_t)((int32_t)ctl >> 31);             // present (bit 31) and running
-        const uint32_t in0 = bit_select(bmask(ctl, 3), bit_select(bmask(ctl, 12), rg[1], rg[0]), imm);
-        const uint32_t b = bit_select(bmask(ctl, 4), rg[1], rg[0]);
-        const uint32_t out = ADDID ? in0 + (b & bmask(ctl, 0)) : alu_eval(ctl & 7u, in0, b);
-        const uint32_t wm = bmask(ctl, 8);                                    // rd: slot 1
+        constexpr int B = 10 * K;
+        const uint32_t pm = run & bmask(pk, B + W3_PRES);
+        const uint32_t in0 = bit_select(bmask(pk, B + W3_IN0), bit_select(bmask(pk, B + W3_RS0), rg[1], rg[0]), imm);
+        const uint32_t b = bit_select(bmask(pk, B + W3_RS1), rg[1], rg[0]);
+        const uint32_t out = ADDID ? in0 + (b & bmask(pk, B + W3_OP)) : alu_eval((pk >> B) & 7u, in0, b);
+        const uint32_t wm = bmask(pk, B + W3_RD);
         rg[1] = bit_select(pm & wm, out, rg[1]);
         rg[0] = bit_select(pm & ~wm, out, rg[0]);
         t += pm & 4u;
         k -= pm;
         n_tr -= pm;
+    }
+    // one lean macro: its ALU slots (the third only when some running lane
+    // has one: ~3 % of an RB image's macros), then the pulse slot
+    __device__ __forceinline__ void macro_lean(const uint4 a, const uint4 u)
+    {
+        static_assert(W3, "the lean path is NR == 2 = MACRO_W3 only");
+        const uint32_t run = st == 0u ? ~0u : 0u;
+        alu_lean_w3<0>(run, a.x, a.y);
+        alu_lean_w3<1>(run, a.z, a.y);
+        if (__ballot(run != 0u && ((a.y >> (20 + W3_PRES)) & 1u))) alu_lean_w3<2>(run, a.w, a.y);
+        pulse_lean(run, u);
     }
     __device__ __forceinline__ void pulse_lean(uint32_t run, const uint4 u)
     {
@@ -776,13 +807,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
             // and no branch between them but the stores' own
             if (L.lean_chunk_ok(info[slot])) {
 #pragma unroll 2
-                for (uint32_t i = 0; i < CH; i++) {
-                    const uint4 a = cur[2 * i], u = cur[2 * i + 1];
-                    const uint32_t run = L.st == 0u ? ~0u : 0u;
-                    L.alu_lean(run, a.x, a.y);
-                    L.alu_lean(run, a.z, a.w);
-                    L.pulse_lean(run, u);
-                }
+                for (uint32_t i = 0; i < CH; i++) L.macro_lean(cur[2 * i], cur[2 * i + 1]);
                 return;
             }
         }
@@ -791,20 +816,22 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
             const uint4 a = cur[2 * i], u = cur[2 * i + 1];
             if constexpr (NR == 2) {
                 if (L.lean_ok(u)) {
-                    const uint32_t run = L.st == 0u ? ~0u : 0u;
-                    L.alu_lean(run, a.x, a.y);
-                    L.alu_lean(run, a.z, a.w);
-                    L.pulse_lean(run, u);
+                    L.macro_lean(a, u);
                     continue;
                 }
             }
+            constexpr bool W3 = MacroLane<NR, ADDID>::W3;
+            const uint32_t c0 = W3 ? w3_ctl(a.y, 0) : a.y, c1 = W3 ? w3_ctl(a.y, 1) : a.w;
+            const uint32_t i1 = a.z;
             if (L.simple_ok(a, u)) {
-                L.alu_simple(a.x, a.y);
-                L.alu_simple(a.z, a.w);
+                L.alu_simple(a.x, c0);
+                L.alu_simple(i1, c1);
+                if (W3) L.alu_simple(a.w, w3_ctl(a.y, 2));
                 L.pulse_simple(u);
             } else {
-                L.alu_step(a.x, a.y);
-                L.alu_step(a.z, a.w);
+                L.alu_step(a.x, c0);
+                L.alu_step(i1, c1);
+                if (W3) L.alu_step(a.w, w3_ctl(a.y, 2));
                 L.pulse_step(u);
             }
         }
