@@ -20,6 +20,7 @@
 //              runs of the residue list instead of interleaving
 // The channel-boundary blocks are written partly by each channel's WG
 // (16-B granular masks), as a channel-bound kernel would.
+// Set "w" (round 5): one tile per wave in address order (wave_tile_k).
 // Also records s_getreg(XCC_ID) per WG of one launch to check that WG g and
 // g + 8 share an XCD (MI355X_MICROARCH.md, workgroup dispatch).
 #include <hip/hip_runtime.h>
@@ -197,6 +198,33 @@ __global__ void __launch_bounds__(BLOCK) cx_k(uint32_t *iq, uint32_t K, uint32_t
     }
 }
 
+// (set "w") one channel-local 1024-sample tile per wave: WG (ch, g) of W
+// waves takes tiles g W .. g W + W - 1 of channel ch, channel-major (so the
+// grid writes the buffer in address order, like the fill); each wave sleeps
+// SLEEP x 64 clocks before its 4 x 1-KiB stores (a stand-in for its compute)
+template <int W, int SLEEP>
+__global__ void __launch_bounds__(64 * W) wave_tile_k(uint32_t *iq, uint32_t per_ch)
+{
+    const uint32_t tiles = (NS + 1023) / 1024;
+    const uint32_t ch = blockIdx.x / per_ch, g = blockIdx.x % per_ch;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    const uint32_t t = g * W + wv;
+    if (t >= tiles) return;
+    for (int k = 0; k < SLEEP; k++) __builtin_amdgcn_s_sleep(1);
+    uint32_t *out = iq + (uint64_t)ch * NS;
+    for (int q = 0; q < 4; q++) {
+        const uint32_t j = t * 1024 + 4 * (64 * q + ln);
+        if (j + 3 < NS) st16(out + j, j);
+    }
+}
+
+// the fill with 64-thread workgroups (one 16-B store per thread)
+__global__ void __launch_bounds__(64) fill64_k(uint32_t *iq, uint64_t total)
+{
+    const uint64_t j = ((uint64_t)blockIdx.x * 64 + threadIdx.x) * 4;
+    if (j + 3 < total) st16(iq + j, (uint32_t)j);
+}
+
 static uint32_t *g_iq;
 static uint32_t g_K, g_scr;
 
@@ -243,6 +271,22 @@ int main(int argc, char **argv)
 {
     const uint64_t total = (uint64_t)NCH * NS, bytes = total * 4;
     if (hipMalloc(&g_iq, bytes) != hipSuccess) { printf("alloc failed\n"); return 1; }
+    if (argc > 1 && argv[1][0] == 'w') {                 // round-5 set: one tile per wave, address order
+        const uint32_t tiles = (NS + 1023) / 1024;
+        for (int rep = 0; rep < 2; rep++) {
+            bench("fill", [&] { fill_k<<<(uint32_t)(total / 4 / BLOCK), BLOCK>>>(g_iq, total); });
+            bench("fill64", [&] { fill64_k<<<(uint32_t)(total / 4 / 64), 64>>>(g_iq, total); });
+            bench("cur", [&] { cur_k<<<NCH * 13, BLOCK>>>(g_iq, 13, nullptr); });
+            bench("wave1", [&] { wave_tile_k<1, 0><<<NCH * tiles, 64>>>(g_iq, tiles); });
+            bench("wave4", [&] { wave_tile_k<4, 0><<<NCH * ((tiles + 3) / 4), 256>>>(g_iq, (tiles + 3) / 4); });
+            bench("wave1_s16", [&] { wave_tile_k<1, 16><<<NCH * tiles, 64>>>(g_iq, tiles); });
+            bench("wave1_s48", [&] { wave_tile_k<1, 48><<<NCH * tiles, 64>>>(g_iq, tiles); });
+            bench("wave4_s16", [&] { wave_tile_k<4, 16><<<NCH * ((tiles + 3) / 4), 256>>>(g_iq, (tiles + 3) / 4); });
+            bench("wave4_s48", [&] { wave_tile_k<4, 48><<<NCH * ((tiles + 3) / 4), 256>>>(g_iq, (tiles + 3) / 4); });
+        }
+        hipFree(g_iq);
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'b') {                 // round-4 set: per-tile granularity, WG lifetime
         const uint32_t nblk = (uint32_t)((total + 1023) / 1024);
         for (int rep = 0; rep < 2; rep++) {
