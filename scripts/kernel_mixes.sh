@@ -30,5 +30,6 @@ python3 scripts/kernel_valu_peak.py $peak "${args[@]}" \
     --pmc "branch_kernelILi11=$pmc/${tag}_active_reset_pmc.json" \
     --pmc "branch_kernelILi14=$pmc/${tag}_lut_pmc.json" \
     --pmc "macro_staged_kernel=$pmc/${tag}_rb_pmc.json" \
-    --pmc "dds_tile_kernel=$pmc/${tag}_dds_pmc.json" --out $out
+    --pmc "dds_tile_kernel=$pmc/${tag}_dds_pmc.json" \
+    --validation profiles/r05_valu_model_check.json --out $out
 rm -rf $tmp

@@ -85,6 +85,8 @@ def main():
     ap.add_argument('peak')
     ap.add_argument('mix', nargs='+')
     ap.add_argument('--pmc', action='append', default=[], help='kernel substring=pmc json (its clock and rate)')
+    ap.add_argument('--validation', default=None,
+                    help='scripts/valu_model_check.py output: recorded with the peaks (does the table model issue?)')
     ap.add_argument('--out', required=True)
     a = ap.parse_args()
     with open(a.peak) as f:
@@ -99,6 +101,15 @@ def main():
             pmcs[k] = json.load(f)
     out = {'what': 'per-kernel VALU issue peak from its own opcode mix (scripts/kernel_valu_peak.py)',
            'peak_source': a.peak, 'kernels': []}
+    if a.validation and os.path.exists(a.validation):
+        with open(a.validation) as f:
+            v = json.load(f)
+        out['validation'] = {'source': a.validation, 'kernel': v['kernel'],
+                             'predicted_cycles_per_inst': v['predicted_cycles_per_inst'],
+                             'measured_cycles_per_inst': v['measured_cycles_per_inst'], 'miss': v['miss'],
+                             'issue_model': v['issue_model'], 'conclusion': v['conclusion']}
+        out['graded_on'] = ('these own-mix peaks' if v['issue_model'] else
+                            'the measured mixed-integer peak (bench.VALU_PEAK); frac_of_own_peak is shown, not graded')
     for m in a.mix:
         with open(m) as f:
             mix = json.load(f)

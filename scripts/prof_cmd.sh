@@ -23,4 +23,8 @@ run sq1 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VME
 run sq2 300 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE || exit $?
 # the VALU stream's 32- / 64-bit integer split (the kernels' own VALU peak, scripts/kernel_valu_peak.py)
 run sq3 300 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_MUL_F32 GRBM_GUI_ACTIVE || exit $?
+# the write path (TA -> TCP -> TCC -> EA): which unit holds a store-heavy
+# kernel's waves (block limits: 2 TA, 4 TCP, 4 TCC counters per pass)
+run wpath 300 --pmc TA_FLAT_WRITE_WAVEFRONTS_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TCP_TCC_WRITE_REQ_sum TCP_TCC_WRITE_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum GRBM_GUI_ACTIVE || exit $?
+run wtcc 300 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum GRBM_GUI_ACTIVE || exit $?
 find $out/trace -name "*kernel_stats.csv" -exec cat {} \;
