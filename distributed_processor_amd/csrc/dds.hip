@@ -176,17 +176,22 @@ __device__ __forceinline__ uint32_t mix_y(uint32_t e, uint32_t ep, uint32_t y)
 }
 
 // ===========================================================================
-// Event index: one workgroup per channel.  Wave w owns events
-// [256 w, 256 w + 256) (4 per lane, all loaded up front), the four waves'
-// strobe / reset counts are scanned in LDS, each wave writes its records at its
-// offset in event order, then the 256 threads find the tile windows, one tile
-// each per pass (binary searches over the channel's LDS time arrays).  (One
-// wave per channel with per-lane tile cursors measured 1 % slower per step.)
+// Event index: one workgroup per channel.  Event chunk q (64 events) goes to
+// wave q % 4 (chunks 4 k + w are wave w's k-th), so every wave loads from the
+// first chunk on and the loads of short lists spread over the waves; all
+// loaded up front.  The 16 chunks' strobe / reset counts are scanned in LDS,
+// each wave writes its records at their offsets in event order, then the 256
+// threads find the tile windows, one tile each per pass: a binary search for
+// the tile's first cycle over the channel's LDS time array, then a forward
+// scan to its last (a tile holds few records).  (One wave per channel with
+// per-lane tile cursors measured 1 % slower per step.)
 // ===========================================================================
 __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
 {
+    constexpr int W = BLOCK / 64;
+    constexpr int K = DDS_MAX_EVENTS / BLOCK;           // event chunks per wave
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    __shared__ uint32_t s_cnt[2][BLOCK / 64];
+    __shared__ uint32_t s_cnt[2][K * W + 1];
     uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn);
     uint32_t *s_rs_t = s_st_t + p.ev_lds;
     const uint32_t tid = threadIdx.x, wl = tid & 63u, wv = tid >> 6;
@@ -197,36 +202,33 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
     uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
     uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
     const uint64_t below = wl ? (~0ull >> (64 - wl)) : 0ull;
-    constexpr int K = DDS_MAX_EVENTS / BLOCK;           // events per lane
     uint4 ev[K];
     bool is_st[K], is_rs[K];
-    uint32_t ns = 0, nr = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-        const uint32_t e = (wv * K + k) * 64u + wl;
+        const uint32_t e = (k * W + wv) * 64u + wl;
         ev[k] = e < n_ev ? p.events[(uint64_t)e * p.n_lanes + lane] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int k = 0; k < K; k++) {
-        const uint32_t e = (wv * K + k) * 64u + wl;
+        const uint32_t e = (k * W + wv) * 64u + wl;
         const uint32_t kind = ev[k].y >> 28;
         is_st[k] = e < n_ev && kind == 0u && ((ev[k].y >> 24) & 3u) == elem;
         is_rs[k] = e < n_ev && kind == 1u;
-        ns += (uint32_t)__popcll(__ballot(is_st[k]));
-        nr += (uint32_t)__popcll(__ballot(is_rs[k]));
+        const uint32_t ns = (uint32_t)__popcll(__ballot(is_st[k])), nr = (uint32_t)__popcll(__ballot(is_rs[k]));
+        if (wl == 0) { s_cnt[0][k * W + wv] = ns; s_cnt[1][k * W + wv] = nr; }
     }
-    if (wl == 0) { s_cnt[0][wv] = ns; s_cnt[1][wv] = nr; }
     __syncthreads();
-    uint32_t os = 0, orr = 0, n_st = 0, n_rs = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < BLOCK / 64; w++) {
-        os += w < wv ? s_cnt[0][w] : 0u;
-        orr += w < wv ? s_cnt[1][w] : 0u;
-        n_st += s_cnt[0][w];
-        n_rs += s_cnt[1][w];
+    if (tid < 2) {                                      // exclusive scans of the chunk counts (+ totals)
+        uint32_t acc = 0;
+        for (int q = 0; q < K * W; q++) { const uint32_t c = s_cnt[tid][q]; s_cnt[tid][q] = acc; acc += c; }
+        s_cnt[tid][K * W] = acc;
     }
+    __syncthreads();
+    const uint32_t n_st = s_cnt[0][K * W], n_rs = s_cnt[1][K * W];
 #pragma unroll
     for (int k = 0; k < K; k++) {
+        const uint32_t os = s_cnt[0][k * W + wv], orr = s_cnt[1][k * W + wv];   // records in the chunks before
         const uint64_t bs = __ballot(is_st[k]), br = __ballot(is_rs[k]);
         if (is_st[k]) {
             const uint32_t i = os + (uint32_t)__popcll(bs & below);
@@ -238,8 +240,6 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
             xr[i] = ev[k].x;
             s_rs_t[i] = ev[k].x;
         }
-        os += (uint32_t)__popcll(bs);
-        orr += (uint32_t)__popcll(br);
     }
     __syncthreads();
     // window of tile c (samples [c DDS_TILE, + DDS_TILE) of the channel): from
@@ -249,8 +249,10 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
         const uint64_t j0 = (uint64_t)c * DDS_TILE;
         const uint64_t j1 = min(j0 + DDS_TILE, (uint64_t)p.n_samples) - 1;
         const uint32_t n0 = (uint32_t)(j0 / spc), n1 = (uint32_t)(j1 / spc);
-        const int a0 = last_le(s_st_t, (int)n_st, n0) + 1, a1 = last_le(s_st_t, (int)n_st, n1) + 1;
-        const int b0 = last_le(s_rs_t, (int)n_rs, n0) + 1, b1 = last_le(s_rs_t, (int)n_rs, n1) + 1;
+        const int a0 = last_le(s_st_t, (int)n_st, n0) + 1, b0 = last_le(s_rs_t, (int)n_rs, n0) + 1;
+        int a1 = a0, b1 = b0;
+        while (a1 < (int)n_st && s_st_t[a1] <= n1) a1++;
+        while (b1 < (int)n_rs && s_rs_t[b1] <= n1) b1++;
         const int sl = max(a0 - 1, 0), rl = max(b0 - 1, 0);
         p.win[(uint64_t)ch * p.tiles + c] = make_uint4((uint32_t)sl, (uint32_t)(a1 - sl), (uint32_t)rl, (uint32_t)(b1 - rl));
     }
