@@ -25,7 +25,7 @@
 //   * the reset hold (qclk(0) = qclk(1) = 0, proc.sv:125-136) can only be
 //     seen by a lane's first decode: a peeled first iteration;
 //   * event records are held per lane and stored a whole wave row at a
-//     time (below, pev0 / pev1);
+//     time (below, pend0 / pend1);
 //   * no register file when no command writes one (FEAT_REGS), and the
 //     workgroup's programs staged in LDS when they are short
 //     (FEAT_PROG_LDS: an LDS fetch does not wait behind the lane's event
@@ -86,20 +86,22 @@ __device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t C)
     return v;
 }
 
-// any lane of the wave
-__device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0ull; }
+// minimum over the whole wave (all lanes converged): DPP within each row of
+// 16, then the four rows' minima by readlane
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+    v = group_reduce<0>(v, 16u);
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return min(min(a, b), min(c, d));
+}
 
 }  // namespace
 
 // CT: the cores per shot when fixed at compile time (8: the BASELINE
 // configs), so group reductions and lane arithmetic are straight-line; 0 = p.C
-// waves per SIMD the register allocation targets: 7 (2 VGPRs spilled; 6 at
-// the default's 75 VGPRs) measured 1.5 % faster on config 3
-// (profiles/r05_branch_rows_ab.json); kernels with a register file or the
-// LUT back end hold fewer by their LDS (16 KiB more each) and keep the default
 template <int FEAT, int CT>
-__global__ void __launch_bounds__(BLOCK)
-__attribute__((amdgpu_waves_per_eu((FEAT & (FEAT_LUT | FEAT_REGS)) ? 1 : 7))) branch_kernel(const KParams p)
+__global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
 {
     constexpr bool FPROC = (FEAT & FEAT_FPROC) != 0;
     constexpr bool LUT = (FEAT & FEAT_LUT) != 0;     // fproc_lut back end (exclusive with FPROC)
@@ -198,13 +200,9 @@ __attribute__((amdgpu_waves_per_eu((FEAT & (FEAT_LUT | FEAT_REGS)) ? 1 : 7))) br
     // storing each part as it comes was slower although it issued fewer
     // stores and the same bytes (config 3: 0.480 -> 0.447 ms median,
     // profiles/r02_ar_rows_ab.json).  Slots [n_st, min(n_ev, cap)) are
-    // pending, slot k in pev0 (k even) or pev1 (k odd); a third record pushes
-    // the oldest out.  Rows below the wave-uniform row_done are stored; row
-    // row_done is stored once no unfinished lane still lacks it (one ballot a
-    // iteration), by the lanes that hold it -- the row's parity is uniform,
-    // so the slot is picked without a per-lane select.
-    uint4 pev0 = make_uint4(0u, 0u, 0u, 0u), pev1 = pev0;
-    uint32_t n_st = 0, row_done = 0;
+    // pending in pend0, pend1; a third record pushes the oldest out.
+    uint4 pend0 = make_uint4(0u, 0u, 0u, 0u), pend1 = pend0;
+    uint32_t n_st = 0;
 
     // pulse_iface strobe at cycle te (kind 0: trigger, 1: phase reset) with the
     // current pulse registers for lanes with `ok`; readout-element triggers
@@ -215,12 +213,13 @@ __attribute__((amdgpu_waves_per_eu((FEAT & (FEAT_LUT | FEAT_REGS)) ? 1 : 7))) br
                 ev_lane[(uint64_t)n_ev * n_lanes] = event_record(te, pe, pp, pa, kind);
             if (!DIRECT && n_ev < p.event_cap && p.events) {
                 const uint4 rec = event_record(te, pe, pp, pa, kind);
-                if (n_ev - n_st == 2u) {                // the oldest (same slot) goes out now
-                    ev_lane[(uint64_t)n_st * n_lanes] = sel4(n_st & 1u, pev1, pev0);
-                    n_st++;
-                }
-                if (n_ev & 1u) pev1 = rec;
-                else pev0 = rec;
+                const bool full = n_ev - n_st == 2u;    // the oldest goes out now
+                if (full) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
+                pend0 = sel4(full, pend1, pend0);
+                n_st += full ? 1u : 0u;
+                const bool first = n_ev == n_st;
+                pend0 = sel4(first, rec, pend0);
+                pend1 = sel4(first, pend1, rec);
             }
             n_ev++;
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {   // meas_elem 0xFF: none
@@ -286,25 +285,23 @@ __attribute__((amdgpu_waves_per_eu((FEAT & (FEAT_LUT | FEAT_REGS)) ? 1 : 7))) br
         mode = stop ? B_FIN : mode;
     };
 
-    // store the rows every unfinished lane has passed; at the end (all) every
-    // lane stores what it still holds
+    // store the pending rows every unfinished lane has passed (all: at the end)
     auto flush_rows = [&](bool all) __attribute__((always_inline)) {
         if (DIRECT || !p.events) return;
         const uint32_t ne = min(n_ev, p.event_cap);
-        if (all) {
-            if (n_st < ne) ev_lane[(uint64_t)n_st * n_lanes] = sel4(n_st & 1u, pev1, pev0);
-            if (n_st + 1u < ne) ev_lane[(uint64_t)(n_st + 1u) * n_lanes] = sel4(n_st & 1u, pev0, pev1);
-            return;
+        if (!__any(ne > n_st)) return;
+        const uint32_t done = all ? INF32 : wave_min(mode == B_FIN ? INF32 : ne);
+        // the held records [n_st, ne) are pend0, pend1: store the rows every
+        // unfinished lane has passed, then shift once (not once per row)
+        const bool f1 = n_st < ne && n_st < done;
+        if (!__any(f1)) return;                      // most iterations complete no row
+        const bool f2 = f1 && n_st + 1u < ne && n_st + 1u < done;
+        if (f1) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
+        if (__any(f2)) {
+            if (f2) ev_lane[(uint64_t)(n_st + 1u) * n_lanes] = pend1;
         }
-#pragma unroll
-        for (int k = 0; k < 2; k++) {                // at most two rows complete in one iteration
-            if (wave_any(mode != B_FIN && ne <= row_done) || !wave_any(ne > row_done)) return;
-            const bool st = ne > row_done && n_st <= row_done;   // (a pushed-out slot went already)
-            const bool odd = row_done & 1u;          // (uniform)
-            if (st) ev_lane[(uint64_t)row_done * n_lanes] = sel4(odd, pev1, pev0);
-            n_st = st ? row_done + 1u : n_st;
-            row_done = __builtin_amdgcn_readfirstlane(row_done + 1u);
-        }
+        pend0 = sel4(f1 && !f2, pend1, pend0);
+        n_st += (f1 ? 1u : 0u) + (f2 ? 1u : 0u);
     };
 
     // One lockstep iteration: every running lane retires at most one command.
