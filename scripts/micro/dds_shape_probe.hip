@@ -68,6 +68,24 @@ __global__ void __launch_bounds__(BLOCK) cur_k(uint32_t *iq, uint32_t stripes, u
     }
 }
 
+// (set "w") the stripes shape with channel rows PITCH samples apart (NS
+// written per row): pitch 216 Ki samples puts every row on a 4-KiB boundary
+__global__ void __launch_bounds__(BLOCK) curP_k(uint32_t *iq, uint32_t stripes, uint32_t pitch)
+{
+    const uint32_t ch = blockIdx.x / stripes, s = blockIdx.x % stripes;
+    const uint32_t tiles = (NS + 1023) / 1024;
+    uint32_t *out = iq + (uint64_t)ch * pitch;
+    const uint32_t n_t = (tiles - s + stripes - 1) / stripes;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    for (uint32_t i = wv; i < n_t; i += 4) {
+        const uint32_t t = s + i * stripes;
+        for (int r = 0; r < 4; r++) {
+            const uint32_t j = t * 1024 + 4 * (64 * r + ln);
+            if (j + 3 < NS) st16(out + j, j);
+        }
+    }
+}
+
 // (round 4, set "b") the stripes shape with the whole workgroup on each tile
 // (thread t writes 16 B at 4 t of the tile) instead of a wave per tile
 __global__ void __launch_bounds__(BLOCK) curG_k(uint32_t *iq, uint32_t stripes)
@@ -218,6 +236,67 @@ __global__ void __launch_bounds__(64 * W) wave_tile_k(uint32_t *iq, uint32_t per
     }
 }
 
+// (set "w") channel-contiguous stripes: stripe s of a channel takes the
+// channel's tiles [s T, s T + T) (T = ceil(tiles / S)), wave w of the
+// workgroup its tiles w, w + 4, ... (4 x 1-KiB stores each)
+__global__ void __launch_bounds__(BLOCK) contig_k(uint32_t *iq, uint32_t S)
+{
+    const uint32_t tiles = (NS + 1023) / 1024, T = (tiles + S - 1) / S;
+    const uint32_t ch = blockIdx.x / S, st = blockIdx.x % S;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    uint32_t *out = iq + (uint64_t)ch * NS;
+    for (uint32_t i = wv; i < T; i += 4) {
+        const uint32_t t = st * T + i;
+        if (t >= tiles) break;
+        for (int q = 0; q < 4; q++) {
+            const uint32_t j = t * 1024 + 4 * (64 * q + ln);
+            if (j + 3 < NS) st16(out + j, j);
+        }
+    }
+}
+
+// (set "w") channel-local tiles in global (channel-major) order, written by
+// whole workgroups (thread t: 16 B at 4 t of the tile):
+//   gtile   : workgroup b writes tile b and exits (the fill, channel-local)
+//   gstride : G persistent workgroups, workgroup g takes tiles g, g + G, ...
+//             (at any time the grid writes a window of ~G tiles)
+//   gstrideW: the same with each WAVE on its own tile (window ~4 G tiles)
+__global__ void __launch_bounds__(BLOCK) gtile_k(uint32_t *iq, uint32_t n_tiles, uint32_t G, uint32_t wave_mode,
+                                                uint32_t pitch = NS)
+{
+    const uint32_t tiles = (NS + 1023) / 1024;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    if (!wave_mode) {
+        for (uint32_t t = blockIdx.x; t < n_tiles; t += G) {
+            const uint32_t ch = t / tiles, c = t - ch * tiles;
+            const uint32_t j = c * 1024 + 4 * threadIdx.x;
+            if (j + 3 < NS) st16(iq + (uint64_t)ch * pitch + j, j);
+        }
+    } else {
+        for (uint32_t t = 4 * blockIdx.x + wv; t < n_tiles; t += 4 * G) {
+            const uint32_t ch = t / tiles, c = t - ch * tiles;
+            for (int q = 0; q < 4; q++) {
+                const uint32_t j = c * 1024 + 4 * (64 * q + ln);
+                if (j + 3 < NS) st16(iq + (uint64_t)ch * pitch + j, j);
+            }
+        }
+    }
+}
+
+// (set "w") persistent fill: G workgroups, workgroup g writes global 4-KiB
+// blocks g, g + G, ... one 16-B store per thread per block (the fill's
+// address stream from long-lived workgroups); SLEEP x 64 clocks per block
+template <int SLEEP>
+__global__ void __launch_bounds__(BLOCK) gblk_k(uint32_t *iq, uint64_t total, uint32_t G)
+{
+    const uint64_t nblk = total / 1024;
+    for (uint64_t b = blockIdx.x; b < nblk; b += G) {
+        for (int k = 0; k < SLEEP; k++) __builtin_amdgcn_s_sleep(1);
+        const uint64_t j = b * 1024 + 4 * threadIdx.x;
+        st16(iq + j, (uint32_t)j);
+    }
+}
+
 // the fill with 64-thread workgroups (one 16-B store per thread)
 __global__ void __launch_bounds__(64) fill64_k(uint32_t *iq, uint64_t total)
 {
@@ -270,7 +349,7 @@ static void check_xcc(uint32_t n_wg, void (*launch)(uint32_t *), const char *nam
 int main(int argc, char **argv)
 {
     const uint64_t total = (uint64_t)NCH * NS, bytes = total * 4;
-    if (hipMalloc(&g_iq, bytes) != hipSuccess) { printf("alloc failed\n"); return 1; }
+    if (hipMalloc(&g_iq, (uint64_t)NCH * 210944u * 4) != hipSuccess) { printf("alloc failed\n"); return 1; }
     if (argc > 1 && argv[1][0] == 'w') {                 // round-5 set: one tile per wave, address order
         const uint32_t tiles = (NS + 1023) / 1024;
         for (int rep = 0; rep < 2; rep++) {
@@ -283,6 +362,46 @@ int main(int argc, char **argv)
             bench("wave1_s48", [&] { wave_tile_k<1, 48><<<NCH * tiles, 64>>>(g_iq, tiles); });
             bench("wave4_s16", [&] { wave_tile_k<4, 16><<<NCH * ((tiles + 3) / 4), 256>>>(g_iq, (tiles + 3) / 4); });
             bench("wave4_s48", [&] { wave_tile_k<4, 48><<<NCH * ((tiles + 3) / 4), 256>>>(g_iq, (tiles + 3) / 4); });
+            for (uint32_t G : {1024u, 1792u, 2048u, 4096u, 8192u}) {
+                g_K = G;
+                char nm[32];
+                snprintf(nm, sizeof nm, "gblk%u", G);
+                bench(nm, [&] { gblk_k<0><<<g_K, BLOCK>>>(g_iq, total, g_K); });
+                snprintf(nm, sizeof nm, "gblk%u_s8", G);
+                bench(nm, [&] { gblk_k<8><<<g_K, BLOCK>>>(g_iq, total, g_K); });
+            }
+            {
+                const uint32_t nt = NCH * tiles;
+                bench("gtile", [&] { gtile_k<<<nt, BLOCK>>>(g_iq, nt, nt, 0); });
+                for (uint32_t P : {210176u, 210944u, 210048u}) {   // 1-KiB, 4-KiB, 512-B aligned rows
+                    g_K = P;
+                    char nm[40];
+                    snprintf(nm, sizeof nm, "gtile_p%u", P);
+                    bench(nm, [&] { gtile_k<<<nt, BLOCK>>>(g_iq, nt, nt, 0, g_K); });
+                    snprintf(nm, sizeof nm, "gstrideW2048_p%u", P);
+                    bench(nm, [&] { gtile_k<<<2048, BLOCK>>>(g_iq, nt, 2048, 1, g_K); });
+                    snprintf(nm, sizeof nm, "curP_p%u", P);
+                    bench(nm, [&] { curP_k<<<NCH * 13, BLOCK>>>(g_iq, 13, g_K); });
+                }
+                for (uint32_t G : {1024u, 1792u, 2048u, 4096u}) {
+                    g_K = G;
+                    char nm[32];
+                    snprintf(nm, sizeof nm, "gstride%u", G);
+                    bench(nm, [&] { gtile_k<<<g_K, BLOCK>>>(g_iq, nt, g_K, 0); });
+                    snprintf(nm, sizeof nm, "gstrideW%u", G);
+                    bench(nm, [&] { gtile_k<<<g_K, BLOCK>>>(g_iq, nt, g_K, 1); });
+                }
+            }
+            bench("curP_ns", [&] { curP_k<<<NCH * 13, BLOCK>>>(g_iq, 13, NS); });
+            bench("curP_210944", [&] { curP_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 210944u); });
+            bench("curP_209984", [&] { curP_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 209984u); });
+            bench("curP_210048", [&] { curP_k<<<NCH * 13, BLOCK>>>(g_iq, 13, 210048u); });
+            for (uint32_t S : {1u, 2u, 4u, 7u, 13u, 26u}) {
+                g_K = S;
+                char nm[32];
+                snprintf(nm, sizeof nm, "contig%u", S);
+                bench(nm, [&] { contig_k<<<NCH * g_K, BLOCK>>>(g_iq, g_K); });
+            }
         }
         hipFree(g_iq);
         return 0;
