@@ -297,6 +297,29 @@ __global__ void __launch_bounds__(BLOCK) gblk_k(uint32_t *iq, uint64_t total, ui
     }
 }
 
+// (set "c") config 2's store shape (0.96 GB: per lane 32-B summary, 5
+// event records of 16 B in slot-major rows, one 8-B measurement row), 8M
+// lanes, one workgroup per 256 lanes; residency capped by dynamic LDS
+__global__ void __launch_bounds__(BLOCK) cfg2_k(uint32_t *base, uint32_t order)
+{
+    extern __shared__ uint32_t s_pad[];
+    const uint64_t n = 8000000ull, lane = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (lane >= n) return;
+    if (threadIdx.x == 1023) s_pad[0] = 0;              // (never: keeps the LDS allocation)
+    uint32_t *summ = base, *ev = base + n * 8, *meas = ev + n * 4 * 5;
+    const uint32_t v = (uint32_t)lane;
+    if (order == 0) {
+        for (int k = 0; k < 5; k++) st16(ev + ((uint64_t)k * n + lane) * 4, v + k);
+        *reinterpret_cast<uint2 *>(meas + lane * 2) = make_uint2(v, 1);
+        st16(summ + lane * 8, v); st16(summ + lane * 8 + 4, v);
+    } else {                                            // one stream at a time per workgroup: rows in turn
+        st16(summ + lane * 8, v); st16(summ + lane * 8 + 4, v);
+        __syncthreads();
+        for (int k = 0; k < 5; k++) { st16(ev + ((uint64_t)k * n + lane) * 4, v + k); __syncthreads(); }
+        *reinterpret_cast<uint2 *>(meas + lane * 2) = make_uint2(v, 1);
+    }
+}
+
 // the fill with 64-thread workgroups (one 16-B store per thread)
 __global__ void __launch_bounds__(64) fill64_k(uint32_t *iq, uint64_t total)
 {
@@ -350,6 +373,22 @@ int main(int argc, char **argv)
 {
     const uint64_t total = (uint64_t)NCH * NS, bytes = total * 4;
     if (hipMalloc(&g_iq, (uint64_t)NCH * 210944u * 4) != hipSuccess) { printf("alloc failed\n"); return 1; }
+    if (argc > 1 && argv[1][0] == 'c') {                 // round-5 set: config 2's store shape
+        const uint64_t bytes2 = 8000000ull * 120;
+        for (int rep = 0; rep < 2; rep++) {
+            bench("fill_0.96GB", [&] { fill_k<<<(uint32_t)(bytes2 / 16 / BLOCK), BLOCK>>>(g_iq, bytes2 / 4); });
+            for (uint32_t lds : {0u, 20u * 1024, 40u * 1024, 60u * 1024}) {
+                for (uint32_t order : {0u, 1u}) {
+                    g_K = lds; g_scr = order;
+                    char nm[48];
+                    snprintf(nm, sizeof nm, "cfg2_lds%uK_o%u", lds / 1024, order);
+                    bench(nm, [&] { cfg2_k<<<8000000 / BLOCK, BLOCK, g_K>>>(g_iq, g_scr); });
+                }
+            }
+        }
+        hipFree(g_iq);
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'w') {                 // round-5 set: one tile per wave, address order
         const uint32_t tiles = (NS + 1023) / 1024;
         for (int rep = 0; rep < 2; rep++) {
