@@ -778,9 +778,11 @@ def main():
     ap.add_argument('--shots', type=int, default=10 ** 6, help='config-2 shots per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
-    ap.add_argument('--dds-depth', type=int, default=1,
-                    help='DDS batches in flight (opt-in, > 1: dds.SynthesisPipeline, measured beside the serial '
-                         'step and reported only when faster; streams beyond the 4 hardware queues share them)')
+    ap.add_argument('--dds-depth', type=int, default=2,
+                    help='DDS batches in flight (> 1: dds.SynthesisPipeline, measured beside the serial step and '
+                         'reported only when faster, both on the line; 1: serial only).  Default 2: the next '
+                         'batch\'s index kernel runs beside this batch\'s tiles (profiles/r05_dds_depth.json: '
+                         '0.312 vs 0.327 ms); the round-4 default of 8 was slower than serial on the driver\'s box')
     ap.add_argument('--rb-depth', type=int, default=1,
                     help='config-4 batches in flight (opt-in, > 1: emulator.RunPipeline, measured beside the '
                          'serial step and reported only when faster)')

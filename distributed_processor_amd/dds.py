@@ -112,9 +112,9 @@ class SynthesisPipeline:
     k % depth: batch k + 1's index kernel runs beside batch k's tile kernel.
     On the builder's box that measured 0.329 -> 0.317 ms per config-5 step
     (``profiles/r03_dds_pipe.json``), but the driver's round-4 record has the
-    8-deep pipeline SLOWER than one context (0.3377 vs 0.3283 ms), so
-    ``bench.py`` runs one context by default (``--dds-depth 1``) and measures
-    a pipeline only when asked, reporting the faster of the two.
+    8-deep pipeline SLOWER than one context (0.3377 vs 0.3283 ms); ``bench.py``
+    measures one context and depth 2 on the same line (``--dds-depth 2``) and
+    reports the faster (round 5: 0.312 vs 0.327 ms, ``profiles/r05_dds_depth.json``).
 
     Streams beyond the process's hardware queues (``GPU_MAX_HW_QUEUES``, 4 by
     default) share them: at most 4 batches execute at once, the others wait
