@@ -946,7 +946,7 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
         const uint32_t fit = fixed < DDS_WG_LDS_BUDGET ? (DDS_WG_LDS_BUDGET - fixed) / 20 & ~7u : 0u;
         p.rec_lds = std::min(p.ev_lds, std::max(fit, DDS_REC_LDS_MIN));
     }
-    const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds, p.tiles);
+    const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds);
     if (need > ctx->dds_index_cap) {         // the event index (grown, never shrunk)
         HIPCHK(ctx, hipStreamSynchronize(s));   // an earlier launch may still use it
         (void)hipFree(ctx->d_dds_index);
@@ -956,8 +956,8 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     }
     uint8_t *b = static_cast<uint8_t *>(ctx->d_dds_index);
     p.xs = reinterpret_cast<uint4 *>(b);
-    p.win = reinterpret_cast<uint4 *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
-    p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16 + (uint64_t)p.n_channels * p.tiles * 16);
+    p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
+    p.cnt = reinterpret_cast<uint2 *>(b + (uint64_t)p.n_channels * p.ev_lds * 20);
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, launch_dds_index(p, s));   // outside the timed bracket: it holds the synthesis kernel alone
     HIPCHK(ctx, timing_start(ctx, s, &ev_stop));

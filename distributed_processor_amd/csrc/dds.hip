@@ -180,24 +180,21 @@ __device__ __forceinline__ uint32_t mix_y(uint32_t e, uint32_t ep, uint32_t y)
 // wave q % 4 (chunks 4 k + w are wave w's k-th), so every wave loads from the
 // first chunk on and the loads of short lists spread over the waves; all
 // loaded up front.  The 16 chunks' strobe / reset counts are scanned in LDS,
-// each wave writes its records at their offsets in event order, then the 256
-// threads find the tile windows, one tile each per pass: a binary search for
-// the tile's first cycle over the channel's LDS time array, then a forward
-// scan to its last (a tile holds few records).  (One wave per channel with
-// per-lane tile cursors measured 1 % slower per step.)
+// each wave writes its records at their offsets in event order, and the
+// channel's two counts go out; the tile workgroups find their tiles' windows
+// in the records they stage.  (Round 4 wrote every tile's window here, 4.5 us
+// of the kernel's 14.8; one wave per channel with per-lane tile cursors
+// measured 1 % slower per step.)
 // ===========================================================================
 __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
 {
     constexpr int W = BLOCK / 64;
     constexpr int K = DDS_MAX_EVENTS / BLOCK;           // event chunks per wave
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     __shared__ uint32_t s_cnt[2][K * W + 1];
-    uint32_t *s_st_t = reinterpret_cast<uint32_t *>(s_dyn);
-    uint32_t *s_rs_t = s_st_t + p.ev_lds;
     const uint32_t tid = threadIdx.x, wl = tid & 63u, wv = tid >> 6;
     const uint32_t ch = blockIdx.x;
     const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
-    const uint32_t lane = d[0], elem = d[1] & 3u, spc = d[2];
+    const uint32_t lane = d[0], elem = d[1] & 3u;
     const uint32_t n_ev = min(p.summary[8ull * lane + 2], p.event_cap);
     uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
     uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
@@ -233,29 +230,34 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
         if (is_st[k]) {
             const uint32_t i = os + (uint32_t)__popcll(bs & below);
             xs[i] = make_uint4(ev[k].x, ev[k].y & 0xFFFFFFu, ev[k].z, ev[k].w & 0xFFFFu);
-            s_st_t[i] = ev[k].x;
         }
         if (is_rs[k]) {
             const uint32_t i = orr + (uint32_t)__popcll(br & below);
             xr[i] = ev[k].x;
-            s_rs_t[i] = ev[k].x;
         }
     }
-    __syncthreads();
-    // window of tile c (samples [c DDS_TILE, + DDS_TILE) of the channel): from
-    // the latest record at or before its first cycle (the first record when
-    // none is) to the latest at or before its last
-    for (uint32_t c = tid; c < p.tiles; c += BLOCK) {
-        const uint64_t j0 = (uint64_t)c * DDS_TILE;
-        const uint64_t j1 = min(j0 + DDS_TILE, (uint64_t)p.n_samples) - 1;
-        const uint32_t n0 = (uint32_t)(j0 / spc), n1 = (uint32_t)(j1 / spc);
-        const int a0 = last_le(s_st_t, (int)n_st, n0) + 1, b0 = last_le(s_rs_t, (int)n_rs, n0) + 1;
-        int a1 = a0, b1 = b0;
-        while (a1 < (int)n_st && s_st_t[a1] <= n1) a1++;
-        while (b1 < (int)n_rs && s_rs_t[b1] <= n1) b1++;
-        const int sl = max(a0 - 1, 0), rl = max(b0 - 1, 0);
-        p.win[(uint64_t)ch * p.tiles + c] = make_uint4((uint32_t)sl, (uint32_t)(a1 - sl), (uint32_t)rl, (uint32_t)(b1 - rl));
+    if (tid == 0) p.cnt[ch] = make_uint2(n_st, n_rs);
+}
+
+// the latest strobe record with t <= x among rec[0, n) (time-sorted), or -1
+__device__ __forceinline__ int last_le_rec(const uint4 *rec, int n, uint32_t x)
+{
+    int lo = 0, hi = n;                 // first index with t > x
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (rec[mid].x <= x) lo = mid + 1; else hi = mid;
     }
+    return lo - 1;
+}
+
+// a tile's window from its raw search results {a0, a1, b0, b1} (a0 / b0:
+// strobes / resets at or before the tile's first cycle, a1 / b1: at or
+// before its last): from the latest record at or before the first cycle
+// (the first record when none is) to the latest at or before the last
+__device__ __forceinline__ uint4 tile_window(uint4 raw)
+{
+    const uint32_t sl = raw.x ? raw.x - 1u : 0u, rl = raw.z ? raw.z - 1u : 0u;
+    return make_uint4(sl, raw.y - sl, rl, raw.w - rl);
 }
 
 // the latest record at or before cycle n inside a window {lo, count} of a
@@ -331,7 +333,7 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
             const uint32_t tb = M.first(i);                                 // the tile's first sample (16 | tb)
             const uint32_t js = tb + 16 * ln;                               // this lane's cycle n = js / 16
             const uint32_t n = js >> 4;
-            const uint4 w = L.win[i];
+            const uint4 w = tile_window(L.win[i]);
             uint32_t v[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) v[q] = 0u;
@@ -432,7 +434,7 @@ __device__ __forceinline__ void tile_sweep(const DDSParams &p, const TileLds &L,
     for (uint32_t i = 0; i < n_t; i++) {
         const uint32_t j0 = M.first(i) + 4 * tid;
         if (j0 >= p.n_samples) continue;
-        const uint4 w = L.win[i];
+        const uint4 w = tile_window(L.win[i]);
         uint32_t v[4] = {0u, 0u, 0u, 0u};
         if (quad) {
             const uint32_t n = j0 >> spc_sh;                         // the thread's 4 samples share cycle n
@@ -563,11 +565,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7)))
     const uint32_t env_off = d[4], env_len = d[5], freq_off = d[6], freq_len = d[7];
     const bool spc_p2 = (spc & (spc - 1)) == 0, int_p2 = (interp & (interp - 1)) == 0;
     const bool staged = (interp == 1 ? dds_env_pairs_words(env_len) : env_len) <= p.env_lds && 2 * freq_len <= p.freq_lds;
-    const uint4 *gwin = p.win + (uint64_t)ch * p.tiles;
-    // the workgroup's strobes / resets: from its first tile's window to its last's end
-    const uint4 w_first = gwin[M.tile(0)], w_last = gwin[M.tile(n_t - 1)];
-    const uint32_t st_lo = w_first.x, st_n = w_last.x + w_last.y - st_lo;
-    const uint32_t rs_lo = w_first.z, rs_n = w_last.z + w_last.w - rs_lo;
+    // the channel's strobes / resets (a stripe's tiles span the channel)
+    const uint2 cnt = p.cnt[ch];
+    const uint32_t st_n = cnt.x, rs_n = cnt.y;
     const bool fits = st_n <= p.rec_lds && rs_n <= p.rec_lds;    // workgroup-uniform
 
     // prologue: every global load of the workgroup up front
@@ -598,16 +598,27 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7)))
     const uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
     const uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
     if (fits) {
-        for (uint32_t i = tid; i < st_n; i += BLOCK) s_st[i] = xs[st_lo + i];
-        for (uint32_t i = tid; i < rs_n; i += BLOCK) s_rs_t[i] = xr[rs_lo + i];
+        for (uint32_t i = tid; i < st_n; i += BLOCK) s_st[i] = xs[i];
+        for (uint32_t i = tid; i < rs_n; i += BLOCK) s_rs_t[i] = xr[i];
     }
-    for (uint32_t i = tid; i < n_t; i += BLOCK) s_win[i] = gwin[M.tile(i)];
     bad = __syncthreads_or(bad);
+    // the tiles' windows: 4 searches per tile, one per thread (raw counts,
+    // tile_window in the sweep)
+    const uint32_t spc_sh = __ffs(spc) - 1;
+    for (uint32_t q = tid; q < 4 * n_t; q += BLOCK) {
+        const uint32_t j0 = M.first(q >> 2), j1 = min(j0 + DDS_TILE, p.n_samples) - 1, j = (q & 1u) ? j1 : j0;
+        const uint32_t n = spc_p2 ? j >> spc_sh : j / spc;
+        int r;
+        if (q & 2u) r = fits ? last_le(s_rs_t, (int)rs_n, n) : last_le(xr, (int)rs_n, n);
+        else r = fits ? last_le_rec(s_st, (int)st_n, n) : last_le_rec(xs, (int)st_n, n);
+        reinterpret_cast<uint32_t *>(s_win)[q] = (uint32_t)(r + 1);
+    }
+    __syncthreads();
 
     const bool quad = staged && !bad && (spc & 3u) == 0 && spc_p2 && int_p2 && (interp == 1 || interp >= 4);
     const TileLds L{s_lut, s_win, s_env, s_freq, s_xpose};
     if (fits)
-        tile_sweep(p, L, d, M, quad, s_st, st_lo, s_rs_t, rs_lo);
+        tile_sweep(p, L, d, M, quad, s_st, 0u, s_rs_t, 0u);
     else
         tile_sweep(p, L, d, M, quad, xs, 0u, xr, 0u);
 }
@@ -615,8 +626,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7)))
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    // the channel's strobe and reset times: 2 * ev_lds words <= 8 KiB
-    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), 2 * p.ev_lds * 4, stream, p);
+    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), 0, stream, p);
     return hipGetLastError();
 }
 

@@ -236,7 +236,7 @@ struct DDSParams {
     // event index (dds_index_kernel -> dds_tile_kernel)
     uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
     uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
-    uint4 *win;                    // [n_channels][tiles] {strobe lo, count, reset lo, count}
+    uint2 *cnt;                    // [n_channels] {strobes, resets}
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
 constexpr uint32_t DDS_MAX_EVENTS = 1024;
@@ -269,10 +269,10 @@ constexpr uint32_t DDS_REC_LDS_MIN = 64;
 // pairs (dds.hip env_pair): whole groups of 8 16-B chunks
 __host__ __device__ inline uint32_t dds_env_pairs_words(uint32_t n) { return (2 * n + 31) & ~31u; }
 
-// bytes of the event index (xs, xr, win)
-inline uint64_t dds_index_bytes(uint32_t n_channels, uint32_t ev_lds, uint32_t tiles)
+// bytes of the event index (xs, xr, cnt)
+inline uint64_t dds_index_bytes(uint32_t n_channels, uint32_t ev_lds)
 {
-    return (uint64_t)n_channels * ev_lds * 20 + (uint64_t)n_channels * tiles * 16;
+    return (uint64_t)n_channels * ev_lds * 20 + (uint64_t)n_channels * 8;
 }
 
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream);
