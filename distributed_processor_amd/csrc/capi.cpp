@@ -958,6 +958,11 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.xs = reinterpret_cast<uint4 *>(b);
     p.xr = reinterpret_cast<uint32_t *>(b + (uint64_t)p.n_channels * p.ev_lds * 16);
     p.cnt = reinterpret_cast<uint2 *>(b + (uint64_t)p.n_channels * p.ev_lds * 20);
+    // channels 2i and 2i + 1 on one lane (a qdrv / rdrv pair per core, say): one
+    // index workgroup loads that lane's events once for both
+    p.pair_lanes = p.n_channels % 2 == 0;
+    for (uint32_t i = 0; p.pair_lanes && i < p.n_channels; i += 2)
+        p.pair_lanes = desc[(size_t)i * DDS_CH_WORDS] == desc[(size_t)(i + 1) * DDS_CH_WORDS];
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, launch_dds_index(p, s));   // outside the timed bracket: it holds the synthesis kernel alone
     HIPCHK(ctx, timing_start(ctx, s, &ev_stop));

@@ -190,17 +190,17 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
 {
     constexpr int W = BLOCK / 64;
     constexpr int K = DDS_MAX_EVENTS / BLOCK;           // event chunks per wave
-    __shared__ uint32_t s_cnt[2][K * W + 1];
+    __shared__ uint32_t s_cnt[3][K * W + 1];            // strobes of channel 0 / 1, resets
     const uint32_t tid = threadIdx.x, wl = tid & 63u, wv = tid >> 6;
-    const uint32_t ch = blockIdx.x;
-    const uint32_t *d = p.ch + DDS_CH_WORDS * ch;
-    const uint32_t lane = d[0], elem = d[1] & 3u;
+    // the workgroup's channels: ch0 and, when p.pair_lanes, ch0 + 1 (same lane)
+    const uint32_t G = p.pair_lanes ? 2u : 1u;
+    const uint32_t ch0 = blockIdx.x * G;
+    const uint32_t *d = p.ch + DDS_CH_WORDS * ch0;
+    const uint32_t lane = d[0], elem0 = d[1] & 3u, elem1 = G == 2u ? d[DDS_CH_WORDS + 1] & 3u : 0xFFu;
     const uint32_t n_ev = min(p.summary[8ull * lane + 2], p.event_cap);
-    uint4 *xs = p.xs + (uint64_t)ch * p.ev_lds;
-    uint32_t *xr = p.xr + (uint64_t)ch * p.ev_lds;
     const uint64_t below = wl ? (~0ull >> (64 - wl)) : 0ull;
     uint4 ev[K];
-    bool is_st[K], is_rs[K];
+    bool is_s0[K], is_s1[K], is_rs[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const uint32_t e = (k * W + wv) * 64u + wl;
@@ -209,34 +209,38 @@ __global__ void __launch_bounds__(BLOCK) dds_index_kernel(const DDSParams p)
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const uint32_t e = (k * W + wv) * 64u + wl;
-        const uint32_t kind = ev[k].y >> 28;
-        is_st[k] = e < n_ev && kind == 0u && ((ev[k].y >> 24) & 3u) == elem;
+        const uint32_t kind = ev[k].y >> 28, el = (ev[k].y >> 24) & 3u;
+        is_s0[k] = e < n_ev && kind == 0u && el == elem0;
+        is_s1[k] = e < n_ev && kind == 0u && el == elem1;
         is_rs[k] = e < n_ev && kind == 1u;
-        const uint32_t ns = (uint32_t)__popcll(__ballot(is_st[k])), nr = (uint32_t)__popcll(__ballot(is_rs[k]));
-        if (wl == 0) { s_cnt[0][k * W + wv] = ns; s_cnt[1][k * W + wv] = nr; }
+        const uint32_t n0 = (uint32_t)__popcll(__ballot(is_s0[k])), n1 = (uint32_t)__popcll(__ballot(is_s1[k]));
+        const uint32_t nr = (uint32_t)__popcll(__ballot(is_rs[k]));
+        if (wl == 0) { s_cnt[0][k * W + wv] = n0; s_cnt[1][k * W + wv] = n1; s_cnt[2][k * W + wv] = nr; }
     }
     __syncthreads();
-    if (tid < 2) {                                      // exclusive scans of the chunk counts (+ totals)
+    if (tid < 3) {                                      // exclusive scans of the chunk counts (+ totals)
         uint32_t acc = 0;
         for (int q = 0; q < K * W; q++) { const uint32_t c = s_cnt[tid][q]; s_cnt[tid][q] = acc; acc += c; }
         s_cnt[tid][K * W] = acc;
     }
     __syncthreads();
-    const uint32_t n_st = s_cnt[0][K * W], n_rs = s_cnt[1][K * W];
+    uint4 *xs0 = p.xs + (uint64_t)ch0 * p.ev_lds, *xs1 = xs0 + p.ev_lds;
+    uint32_t *xr0 = p.xr + (uint64_t)ch0 * p.ev_lds, *xr1 = xr0 + p.ev_lds;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-        const uint32_t os = s_cnt[0][k * W + wv], orr = s_cnt[1][k * W + wv];   // records in the chunks before
-        const uint64_t bs = __ballot(is_st[k]), br = __ballot(is_rs[k]);
-        if (is_st[k]) {
-            const uint32_t i = os + (uint32_t)__popcll(bs & below);
-            xs[i] = make_uint4(ev[k].x, ev[k].y & 0xFFFFFFu, ev[k].z, ev[k].w & 0xFFFFu);
-        }
+        const uint32_t q = k * W + wv;                  // records in the chunks before: s_cnt[.][q]
+        const uint64_t b0 = __ballot(is_s0[k]), b1 = __ballot(is_s1[k]), br = __ballot(is_rs[k]);
+        const uint4 rec = make_uint4(ev[k].x, ev[k].y & 0xFFFFFFu, ev[k].z, ev[k].w & 0xFFFFu);
+        if (is_s0[k]) xs0[s_cnt[0][q] + (uint32_t)__popcll(b0 & below)] = rec;
+        if (is_s1[k]) xs1[s_cnt[1][q] + (uint32_t)__popcll(b1 & below)] = rec;
         if (is_rs[k]) {
-            const uint32_t i = orr + (uint32_t)__popcll(br & below);
-            xr[i] = ev[k].x;
+            const uint32_t i = s_cnt[2][q] + (uint32_t)__popcll(br & below);
+            xr0[i] = ev[k].x;
+            if (G == 2u) xr1[i] = ev[k].x;
         }
     }
-    if (tid == 0) p.cnt[ch] = make_uint2(n_st, n_rs);
+    if (tid == 0) p.cnt[ch0] = make_uint2(s_cnt[0][K * W], s_cnt[2][K * W]);
+    if (tid == 0 && G == 2u) p.cnt[ch0 + 1] = make_uint2(s_cnt[1][K * W], s_cnt[2][K * W]);
 }
 
 // the latest strobe record with t <= x among rec[0, n) (time-sorted), or -1
@@ -626,7 +630,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7)))
 hipError_t launch_dds_index(const DDSParams &p, hipStream_t stream)
 {
     if (!p.n_channels || !p.n_samples) return hipSuccess;
-    hipLaunchKernelGGL(dds_index_kernel, dim3(p.n_channels), dim3(BLOCK), 0, stream, p);
+    // a workgroup per channel, or per pair of channels on one lane (pair_lanes)
+    hipLaunchKernelGGL(dds_index_kernel, dim3(p.pair_lanes ? p.n_channels / 2 : p.n_channels), dim3(BLOCK), 0, stream, p);
     return hipGetLastError();
 }
 

@@ -237,6 +237,7 @@ struct DDSParams {
     uint4 *xs;                     // [n_channels][ev_lds] strobes {t, env word, phase | freq << 17, amp}
     uint32_t *xr;                  // [n_channels][ev_lds] pulse_reset times
     uint2 *cnt;                    // [n_channels] {strobes, resets}
+    uint32_t pair_lanes;           // channels 2i, 2i + 1 share a lane (one index workgroup per pair)
 };
 constexpr uint32_t DDS_CH_WORDS = 8;   // lane, elem, spc, interp, env_off, env_len, freq_off, freq_len
 constexpr uint32_t DDS_MAX_EVENTS = 1024;
