@@ -281,13 +281,16 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
             an = q[0];
             un = q[1];
         }
-        if (p.macro_w3) {                               // (uniform) three ALU slots, ctl packed in a.y
-            alu_step(a.x, w3_ctl(a.y, 0));
-            alu_step(a.z, w3_ctl(a.y, 1));
-            alu_step(a.w, w3_ctl(a.y, 2));
-        } else {
-            alu_step(a.x, a.y);
-            alu_step(a.z, a.w);
+        // the ALU slots: three with ctl packed in a.y (MACRO_W3, uniform), else
+        // two; one copy of the slot code in a rolled loop (three inlined
+        // copies left the kernel's lambda state in scratch: 4.4 -> 44 ms on
+        // config 4 through this kernel)
+        const uint32_t n_alu = p.macro_w3 ? 3u : 2u;
+#pragma unroll 1
+        for (uint32_t s = 0; s < n_alu; s++) {
+            const uint32_t imm = s == 0u ? a.x : s == 1u ? a.z : a.w;
+            const uint32_t ctl = p.macro_w3 ? w3_ctl(a.y, (int)s) : (s == 0u ? a.y : a.w);
+            alu_step(imm, ctl);
         }
         pulse_step(u);
     }
