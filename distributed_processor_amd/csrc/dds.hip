@@ -7,17 +7,18 @@
 // sample, nothing else leaves the chip.
 //
 // Two launches per synthesis:
-//   * dds_index_kernel (one workgroup per channel) compacts the lane's strobes
-//     of the channel's element and its pulse_resets (time-sorted: a core emits
-//     them in time order) once, channel-contiguous, and writes every sample
-//     tile's window of them (the records a tile's samples can see);
+//   * dds_index_kernel (one workgroup per channel, or per two channels of one
+//     lane) compacts the lane's strobes of the channel's element and its
+//     pulse_resets (time-sorted: a core emits them in time order) once,
+//     channel-contiguous, and writes the channel's two counts;
 //   * dds_tile_kernel, grid (stripes, channels).  A channel's 1,024-sample
 //     tiles go round-robin to its stripe workgroups, so at any time the
 //     stripes of a channel write ADJACENT tiles.  A workgroup stages the
 //     quarter-wave sine table, the channel's env / freq tables -- as
 //     (E, E') / (R, R') pairs for the Y-form products, the env pairs in
-//     bank-swizzled chunks -- its strobes (up to rec_lds; a denser stripe
-//     reads them from the global index) and its tiles' windows in LDS, then
+//     bank-swizzled chunks -- and the channel's records (up to rec_lds; a
+//     denser channel is read from the global index) in LDS, finds each of its
+//     tiles' window of records (the ones the tile's samples can see), then
 //     sweeps with no global loads in the loop (on gfx950 stores count in
 //     vmcnt, so a load there would wait for the previous tile's stores).
 //     At 16 samples per clock (the RFSoC rate) a lane makes one whole cycle
