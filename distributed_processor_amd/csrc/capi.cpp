@@ -670,6 +670,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     // wave: (program groups a wave's run of consecutive shots can span) x
     // (cores in the wave), for the thread mapping of block_core_major
     bool staged = false;
+    uint32_t slots = 0;                     // program slots per wave of the staged kernel (0: macro_kernel)
     if (macro && !(cfg->exec_flags & DPEMU_X_MACRO_DIRECT)) {
         uint64_t shots_run, cores_w;
         if (cfg->lane_order == DPEMU_LANES_SHOT_MAJOR) {
@@ -682,7 +683,9 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
         }
         const uint64_t spg = cfg->shots_per_group;
         const uint64_t groups = ng == 1 ? 1 : std::min<uint64_t>(ng, (shots_run - 1 + spg - 1) / spg + 1);
-        staged = groups * cores_w <= MACRO_SLOTS;
+        const uint64_t need = groups * cores_w;
+        slots = need <= MACRO_SLOTS ? MACRO_SLOTS : (need <= MACRO_SLOTS_WIDE && ctx->macro_nr == 2) ? MACRO_SLOTS_WIDE : 0u;
+        staged = slots != 0u;
     }
     int src = cmd_major ? STRAIGHT_ROWS : STRAIGHT_PROG;
     if (uniform) {
@@ -766,7 +769,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     hipEvent_t ev_stop = nullptr;
     HIPCHK(ctx, timing_start(ctx, stream, &ev_stop));
     if (uniform) HIPCHK(ctx, launch_straight(p, src, fetch_batch, stream));
-    else if (macro) HIPCHK(ctx, launch_macro(p, staged, ctx->macro_nr, ctx->macro_addid, stream));
+    else if (macro) HIPCHK(ctx, launch_macro(p, slots, ctx->macro_nr, ctx->macro_addid, stream));
     else if (branch) HIPCHK(ctx, launch_branch(p, bfeat, stream));
     else HIPCHK(ctx, launch_interp(p, feat, stream));
     if (ev_stop) HIPCHK(ctx, hipEventRecord(ev_stop, stream));
@@ -776,7 +779,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
             snprintf(name, sizeof name, "straight_kernel<%s,fb%d>",
                      src == STRAIGHT_ROWS ? "rows" : src == STRAIGHT_PROG ? "prog" : "lds", fetch_batch);
         else if (macro && staged)
-            snprintf(name, sizeof name, "macro_staged_kernel<%d%s>", ctx->macro_nr, ctx->macro_addid ? ",addid" : "");
+            snprintf(name, sizeof name, "macro_staged_kernel<%d%s%s>", ctx->macro_nr, ctx->macro_addid ? ",addid" : "",
+                     slots > MACRO_SLOTS ? ",12" : "");
         else if (macro)
             snprintf(name, sizeof name, "macro_kernel");
         else if (branch)

@@ -182,9 +182,11 @@ hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream);
 // register slots the macro image names: 2, else 16 in LDS), else
 // macro_kernel (staged = false)
 constexpr uint32_t MACRO_SLOTS = 8;     // distinct programs per wave whose macros are staged in LDS
+constexpr uint32_t MACRO_SLOTS_WIDE = 12;   // ... for runs whose waves span 9-12 programs (NR == 2 images)
 constexpr uint32_t MACRO_CHUNK = 16;    // macros per program per staged chunk (8: 3.84-4.12 vs 3.60 ms)
 // addid: every ALU slot of the image is reg_alu id0 / add (RB phase updates)
-hipError_t launch_macro(const KParams &p, bool staged, int nr, bool addid, hipStream_t stream);
+// slots: 0 = macro_kernel (per-lane fetch), else the staged kernel's program slots per wave
+hipError_t launch_macro(const KParams &p, uint32_t slots, int nr, bool addid, hipStream_t stream);
 constexpr uint32_t MACRO_ABSENT = 0x80000000u;   // pulse slot w bit 31: no command; ALU ctl bit 31: present
 // pulse slot w bit 30 (capi.cpp mark_simple_macros): not a program's first
 // macro, its ALU slots are reg_alu (no inc_qclk) and its pulse slot is a

@@ -697,10 +697,14 @@ struct MacroLane {
     }
 };
 
-template <int NR, bool ADDID>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR == 16 ? 3 : 4))) macro_staged_kernel(const KParams p)
+// NSL: program slots per wave -- MACRO_SLOTS, or MACRO_SLOTS_WIDE (NR == 2
+// only) for runs whose waves span more programs (fewer shots per program);
+// the wide chunks (48 KiB per workgroup) hold 3 workgroups per CU
+template <int NR, bool ADDID, int NSL>
+__global__ void __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(NR == 16 || NSL > (int)MACRO_SLOTS ? 3 : 4))) macro_staged_kernel(const KParams p)
 {
-    constexpr uint32_t NW = BLOCK / 64, CH = MACRO_CHUNK, NS = MACRO_SLOTS;
+    constexpr uint32_t NW = BLOCK / 64, CH = MACRO_CHUNK, NS = NSL;
     constexpr uint32_t PIECES = NS * CH * 2;          // 16-B pieces of a chunk
     constexpr uint32_t PL = PIECES / 64;              // pieces per lane
     static_assert(PIECES % 64 == 0 && (CH & (CH - 1)) == 0, "whole pieces per lane, power-of-two chunk");
@@ -870,17 +874,22 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NR =
     count_outcome_block(p, s_hist, s_key, valid, core, sl, valid ? shot_group(p, sl) : 0u, L.last_bit);
 }
 
-hipError_t launch_macro(const KParams &p, bool staged, int nr, bool addid, hipStream_t stream)
+hipError_t launch_macro(const KParams &p, uint32_t slots, int nr, bool addid, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p.n_lanes + BLOCK - 1) / BLOCK);
     if (blocks == 0) return hipSuccess;
-    if (!staged) hipLaunchKernelGGL(macro_kernel, dim3(blocks), dim3(BLOCK), 0, stream, p);
-    else {
-        const size_t shmem = p.hist_lds ? HIST_LDS_MAX * sizeof(uint32_t) : 0;
-        if (nr == 2 && addid) hipLaunchKernelGGL((macro_staged_kernel<2, true>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
-        else if (nr == 2) hipLaunchKernelGGL((macro_staged_kernel<2, false>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
-        else hipLaunchKernelGGL((macro_staged_kernel<16, false>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
-    }
+    const size_t shmem = p.hist_lds ? HIST_LDS_MAX * sizeof(uint32_t) : 0;
+    constexpr int S = MACRO_SLOTS, SW = MACRO_SLOTS_WIDE;
+    if (slots == 0u) hipLaunchKernelGGL(macro_kernel, dim3(blocks), dim3(BLOCK), 0, stream, p);
+    else if (slots > MACRO_SLOTS && nr == 2 && addid)
+        hipLaunchKernelGGL((macro_staged_kernel<2, true, SW>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    else if (slots > MACRO_SLOTS && nr == 2)
+        hipLaunchKernelGGL((macro_staged_kernel<2, false, SW>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    else if (slots > MACRO_SLOTS)
+        return hipErrorInvalidValue;                     // (the host offers wide slots to NR == 2 images only)
+    else if (nr == 2 && addid) hipLaunchKernelGGL((macro_staged_kernel<2, true, S>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    else if (nr == 2) hipLaunchKernelGGL((macro_staged_kernel<2, false, S>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
+    else hipLaunchKernelGGL((macro_staged_kernel<16, false, S>), dim3(blocks), dim3(BLOCK), shmem, stream, p);
     return hipGetLastError();
 }
 

@@ -19,14 +19,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def workload(name):
     from distributed_processor_amd import _abi, isa, workloads
     from distributed_processor_amd.emulator import ProgramSet
-    if name in ('rb', 'rb_sm'):   # rb_sm: 10^4 shots (a quick correctness check of a new build)
-        ps = workloads.config4_rb_set(100000 if name == 'rb' else 1000, 200)
+    if name in ('rb', 'rb_sm', 'rb8'):   # rb_sm: 10^4 shots (a quick check of a new build); rb8: 8 shots per sequence
+        spg = 8 if name == 'rb8' else 10
+        ps = workloads.config4_rb_set(100000 if name != 'rb_sm' else 1000, 200)
         ops = ps.words[:, 3] >> 28
         ev = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
                              ps.offsets.astype(np.int64))
-        cfg = _abi.make_config(2, n_groups=ps.n_groups, shots_per_group=10, max_cycles=1 << 20,
+        cfg = _abi.make_config(2, n_groups=ps.n_groups, shots_per_group=spg, max_cycles=1 << 20,
                                event_cap=int(ev.max()) + 1, meas_cap=2, seed=0x5EED)
-        return ps, cfg, 10 ** 6 if name == 'rb' else 10 ** 4
+        return ps, cfg, 10 ** 4 if name == 'rb_sm' else spg * 10 ** 5
     if name == 'ramsey':
         ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
         cfg = _abi.make_config(8, n_groups=100, max_cycles=1 << 20, event_cap=8, meas_cap=2, seed=0x5EED)

@@ -5,7 +5,7 @@
 set -o pipefail
 out=gpurun_out/r5/rb_spg
 mkdir -p $out
-for spg in 8 10 16; do
+for spg in ${SPGS:-8 10 16}; do
   timeout -k 10 300 python bench.py --legs rb --no-cpu-baseline --rb-spg $spg --steps 10 > $out/spg$spg.json 2> $out/spg$spg.err || { tail $out/spg$spg.err; exit 1; }
   python - $out/spg$spg.json $spg <<'PY'
 import json, sys

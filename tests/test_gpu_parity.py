@@ -154,14 +154,20 @@ def test_fuzz_linear_few_registers(emu, seed):
                            lane_order=order)
     g, f = run_pair(emu, ps, cfg, 64 * 9 + 7 * seed, shot0=seed * 31)
     compare_all(g, f, 'seed {} regs {}'.format(seed, regs))
-    # the kernel the run used: staged when a wave spans <= 8 distinct programs (capi.cpp)
+    # the kernel the run used (capi.cpp): staged when a wave spans <= 8 distinct
+    # programs, or <= 12 (MACRO_SLOTS_WIDE) with the 2-register VGPR file
     shots_run = 64 // C if order else min(256 // C, 64)
     cores_w = C if order else 64 // shots_run
-    staged = (-(-(shots_run - 1) // spg) + 1) * cores_w <= 8
+    need = (-(-(shots_run - 1) // spg) + 1) * cores_w
     emu.run(3, 0, cfg=cfg)
     got = emu.last_kernel().replace(',addid', '')   # addid: every ALU op of the image is id0 / add
-    if not staged:
+    if need > 12:
         assert got == 'macro_kernel', got
+    elif need > 8:
+        if len(regs) <= 2:
+            assert got == 'macro_staged_kernel<2,12>', got
+        else:                   # the wide kernel only with the 2-register file
+            assert got in ('macro_staged_kernel<2,12>', 'macro_kernel'), got
     elif len(regs) <= 2:
         assert got == 'macro_staged_kernel<2>', got
     else:                       # <2> when the programs happen to read / write at most 2 of them

@@ -158,8 +158,9 @@ def test_rb_lean_path_edges(max_cycles):
                 g, f = run_pair(emu, ps, cfg, 960, 13)
                 compare_all(g, f, 'max_cycles {} order {} trace {}'.format(max_cycles, order, trace_cap))
                 emu.run(3, 0, cfg=cfg)
-                # shot-major waves span 5 sequences x 2 cores > MACRO_SLOTS: the per-lane macro_kernel
-                want = 'macro_staged_kernel<2,addid>' if order == _abi.LANES_CORE_MAJOR else 'macro_kernel'
+                # shot-major waves span 5 sequences x 2 cores > MACRO_SLOTS: the 12-slot staged kernel
+                want = 'macro_staged_kernel<2,addid>' if order == _abi.LANES_CORE_MAJOR else \
+                    'macro_staged_kernel<2,addid,12>'
                 assert emu.last_kernel() == want, emu.last_kernel()
 
 
@@ -192,3 +193,38 @@ def test_lean_chunk_after_qclk_wrap(max_cycles):
     status = _abi.unpack_summary(np.asarray(g['summary']).view(np.uint32))['status']
     if max_cycles < 1600:
         assert (status == _abi.ST_MAX_CYCLES).all()
+
+
+@pytest.mark.parametrize('spg,kernel', [(8, 'macro_staged_kernel<2,addid,12>'), (6, 'macro_staged_kernel<2,addid,12>'),
+                                        (4, 'macro_kernel')])
+def test_fewer_shots_per_sequence(spg, kernel):
+    """RB sequences with 8 / 6 / 4 shots each: a wave of 64 consecutive shots
+    spans 9-12 programs (the 12-slot staged kernel) or more (the per-lane
+    fetch macro_kernel); every output against oracle_fast"""
+    import torch
+    n_seq = 3000
+    ps = workloads.config4_rb_set(n_seq, 60)
+    ops = ps.words[:, 3] >> 28
+    strobes = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
+                              ps.offsets.astype(np.int64))
+    cfg = _abi.make_config(2, n_groups=n_seq, shots_per_group=spg, max_cycles=1 << 20,
+                           event_cap=int(strobes.max()) + 1, meas_cap=2, meas_latency=64, seed=0xBEEF, p1=0.5)
+    n_shots = n_seq * spg
+    emu = Emulator(0)
+    try:
+        emu.load(ps)
+        want = ('summary', 'events', 'meas', 'regs')
+        out = alloc_device_outputs(cfg, n_shots, want=want + ('hist',))
+        for t in out.values():
+            t.zero_()
+        emu.run_device(cfg, n_shots, 0, out)
+        torch.cuda.synchronize()
+        assert emu.last_kernel() == kernel, emu.last_kernel()
+        f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n_shots, threads=8,
+                            want=want + ('hist',))
+        for k in want:
+            a = out[k].cpu().numpy().view(f[k].dtype)
+            assert np.array_equal(a, f[k]), (spg, k, int((a != f[k]).sum()))
+        assert np.array_equal(out['hist'].cpu().numpy().view(f['hist'].dtype).reshape(f['hist'].shape), f['hist'])
+    finally:
+        emu.close()
