@@ -179,8 +179,8 @@ hipError_t opt_in_dynamic_lds(const void *fn, size_t bytes);
 hipError_t launch_branch(const KParams &p, int feat, hipStream_t stream);
 // branch-free programs with reg_alu / inc_qclk (macro.hip): macro_staged_kernel
 // when every wave runs at most MACRO_SLOTS distinct programs (nr = the
-// register slots the macro image names: 2, else 16 in LDS), else
-// macro_kernel (staged = false)
+// register slots the macro image names: 2, else 16 in LDS), or at most
+// MACRO_SLOTS_WIDE with nr == 2, else macro_kernel (slots = 0)
 constexpr uint32_t MACRO_SLOTS = 8;     // distinct programs per wave whose macros are staged in LDS
 constexpr uint32_t MACRO_SLOTS_WIDE = 12;   // ... for runs whose waves span 9-12 programs (NR == 2 images)
 constexpr uint32_t MACRO_CHUNK = 16;    // macros per program per staged chunk (8: 3.84-4.12 vs 3.60 ms)
