@@ -23,6 +23,11 @@ Sub-objects on the same line, each with its own roofline and CPU baselines:
                   shots per GPU (10^7 over 8 GPUs)
   "lut"           config 3's circuit through the fproc_lut back end: every
                   core waits on a syndrome LUT over the 8 measurements
+  "demod"         config 3 with the readout demodulation model (meas_model
+                  DEMOD: each rdlo window demodulates its rdrv return into an
+                  accumulated I/Q, written per readout, and a per-core
+                  discriminator decides the outcome); its cost over the
+                  STATE model's leg is on the line ("model_cost")
   "rb"            config 4 at its stated size: 10^5 distinct 2-core depth-200
                   RB sequences x 10 shots per GPU, one batch per step
                   (--rb-depth > 1 also measures batches in flight,
@@ -128,7 +133,7 @@ def median_rate(run, units_per_n, n0, target_s=0.8, reps=5):
     return n * units_per_n / float(np.median(times)), n, times
 
 
-def cpu_baselines(ps, cfg, horizon, what, all_cores=False):
+def cpu_baselines(ps, cfg, horizon, what, all_cores=False, ro=None):
     """oracle_fast (the job's threads) and oracle_rtl (1 thread, the job's
     threads) on the leg's workload.  all_cores: also oracle_fast at one
     thread, and the whole host's rate (BASELINE.md:46 asks for all host
@@ -139,8 +144,9 @@ def cpu_baselines(ps, cfg, horizon, what, all_cores=False):
     threads, info = host_cores()
     C = cfg.cores_per_shot
     want = ('summary', 'events', 'meas', 'hist')
-    fast = lambda k: lambda n: oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n, k, want)
-    rtl = lambda k: lambda n: oracle.rtl_run_batch(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n, horizon, k)
+    fast = lambda k: lambda n: oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n, k, want, ro=ro)
+    rtl = lambda k: lambda n: oracle.rtl_run_batch(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, n, horizon, k,
+                                                   ro=ro)
     f_rate, f_n, f_t = median_rate(fast(threads), C, 2000)
     r1_rate, r1_n, r1_t = median_rate(rtl(1), C, 20)
     ra_rate, ra_n, ra_t = median_rate(rtl(threads), C, 20 * threads)
@@ -160,13 +166,14 @@ def cpu_baselines(ps, cfg, horizon, what, all_cores=False):
         f1_rate, f1_n, _ = median_rate(fast(1), C, 200)
         nproc = info['nproc']
         res['oracle_fast']['value_1_thread'] = f1_rate
+        eff = f_rate / (f1_rate * threads)
         res['all_cores'] = {
             'value': f_rate * nproc / threads, 'unit': 'core-shots/s', 'threads': nproc, 'kind': 'extrapolated',
-            'scaling_1_to_{}_threads'.format(threads): f_rate / (f1_rate * threads),
-            'note': 'oracle_fast on all {} host CPUs, extrapolated linearly from the measured {}-thread rate '
-                    '(shots are independent; the 1 -> {} thread scaling measured beside it is the efficiency '
-                    'shown); not run at {} threads because the harness grants this job {} of them'.format(
-                        nproc, threads, threads, nproc, threads)}
+            'bound': 'upper', 'scaling_1_to_{}_threads'.format(threads): eff,
+            'note': 'an UPPER BOUND on oracle_fast over all {} host CPUs: the measured {}-thread rate scaled '
+                    'linearly, although the 1 -> {} thread efficiency measured beside it is only {:.2f}; not run '
+                    'at {} threads because the harness grants this job {} of them'.format(
+                        nproc, threads, threads, eff, nproc, threads)}
     return res
 
 
@@ -247,12 +254,13 @@ def hbm_roofline(alg_bytes, kernel_ms, ms_per_step, kernel, prof, rocprof_key):
     return r
 
 
-def bytes_per_lane(summary_np, cfg):
+def bytes_per_lane(summary_np, cfg, acc=False):
     """algorithmic HBM bytes written per lane: 32 B summary + 16 B per event
-    record + 8 B per measurement record"""
+    record + 8 B per measurement record (+ 8 B of accumulated I/Q per
+    measurement when the run writes dpemu_outputs.acc)"""
     n_ev = np.minimum(summary_np[:, 2], cfg.event_cap).astype(np.float64)
     n_me = np.minimum(summary_np[:, 5], cfg.meas_cap).astype(np.float64)
-    return 32.0 + 16.0 * n_ev + 8.0 * n_me
+    return 32.0 + 16.0 * n_ev + (16.0 if acc else 8.0) * n_me
 
 
 SETTLE_S = 0.3
@@ -397,6 +405,8 @@ def compact_leg(res):
         c['serial_ms'] = _sig(res['serial_ms_per_step'])
     if 'pipelined_ms_per_step' in res:
         c['pipe_ms'] = _sig(res['pipelined_ms_per_step'])
+    if 'model_cost' in res:
+        c['cost_x'] = _sig(res['model_cost']['kernel_ratio'], 3)
     if 'cpu_baseline' in res:
         c['cpu'] = _sig(res['cpu_baseline']['value'], 3)
         if 'all_cores' in res['cpu_baseline']:
@@ -554,8 +564,8 @@ def leg_dds(emu, args, world, rank, stream):
     pipe_ms = None
     if args.dds_depth > 1:
         # opt-in: `dds_depth` batches in flight on as many contexts / streams
-        # (dds.SynthesisPipeline); the leg reports whichever of the two
-        # measured faster, both on the line
+        # (dds.SynthesisPipeline); the flag, not the faster measurement, picks
+        # the reported mode (no best-of-two bias), both on the line
         pipe = SynthesisPipeline(torch.cuda.current_device(), depth=args.dds_depth, streams=args.pipe_streams)
         last = {}
 
@@ -568,8 +578,7 @@ def leg_dds(emu, args, world, rank, stream):
         assert torch.equal(last['iq'], iq), 'config 5: pipelined and serial I/Q differ'
         pipe.close()
         pipe_ms = dt_pipe / args.steps * 1e3
-        if dt_pipe < dt_serial:
-            dt, mode = dt_pipe, 'pipelined'
+        dt, mode = dt_pipe, 'pipelined'
     samples = plan.n_channels * n_samples
     ms_step = dt / args.steps * 1e3
     prof = pmc('dds') if args.dds_seqs == 128 else None
@@ -579,11 +588,12 @@ def leg_dds(emu, args, world, rank, stream):
     res = {'metric': 'DDS I/Q GSamples/s (config 5: RB timelines, 16 channels/sequence, 16 samples/clk)',
            'value': samples * world * args.steps / dt / 1e9, 'unit': 'GSamples/s', 'ms_per_step': ms_step,
            'kernel_ms': kernel_ms, 'dtype': 'int16 I/Q',
-           'step': 'dds_index_kernel (per-channel event index + tile windows) + dds_tile_kernel per batch on one '
-                   'stream ({}); kernel_ms and the roofline hold dds_tile_kernel alone, value and ms_per_step the '
-                   'whole step'.format('serial' if args.dds_depth <= 1 else
-                                       'serial and {} batches in flight measured, the faster reported'.format(
-                                           args.dds_depth)),
+           'step': 'dds_index_kernel (per-channel event index and counts; each tile\'s window found in the '
+                   'tile kernel) + dds_tile_kernel per batch on one stream ({}); kernel_ms and the roofline hold '
+                   'dds_tile_kernel alone, value and ms_per_step the whole step'.format(
+                       'serial' if args.dds_depth <= 1 else
+                       '{} batches in flight reported (--dds-depth), the serial step measured beside it'.format(
+                           args.dds_depth)),
            'step_mode': mode, 'batches_in_flight': args.dds_depth if mode == 'pipelined' else 1,
            'step_roofline_frac': samples * 4 / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
            'serial_ms_per_step': dt_serial / args.steps * 1e3,
@@ -611,23 +621,30 @@ def leg_dds(emu, args, world, rank, stream):
     return res
 
 
-def leg_active_reset(emu, args, world, rank, stream, lut=False):
+def leg_active_reset(emu, args, world, rank, stream, lut=False, demod=False):
     """config 3 (BASELINE configs[2]): 8-core active reset -- readout,
     fproc_meas branch to a conditional X180, sync barriers -- 10^7 shots per
     step over 8 GPUs, i.e. 1.25*10^6 shots per GPU (weak).  lut: the same
     circuit through the fproc_lut back end (workloads.config3_lut: every core
-    waits on a syndrome LUT over all 8 measurements, hdl/fproc_lut.sv)"""
+    waits on a syndrome LUT over all 8 measurements, hdl/fproc_lut.sv).
+    demod: the same circuit with the readout demodulation model
+    (workloads.config3_demod: the rdlo window demodulates the rdrv return,
+    the accumulated I/Q of every readout is an output, a per-core
+    discriminator decides; meas_valid at the same cycles as the STATE leg)"""
     import torch
     from distributed_processor_amd import _abi, sharding, workloads
     from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
     ps = ProgramSet(workloads.config3_lut(8) if lut else workloads.config3_active_reset(8))
     emu.load(ps)
     lut_kw = dict(fproc_mode=_abi.FPROC_LUT, lut_mask=0xFF, lut_table=workloads.config3_lut_table(8)) if lut else {}
+    if demod:
+        lut_kw = dict(demod=workloads.config3_demod(ps))
     cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=50000, event_cap=16, trace_cap=0, meas_cap=4,
-                           meas_latency=workloads.CONFIG3_MEAS_LATENCY, seed=0x5EED, p1=0.5, hist_assign=True,
+                           meas_latency=workloads.CONFIG3_DEMOD_LATENCY if demod else workloads.CONFIG3_MEAS_LATENCY,
+                           seed=0x5EED, p1=0.5, hist_assign=True,
                            lane_order=_abi.LANES_SHOT_MAJOR, **lut_kw)   # whole-line event stores (DESIGN.md §3)
     shot0, n = sharding.weak_shard(args.ar_shots, rank)
-    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist'))
+    out = alloc_device_outputs(cfg, n, want=('summary', 'events', 'meas', 'hist') + (('acc',) if demod else ()))
     pipe = sharding.HistogramPipeline(out['hist'], zero=False)     # each run assigns its histogram
 
     def launch(h):
@@ -641,26 +658,38 @@ def leg_active_reset(emu, args, world, rank, stream, lut=False):
     s = _abi.unpack_summary(summ)
     assert (s['status'] == _abi.ST_DONE).all(), 'config 3: not every lane reached DONE'
     assert int(pipe.result().sum().item()) == n * world
-    alg = float(bytes_per_lane(summ, cfg).sum())
-    prof = pmc('lut' if lut else 'active_reset') if args.ar_shots == 1250000 else None
+    alg = float(bytes_per_lane(summ, cfg, acc=demod).sum())
+    pname = 'lut' if lut else 'demod' if demod else 'active_reset'
+    prof = pmc(pname) if args.ar_shots == 1250000 else None
     ms_step = dt / args.steps * 1e3
     roof = hbm_roofline(alg, kernel_ms, ms_step, 'dpemu::' + kernel, prof, 'branch_kernel')
     roof['kernel_ms_block'] = kernel_ms_blk
     roof['valu'] = valu_view(prof, roof['kernel_ms'], float(s['n_instr'].astype(np.float64).sum()))
     res = {'metric': ('emulated core-shots/s (config 3 via the fproc_lut back end: syndrome LUT over 8 '
                       'measurements + sync, 1.25e6 shots/GPU)') if lut else
+                     ('emulated core-shots/s (config 3 with the readout demodulation model: rdrv return x rdlo '
+                      'LO accumulated per readout, per-core discriminator, 1.25e6 shots/GPU)') if demod else
                      ('emulated core-shots/s (config 3: 8-core active reset, fproc_meas branch + sync, '
                       '1.25e6 shots/GPU)'),
            'value': n * 8 * world * args.steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * args.steps / dt,
            'ms_per_step': ms_step, 'kernel_ms': kernel_ms,
            'instructions_per_s': float(s['n_instr'].astype(np.float64).sum()) * world * args.steps / dt,
            'kernel': kernel,
-           'config': {'workload': 'config3_lut_8core' if lut else 'config3_active_reset_8core', 'shots_per_gpu': n,
+           'config': {'workload': 'config3_lut_8core' if lut else 'config3_demod_8core' if demod else
+                      'config3_active_reset_8core', 'shots_per_gpu': n,
                       'global_shots_per_step': n * world,
                       'lane_order': LANE_ORDER_NAMES[cfg.lane_order]},
            'roofline': roof}
+    if demod:
+        # the first readout's assignment against the prepared state (Philox word 0 of (shot, core, 0))
+        import oracle
+        st = np.array([[oracle.lib().oracle_philox_u32(0x5EED, int(shot0 + i), c, 0) < (1 << 31)
+                        for c in range(8)] for i in range(2048)])
+        res['assignment_fidelity'] = float(((s['meas_bits'][:2048 * 8] & 1).reshape(2048, 8) == st).mean())
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res['cpu_baseline'] = cpu_baselines(ps, cfg, 8192, 'config 3 ' + ('syndrome LUT' if lut else 'active reset'))
+        res['cpu_baseline'] = cpu_baselines(ps, cfg, 8192, 'config 3 ' + ('syndrome LUT' if lut else
+                                                                         'demod readout' if demod else 'active reset'),
+                                            ro=ps.readout_freqs(cfg.ro_drv_elem, cfg.meas_elem) if demod else None)
     del out
     torch.cuda.empty_cache()
     return res
@@ -708,8 +737,8 @@ def leg_rb(emu, args, world, rank, stream):
     if depth > 1:
         # opt-in: `rb_depth` batches in flight on as many contexts / streams
         # (emulator.RunPipeline: the next batch's waves fill the CUs this
-        # batch's tail of long sequences leaves idle); the faster of the two
-        # is the leg's value, both on the line
+        # batch's tail of long sequences leaves idle); the flag picks the
+        # reported mode, both on the line
         rp = RunPipeline(ps, cfg, n, want=want, depth=depth, device=torch.cuda.current_device(), first=emu,
                          streams=args.pipe_streams)
         hp = sharding.HistogramPipeline(rp.outputs[0]['hist'], n_buffers=max(2, depth))
@@ -725,8 +754,7 @@ def leg_rb(emu, args, world, rank, stream):
         rp.close()
         del rp
         pipe_ms = dt_pipe / steps * 1e3
-        if dt_pipe < dt_serial:
-            dt, mode = dt_pipe, 'pipelined'
+        dt, mode = dt_pipe, 'pipelined'
     summ = out['summary'].cpu().numpy().view(np.uint32)
     if s_pipe is not None:
         assert np.array_equal(summ, s_pipe.view(np.uint32)), 'config 4: pipelined and serial batches differ'
@@ -779,18 +807,18 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
     ap.add_argument('--dds-depth', type=int, default=2,
-                    help='DDS batches in flight (> 1: dds.SynthesisPipeline, measured beside the serial step and '
-                         'reported only when faster, both on the line; 1: serial only).  Default 2: the next '
-                         'batch\'s index kernel runs beside this batch\'s tiles (profiles/r05_dds_depth.json: '
-                         '0.312 vs 0.327 ms); the round-4 default of 8 was slower than serial on the driver\'s box')
+                    help='DDS batches in flight (> 1: dds.SynthesisPipeline reported, the serial step measured '
+                         'beside it; 1: serial only).  Default 2: the next batch\'s index kernel runs beside this '
+                         'batch\'s tiles (profiles/r05_dds_depth.json: 0.312 vs 0.327 ms)')
     ap.add_argument('--rb-depth', type=int, default=1,
-                    help='config-4 batches in flight (opt-in, > 1: emulator.RunPipeline, measured beside the '
-                         'serial step and reported only when faster)')
+                    help='config-4 batches in flight (opt-in, > 1: emulator.RunPipeline, reported with the serial '
+                         'step measured beside it)')
     ap.add_argument('--ar-shots', type=int, default=1250000, help='config-3 shots per GPU per step')
     ap.add_argument('--rb-seqs', type=int, default=100000, help='config-4 RB sequences')
     ap.add_argument('--rb-spg', type=int, default=10, help='config-4 shots per sequence')
     ap.add_argument('--c1-shots', type=int, default=10 ** 6, help='config-1 shots per GPU per step')
-    ap.add_argument('--legs', default='config1,dds,active_reset,lut,rb', help='sub-legs to run (comma list; "" for none)')
+    ap.add_argument('--legs', default='config1,dds,active_reset,demod,lut,rb',
+                    help='sub-legs to run (comma list; "" for none)')
     args = ap.parse_args()
 
     import torch
@@ -835,9 +863,18 @@ def main():
         if k in main_leg:
             result[k] = main_leg[k]
     fns = {'config1': leg_config1, 'dds': leg_dds, 'active_reset': leg_active_reset, 'rb': leg_rb,
-           'lut': lambda *a: leg_active_reset(*a, lut=True)}
+           'lut': lambda *a: leg_active_reset(*a, lut=True), 'demod': lambda *a: leg_active_reset(*a, demod=True)}
     for name in [x for x in args.legs.split(',') if x]:
         result[name] = fns[name](emu, args, world, rank, stream)
+    if 'demod' in result and 'active_reset' in result:
+        # the demodulation model's own cost: the same circuit, shots and launch
+        # shape as the STATE leg, so the kernel-time ratio is the model's price
+        a, d = result['active_reset'], result['demod']
+        d['model_cost'] = {'kernel_ms_state': a['kernel_ms'], 'kernel_ms_demod': d['kernel_ms'],
+                           'kernel_ratio': d['kernel_ms'] / a['kernel_ms'],
+                           'step_ratio': d['ms_per_step'] / a['ms_per_step'],
+                           'extra_bytes_per_launch': d['roofline']['bytes_per_launch'] -
+                           a['roofline']['bytes_per_launch']}
     result['box'] = {'fill_GBps': fill_gbps(), 'device': torch.cuda.get_device_name(local)}
     # LAST on the line: one compact record per leg, so that a reader who keeps
     # only the tail of the line (the driver stores ~8 KB) still has every

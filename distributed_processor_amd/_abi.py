@@ -4,14 +4,15 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_CORES = 64
 MEAS_LOOKUP = 16     # measurements per core visible to fproc reads
 
 ST_DONE, ST_MAX_CYCLES, ST_HUNG_OPCODE, ST_DEADLOCK = 1, 2, 3, 4
 F_LATE, F_EVENT_OVF, F_TRACE_OVF, F_MEAS_OVF, F_DOUBLE_STROBE, F_GUARD = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 FPROC_MEAS, FPROC_LUT = 0, 1
-MEAS_STATE, MEAS_READOUT = 0, 1
+MEAS_STATE, MEAS_READOUT, MEAS_DEMOD = 0, 1, 2
+RO_CPW_MAX = 8
 LANES_CORE_MAJOR, LANES_SHOT_MAJOR = 0, 1
 EV_STROBE, EV_PULSE_RESET = 0, 1
 TRACE_QCLK_LOAD, TRACE_QCLK_RST = 16, 17
@@ -38,13 +39,15 @@ class Config(C.Structure):
                 ('lut_mask', C.c_uint32), ('meas_model', C.c_uint32),
                 ('p1_threshold', C.c_uint32 * MAX_CORES), ('lut_table', C.c_uint64 * 256),
                 ('ro_sep', C.c_int32), ('ro_sigma', C.c_uint32), ('ro_thr', C.c_int32),
-                ('ro_win', C.c_uint32), ('hist_assign', C.c_uint32), ('lane_order', C.c_uint32)]
+                ('ro_win', C.c_uint32), ('hist_assign', C.c_uint32), ('lane_order', C.c_uint32),
+                ('ro_drv_elem', C.c_uint32), ('ro_cpw', C.c_uint32), ('ro_delay', C.c_uint32),
+                ('ro_theta', C.c_uint32 * 2), ('ro_gain', C.c_uint32 * 2), ('ro_axis', C.c_uint32 * MAX_CORES)]
 
 
 class Outputs(C.Structure):
     _fields_ = [('summary', C.c_void_p), ('events', C.c_void_p),
                 ('trace', C.c_void_p), ('meas', C.c_void_p), ('regs', C.c_void_p),
-                ('hist', C.c_void_p), ('hist_next', C.c_void_p)]
+                ('hist', C.c_void_p), ('hist_next', C.c_void_p), ('acc', C.c_void_p)]
 
 
 class DDSChannels(C.Structure):
@@ -60,10 +63,16 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
                 event_cap=64, trace_cap=0, meas_cap=8, fproc_mode=FPROC_MEAS, meas_elem=2,
                 meas_latency=64, sync_latency=1, sync_mask=0, seed=0x5EED, p1=0.5,
                 lut_mask=0b00011, lut_table=DEFAULT_LUT_TABLE, exec_flags=0, readout=None,
-                hist_assign=False, lane_order=LANES_CORE_MAJOR):
+                hist_assign=False, lane_order=LANES_CORE_MAJOR, demod=None):
     """Validated Config.  p1: float or per-core list of P(state = 1).
     readout: None (outcome = prepared state) or dict(sep=, sigma=, thr=) for the
     readout model of include/dpemu.h (sigma a float noise scale, stored Q16).
+    demod: None or dict for the demodulation model (meas_model DEMOD,
+    include/dpemu.h; meas_elem is the LO element): drv_elem, cpw (clocks per
+    env word, default 4), delay (clocks), theta=(state-0, state-1 return
+    phase, radians), gain=(state-0, state-1 amplitude, <= 1.0), axis (radians,
+    one or per core: the discriminator direction), sigma (noise scale of the
+    accumulated value, float; stored Q16), thr (int).
     hist_assign: a run writes its outcome histogram instead of adding to it.
     lane_order: LANES_CORE_MAJOR (lane = core * n_shots + shot) or
     LANES_SHOT_MAJOR (lane = shot * C + core)."""
@@ -116,6 +125,50 @@ def make_config(cores_per_shot, n_groups=1, shots_per_group=1, max_cycles=1 << 2
         if not 0 <= win < 2 ** 12:
             raise ValueError('readout win must fit the 12-bit envelope-length field')
         cfg.ro_win = win
+    if demod is not None:
+        if readout is not None:
+            raise ValueError('readout and demod are exclusive measurement models')
+        set_demod(cfg, **demod)
+    return cfg
+
+
+def phase_u32(rad):
+    """a phase in radians as the model's 32-bit phase (2^32 = 2 pi)"""
+    return int(round(float(rad) / (2 * np.pi) * 2 ** 32)) & 0xFFFFFFFF
+
+
+def axis_word(rad):
+    """discriminator axis word: Q15 cos | Q15 sin << 16 (include/dpemu.h ro_axis)"""
+    i = max(-32768, min(32767, int(round(np.cos(rad) * 32767))))
+    q = max(-32768, min(32767, int(round(np.sin(rad) * 32767))))
+    return (i & 0xFFFF) | ((q & 0xFFFF) << 16)
+
+
+def set_demod(cfg, drv_elem=1, cpw=4, delay=0, theta=(0.0, np.pi), gain=(1.0, 1.0), axis=0.0, sigma=0.0, thr=0):
+    """switch cfg to meas_model DEMOD (see make_config)"""
+    if not 0 <= int(drv_elem) <= 3 or int(drv_elem) == cfg.meas_elem:
+        raise ValueError('demod drv_elem must be an element 0..3 other than meas_elem')
+    if not 1 <= int(cpw) <= RO_CPW_MAX:
+        raise ValueError('demod cpw must be in [1, {}]'.format(RO_CPW_MAX))
+    if not 0 <= int(delay) < 2 ** 20:
+        raise ValueError('demod delay must be in [0, 2^20)')
+    sig = int(round(float(sigma) * 65536))
+    if not 0 <= sig < 2 ** 24:
+        raise ValueError('demod sigma * 2^16 must be < 2^24')
+    if not -2 ** 31 <= int(thr) < 2 ** 31:
+        raise ValueError('demod thr must fit int32')
+    cfg.meas_model = MEAS_DEMOD
+    cfg.ro_drv_elem, cfg.ro_cpw, cfg.ro_delay = int(drv_elem), int(cpw), int(delay)
+    for s_ in (0, 1):
+        g = int(round(float(gain[s_]) * 65536))
+        if not 0 <= g <= 65536:
+            raise ValueError('demod gain must be in [0, 1]')
+        cfg.ro_gain[s_] = g
+        cfg.ro_theta[s_] = phase_u32(theta[s_])
+    axes = list(axis) if isinstance(axis, (list, tuple, np.ndarray)) else [axis] * MAX_CORES
+    for c in range(MAX_CORES):
+        cfg.ro_axis[c] = axis_word(axes[c] if c < len(axes) else 0.0)
+    cfg.ro_sigma, cfg.ro_thr = sig, int(thr)
     return cfg
 
 
@@ -128,7 +181,7 @@ def prob_to_threshold(p):
     return min(int(round(p * 2 ** 32)), 0xFFFFFFFE)
 
 
-OUTPUT_NAMES = ('summary', 'events', 'trace', 'meas', 'regs', 'hist', 'hist_next')
+OUTPUT_NAMES = ('summary', 'events', 'trace', 'meas', 'regs', 'hist', 'hist_next', 'acc')
 
 
 def lane_index(shot_local, core, n_shots, cores_per_shot=None, lane_order=LANES_CORE_MAJOR):
@@ -164,6 +217,8 @@ def alloc_host_outputs(cfg, n_shots, want=OUTPUT_NAMES):
         out['trace'] = np.zeros((cfg.trace_cap, n_lanes, 4), np.uint32)
     if 'meas' in want and cfg.meas_cap:
         out['meas'] = np.zeros((cfg.meas_cap, n_lanes, 2), np.uint32)
+    if 'acc' in want and cfg.meas_cap and cfg.meas_model == MEAS_DEMOD:
+        out['acc'] = np.zeros((cfg.meas_cap, n_lanes, 2), np.int32)
     if 'regs' in want:
         out['regs'] = np.zeros((16, n_lanes), np.uint32)
     if 'hist' in want and cfg.cores_per_shot <= 12:

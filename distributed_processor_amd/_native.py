@@ -9,7 +9,7 @@ LIB_PATH = os.path.join(HERE, 'libdpemu.so')
 
 # every entry point declared in include/dpemu.h
 EXPORTS = ('dpemu_abi_version', 'dpemu_struct_sizes', 'dpemu_create', 'dpemu_destroy', 'dpemu_last_error',
-           'dpemu_load_programs', 'dpemu_run', 'dpemu_run_host', 'dpemu_dds', 'dpemu_dds_sin_lut',
+           'dpemu_load_programs', 'dpemu_load_readout_freqs', 'dpemu_run', 'dpemu_run_host', 'dpemu_dds', 'dpemu_dds_sin_lut',
            'dpemu_set_kernel_timing', 'dpemu_kernel_times', 'dpemu_last_kernel')
 
 _libs = {}
@@ -50,6 +50,7 @@ def load_library(path=LIB_PATH):
     L.dpemu_last_error.argtypes = [vp]
     L.dpemu_last_error.restype = C.c_char_p
     L.dpemu_load_programs.argtypes = [vp, vp, u64, vp, vp, u32, vp, u32, u32]
+    L.dpemu_load_readout_freqs.argtypes = [vp, vp, u64, vp, vp, vp, vp]
     L.dpemu_run.argtypes = [vp, vp, u64, u64, vp, vp]
     L.dpemu_run_host.argtypes = [vp, vp, u64, u64, vp]
     L.dpemu_dds.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]

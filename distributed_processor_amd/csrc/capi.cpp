@@ -59,7 +59,10 @@ struct dpemu_ctx {
     uint32_t reg_used = 0xFFFFu;
     uint32_t max_len = 0;              // longest program (commands)
     std::vector<uint64_t> group_len;   // instructions of all C programs of each group
-    // run constants
+    // DEMOD frequency tables (dpemu_load_readout_freqs), per loaded program
+    uint32_t *d_ro_fq = nullptr;
+    uint4 *d_ro_hdr = nullptr;
+    // run constants: p1 thresholds [64] then DEMOD axes [64]
     uint32_t *d_thr = nullptr;
     uint64_t *d_lut = nullptr;
     std::vector<uint32_t> thr_cache;
@@ -323,6 +326,10 @@ static void free_programs(dpemu_ctx *ctx)
     ctx->d_mchunk = ctx->d_mcoff = nullptr;
     ctx->d_moff = ctx->d_offsets = ctx->d_ninstr = ctx->d_table = nullptr;
     ctx->n_programs = 0;
+    (void)hipFree(ctx->d_ro_fq);
+    (void)hipFree(ctx->d_ro_hdr);
+    ctx->d_ro_fq = nullptr;
+    ctx->d_ro_hdr = nullptr;
 }
 
 extern "C" {
@@ -352,7 +359,7 @@ int dpemu_create(int device, dpemu_ctx **out)
         ctx->n_cu = (uint32_t)cus;
     std::vector<int16_t> lut(4096);
     dpemu_dds_sin_lut(lut.data());
-    if (hipMalloc(&ctx->d_thr, DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
+    if (hipMalloc(&ctx->d_thr, 2 * DPEMU_MAX_CORES * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&ctx->d_lut, 256 * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&ctx->d_sin, 4096 * sizeof(int16_t)) != hipSuccess ||
         hipMemcpy(ctx->d_sin, lut.data(), 4096 * sizeof(int16_t), hipMemcpyHostToDevice) != hipSuccess ||
@@ -525,6 +532,33 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, 
     return DPEMU_OK;
 }
 
+int dpemu_load_readout_freqs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words, const uint32_t *drv_off,
+                             const uint32_t *drv_len, const uint32_t *lo_off, const uint32_t *lo_len)
+{
+    if (!ctx) return DPEMU_E_INVALID;
+    if (!ctx->n_programs) return fail(ctx, DPEMU_E_NOPROG, "load_readout_freqs before load_programs");
+    if ((!words && n_words) || !drv_off || !drv_len || !lo_off || !lo_len)
+        return fail(ctx, DPEMU_E_INVALID, "load_readout_freqs: null array");
+    std::vector<uint32_t> hdr(4ull * ctx->n_programs);
+    for (uint32_t i = 0; i < ctx->n_programs; i++) {
+        if ((uint64_t)drv_off[i] + drv_len[i] > n_words || (uint64_t)lo_off[i] + lo_len[i] > n_words)
+            return fail(ctx, DPEMU_E_INVALID, "load_readout_freqs: program %u's table runs past the %llu words", i,
+                        (unsigned long long)n_words);
+        hdr[4 * i] = drv_off[i]; hdr[4 * i + 1] = drv_len[i]; hdr[4 * i + 2] = lo_off[i]; hdr[4 * i + 3] = lo_len[i];
+    }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (ctx->ord_valid) HIPCHK(ctx, hipEventSynchronize(ctx->ord_ev));   // earlier runs may still read the old tables
+    (void)hipFree(ctx->d_ro_fq);
+    (void)hipFree(ctx->d_ro_hdr);
+    ctx->d_ro_fq = nullptr;
+    ctx->d_ro_hdr = nullptr;
+    HIPCHK(ctx, hipMalloc(&ctx->d_ro_fq, std::max<uint64_t>(n_words, 1) * 4));
+    if (n_words) HIPCHK(ctx, hipMemcpy(ctx->d_ro_fq, words, n_words * 4, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMalloc(&ctx->d_ro_hdr, hdr.size() * 4));
+    HIPCHK(ctx, hipMemcpy(ctx->d_ro_hdr, hdr.data(), hdr.size() * 4, hipMemcpyHostToDevice));
+    return DPEMU_OK;
+}
+
 static int validate(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t n_shots, bool want_hist)
 {
     if (!cfg) return fail(ctx, DPEMU_E_INVALID, "null config");
@@ -540,8 +574,23 @@ static int validate(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t n_shots, b
     if (cfg->meas_latency < 1 || cfg->meas_latency > (1u << 20) || cfg->sync_latency < 1 ||
         cfg->sync_latency > (1u << 20))
         return fail(ctx, DPEMU_E_INVALID, "meas_latency / sync_latency must be in [1, 2^20]");
-    if (cfg->meas_model != DPEMU_MEAS_STATE && cfg->meas_model != DPEMU_MEAS_READOUT)
-        return fail(ctx, DPEMU_E_INVALID, "meas_model must be DPEMU_MEAS_STATE or DPEMU_MEAS_READOUT");
+    if (cfg->meas_model > DPEMU_MEAS_DEMOD)
+        return fail(ctx, DPEMU_E_INVALID, "meas_model must be DPEMU_MEAS_STATE, _READOUT or _DEMOD");
+    if (cfg->meas_model == DPEMU_MEAS_DEMOD) {
+        if (cfg->ro_drv_elem > 3 || cfg->ro_drv_elem == cfg->meas_elem)
+            return fail(ctx, DPEMU_E_INVALID, "ro_drv_elem %u must be an element 0..3 other than meas_elem",
+                        cfg->ro_drv_elem);
+        if (cfg->ro_cpw < 1 || cfg->ro_cpw > DPEMU_RO_CPW_MAX)
+            return fail(ctx, DPEMU_E_INVALID, "ro_cpw %u not in [1, %u]", cfg->ro_cpw, DPEMU_RO_CPW_MAX);
+        if (cfg->ro_delay >= (1u << 20)) return fail(ctx, DPEMU_E_INVALID, "ro_delay must be < 2^20");
+        if (cfg->ro_gain[0] > 65536 || cfg->ro_gain[1] > 65536)
+            return fail(ctx, DPEMU_E_INVALID, "ro_gain must be <= 65536 (1.0 in Q16)");
+        if (cfg->ro_sigma >= (1u << 24)) return fail(ctx, DPEMU_E_INVALID, "DEMOD: ro_sigma must be < 2^24");
+        if ((uint64_t)cfg->max_cycles + cfg->meas_latency + 4096ull * DPEMU_RO_CPW_MAX + 64 >= 0x80000000ull)
+            return fail(ctx, DPEMU_E_INVALID, "max_cycles + meas_latency + the readout window must stay below 2^31");
+        if (!ctx->d_ro_hdr)
+            return fail(ctx, DPEMU_E_INVALID, "DEMOD run without readout frequency tables (dpemu_load_readout_freqs)");
+    }
     if (cfg->hist_assign > 1) return fail(ctx, DPEMU_E_INVALID, "hist_assign must be 0 or 1");
     if (cfg->lane_order > DPEMU_LANES_SHOT_MAJOR)
         return fail(ctx, DPEMU_E_INVALID, "lane_order %u is not DPEMU_LANES_CORE_MAJOR / SHOT_MAJOR", cfg->lane_order);
@@ -570,6 +619,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     // run constants, uploaded when they change (stream-ordered: the copy lands
     // before this call's kernel and after the previous call's)
     std::vector<uint32_t> thr(cfg->p1_threshold, cfg->p1_threshold + DPEMU_MAX_CORES);
+    thr.insert(thr.end(), cfg->ro_axis, cfg->ro_axis + DPEMU_MAX_CORES);   // d_thr[64..127]: DEMOD axes
     std::vector<uint64_t> lut(cfg->lut_table, cfg->lut_table + 256);
     if (thr != ctx->thr_cache) {
         ctx->thr_cache = thr;
@@ -624,6 +674,12 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.meas_model = cfg->meas_model; p.ro_sep = cfg->ro_sep; p.ro_thr = cfg->ro_thr; p.ro_sigma = cfg->ro_sigma;
     p.ro_win = cfg->ro_win;
     p.ro_wrecip = cfg->ro_win ? (1u << 24) / cfg->ro_win : 0u;
+    p.ro_drv_elem = cfg->ro_drv_elem; p.ro_cpw = cfg->ro_cpw; p.ro_delay = cfg->ro_delay;
+    p.ro_theta0 = cfg->ro_theta[0]; p.ro_theta1 = cfg->ro_theta[1];
+    p.ro_gain0 = cfg->ro_gain[0]; p.ro_gain1 = cfg->ro_gain[1];
+    p.ro_axis = ctx->d_thr + DPEMU_MAX_CORES;
+    p.ro_fq = ctx->d_ro_fq; p.ro_hdr = ctx->d_ro_hdr;
+    p.acc = reinterpret_cast<int2 *>(out->acc);
     p.lut_mask = cfg->lut_mask;
     const uint64_t guard = (uint64_t)C * (cfg->max_cycles / 3u + 4u) + 1024u;
     p.iter_guard = guard > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)guard;
@@ -664,8 +720,11 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     const uint64_t blocks = ((uint64_t)p.n_lanes + BLOCK - 1) / BLOCK;
     const bool small = blocks <= 4 * 256;
     const int fetch_batch = small ? 4 : 1;
-    const bool uniform = ctx->straight && ctx->max_len < 65536u && !(cfg->exec_flags & DPEMU_X_GENERAL);
-    const bool macro = !uniform && ctx->d_macro && !(cfg->exec_flags & (DPEMU_X_GENERAL | DPEMU_X_PROG_LDS));
+    // the DEMOD readout model runs on branch_kernel<FEAT_DEMOD> (or the
+    // general interpreter): the straight / macro kernels do not carry it
+    const bool demod = cfg->meas_model == DPEMU_MEAS_DEMOD;
+    const bool uniform = !demod && ctx->straight && ctx->max_len < 65536u && !(cfg->exec_flags & DPEMU_X_GENERAL);
+    const bool macro = !demod && !uniform && ctx->d_macro && !(cfg->exec_flags & (DPEMU_X_GENERAL | DPEMU_X_PROG_LDS));
     // the staged macro kernel needs at most MACRO_SLOTS distinct programs per
     // wave: (program groups a wave's run of consecutive shots can span) x
     // (cores in the wave), for the thread mapping of block_core_major
@@ -753,7 +812,8 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     // stores, which share vmcnt with global loads on gfx950
     // (DPEMU_X_PROG_MAJOR keeps the global fetch).
     const bool branch = !uniform && !macro && !(cfg->exec_flags & (DPEMU_X_GENERAL | DPEMU_X_PROG_LDS));
-    int bfeat = (feat & (FEAT_FPROC | FEAT_LUT | FEAT_SYNC)) | (ctx->reg_writes ? FEAT_REGS : 0);
+    int bfeat = (feat & (FEAT_FPROC | FEAT_LUT | FEAT_SYNC)) | (ctx->reg_writes ? FEAT_REGS : 0) |
+                (demod ? FEAT_DEMOD : 0);
     if (branch) {
         p.prog_lds_words = 0;
         if (footprint <= BRANCH_LDS_MAX && !(cfg->exec_flags & DPEMU_X_PROG_MAJOR)) {
@@ -805,6 +865,8 @@ int dpemu_run(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin, uint
     if (!out) return fail(ctx, DPEMU_E_INVALID, "null outputs");
     int rc = validate(ctx, cfg, n_shots, out->hist != nullptr || out->hist_next != nullptr);
     if (rc) return rc;
+    if (out->acc && cfg->meas_model != DPEMU_MEAS_DEMOD)
+        return fail(ctx, DPEMU_E_INVALID, "acc: DEMOD runs only");
     if (out->hist_next) {
         const uint64_t bytes = ((uint64_t)cfg->n_groups << cfg->cores_per_shot) * sizeof(uint64_t);
         const uintptr_t a = (uintptr_t)out->hist, b = (uintptr_t)out->hist_next;
@@ -834,17 +896,20 @@ int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
     if (host_out->hist_next) return fail(ctx, DPEMU_E_INVALID, "hist_next: device runs (dpemu_run) only");
     int rc = validate(ctx, cfg, n_shots, host_out->hist != nullptr);
     if (rc) return rc;
+    if (host_out->acc && cfg->meas_model != DPEMU_MEAS_DEMOD)
+        return fail(ctx, DPEMU_E_INVALID, "acc: DEMOD runs only");
     if (n_shots == 0) return DPEMU_OK;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     const uint64_t nl = n_shots * cfg->cores_per_shot;
     struct Buf { void *host; void *dev; size_t bytes; bool in; };
-    Buf bufs[6] = {
+    Buf bufs[7] = {
         {host_out->summary, nullptr, nl * 32, false},
         {host_out->events, nullptr, (size_t)cfg->event_cap * nl * 16, false},
         {host_out->trace, nullptr, (size_t)cfg->trace_cap * nl * 16, false},
         {host_out->meas, nullptr, (size_t)cfg->meas_cap * nl * 8, false},
         {host_out->regs, nullptr, nl * 64, false},
         {host_out->hist, nullptr, (size_t)cfg->n_groups * (cfg->cores_per_shot <= 12 ? (1u << cfg->cores_per_shot) : 0) * 8, true},
+        {host_out->acc, nullptr, (size_t)cfg->meas_cap * nl * 8, false},
     };
     int result = DPEMU_OK;
     for (auto &b : bufs) {
@@ -858,6 +923,7 @@ int dpemu_run_host(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin,
         d.summary = (uint32_t *)bufs[0].dev; d.events = (uint32_t *)bufs[1].dev;
         d.trace = (uint32_t *)bufs[2].dev; d.meas = (uint32_t *)bufs[3].dev;
         d.regs = (uint32_t *)bufs[4].dev; d.hist = (uint64_t *)bufs[5].dev;
+        d.acc = (int32_t *)bufs[6].dev;
         result = run_impl(ctx, cfg, shot_begin, n_shots, &d, nullptr);
         if (result == DPEMU_OK) {
             hipError_t e = hipDeviceSynchronize();

@@ -140,6 +140,11 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
     uint32_t wait_d = 0, status = 0, flags = 0;
     uint32_t n_ev = 0, n_tr = 0, n_meas = 0, n_exec = 0, meas_bits = 0, last_bit = 0;
     uint32_t t_end = 0;
+    // DEMOD (run-time: this kernel is the general path): the latest
+    // readout-drive strobe and pulse_reset, the last meas_valid
+    const bool demod = p.meas_model == DPEMU_MEAS_DEMOD;
+    RoDrive ro_d{0u, 0u, 0u};
+    uint32_t ro_tref = 0, ro_ltv = 0;
     // leader-only meas_lut state
     uint64_t lut_valid = 0, lut_addr = 0;
     uint32_t lut_last_fire = INF32, nfire = 0;
@@ -158,9 +163,23 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
             if (p.events) p.events[(uint64_t)n_ev * n_lanes + lane] = event_record(te, pe, pp, pa, kind);
         } else flags |= F_EVENT_OVF;
         n_ev++;
+        if (demod) {
+            if (kind == 1u) ro_tref = te;
+            if (kind == 0u && ((pe >> 24) & 3u) == p.ro_drv_elem)
+                ro_d = RoDrive{te, pp & 0x03FFFFFFu, (pa & 0xFFFFu) | (((pe >> 12) & 0xFFFu) << 16) | 0x80000000u};
+        }
         if (kind == 0 && p.meas_elem != 0xFFu && ((pe >> 24) & 3u) == p.meas_elem) {
-            const uint32_t bit = meas_bit(p, shot, core, n_meas, thr_core, pa, pe);
-            const uint32_t tv = te + p.meas_latency;
+            uint32_t bit, tv;
+            if (demod) {
+                int2 a;
+                bit = demod_readout(p, shot, core, n_meas, thr_core, prog, te, pe, pp, ro_d, ro_tref, a);
+                tv = demod_valid(p, te, pe, ro_ltv);
+                ro_ltv = tv;
+                if (p.acc && n_meas < p.meas_cap) p.acc[(uint64_t)n_meas * n_lanes + lane] = a;
+            } else {
+                bit = meas_bit(p, shot, core, n_meas, thr_core, pa, pe);
+                tv = te + p.meas_latency;
+            }
             if constexpr (XMEAS) {
                 if (n_meas < MEAS_LOOKUP) s_mt[n_meas < MT ? n_meas : 0][tid] = (tv << 1) | bit;
             }

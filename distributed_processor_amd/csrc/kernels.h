@@ -43,6 +43,7 @@ constexpr int FEAT_LUT = 4;     // fproc_lut back end
 constexpr int FEAT_PROG_LDS = 8; // the workgroup's programs staged in LDS (fits PROG_LDS_MAX)
 constexpr int FEAT_STRAIGHT = 16; // only pulse / idle / done / hang opcodes: no register file
 constexpr int FEAT_REGS = 32;   // branch.hip: some command writes the reg_file (reg_alu / alu_fproc)
+constexpr int FEAT_DEMOD = 64;  // branch.hip: meas_model DPEMU_MEAS_DEMOD (lane.h demod_readout)
 constexpr uint32_t PROG_LDS_MAX = 1024;   // commands (16 KiB) of dynamic LDS per workgroup
 constexpr uint32_t BRANCH_LDS_MAX = 512;  // commands (8 KiB): branch.hip stages its programs up to this
 
@@ -153,6 +154,13 @@ struct KParams {
     uint32_t meas_model;          // DPEMU_MEAS_STATE / DPEMU_MEAS_READOUT (ro_*: include/dpemu.h)
     int32_t ro_sep, ro_thr;
     uint32_t ro_sigma, ro_win, ro_wrecip;   // ro_wrecip = floor(2^24 / ro_win)
+    // DEMOD readout model (lane.h demod_readout): config fields, the per-core
+    // axes, the frequency tables (dpemu_load_readout_freqs) and the acc output
+    uint32_t ro_drv_elem, ro_cpw, ro_delay, ro_theta0, ro_theta1, ro_gain0, ro_gain1;
+    const uint32_t *ro_axis;      // [64] Q15 I | Q << 16
+    const uint32_t *ro_fq;        // frequency words
+    const uint4 *ro_hdr;          // [n_programs] {drv_off, drv_len, lo_off, lo_len}
+    int2 *acc;                    // dpemu_outputs.acc (nullable)
     uint32_t iter_guard;
     uint32_t prog_lds_words;      // dynamic LDS commands (FEAT_PROG_LDS)
     uint32_t *hist_rep;           // [hist_reps][hist_stride] u32 replicas (128-B aligned rows)

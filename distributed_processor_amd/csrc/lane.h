@@ -96,6 +96,106 @@ __device__ __forceinline__ uint32_t meas_bit(const KParams &p, uint64_t shot, ui
     return x > (int64_t)p.ro_thr;
 }
 
+// ---- readout demodulation model (meas_model DPEMU_MEAS_DEMOD) --------------
+// The closed form of include/dpemu.h / DESIGN.md §2, restated for the CPU in
+// oracle/readout.c (that file's header is the normative spec).  Integer
+// arithmetic only; every intermediate is the oracle's value.
+
+// sin(2 pi x / 2^33) * 2^61 (x mod 2^33): quarter-wave reduction, then
+// y * P(y^2) with P the Q30 Taylor polynomial of sin(pi/2 t) / t, t = y / 2^31
+// (each Horner step one v_mad_i64_i32; every P value fits int32)
+__device__ __forceinline__ int64_t sin33(uint64_t x)
+{
+    const uint32_t q = (uint32_t)(x >> 31) & 3u;
+    const uint32_t f = (uint32_t)x & 0x7FFFFFFFu;
+    const uint32_t y = (q & 1u) ? 0x80000000u - f : f;      // <= 2^31
+    const int32_t z = (int32_t)(uint32_t)(((uint64_t)y * y) >> 32);   // t^2, Q30
+    int32_t P = -3864;
+    P = 172272 + (int32_t)(((int64_t)P * z) >> 30);
+    P = -5026995 + (int32_t)(((int64_t)P * z) >> 30);
+    P = 85569306 + (int32_t)(((int64_t)P * z) >> 30);
+    P = -693598668 + (int32_t)(((int64_t)P * z) >> 30);
+    P = 1686629713 + (int32_t)(((int64_t)P * z) >> 30);     // > 0
+    const int64_t s = (int64_t)((uint64_t)y * (uint32_t)P);  // Q61
+    return (q & 2u) ? -s : s;
+}
+
+// sin(n b pi / 2^32) / sin(b pi / 2^32) in Q16, b = (int32) beta, n >= 1: the
+// modulus of the sum of n unit phasors advancing by beta per clock
+__device__ __forceinline__ int64_t dirichlet_q16(uint32_t n, uint32_t beta)
+{
+    const int32_t b = (int32_t)beta;
+    if (b == 0) return (int64_t)n << 16;
+    const int64_t den = sin33((uint64_t)(int64_t)b);
+    const int64_t num = sin33((uint64_t)((int64_t)n * b));
+    uint64_t ad = (uint64_t)(den < 0 ? -den : den), an = (uint64_t)(num < 0 ? -num : num);
+    const int bl = 64 - __clzll((long long)ad);               // ad > 0
+    const int sh = bl > 31 ? bl - 31 : 0;                     // the divisor below 2^31
+    ad >>= sh;
+    an >>= sh;
+    const int64_t qv = (int64_t)((an << 16) / ad);
+    return ((num < 0) != (den < 0)) ? -qv : qv;
+}
+
+// env length field (bits 23:12) in env words, 0 (a CW envelope) = 4096
+__device__ __forceinline__ uint32_t ro_words(uint32_t env) { const uint32_t L = (env >> 12) & 0xFFFu; return L ? L : 4096u; }
+
+// meas_valid of a readout strobe at t_lo after the lane's previous one at
+// last_tv (0: none): its window, then meas_latency, in order
+__device__ __forceinline__ uint32_t demod_valid(const KParams &p, uint32_t t_lo, uint32_t pe, uint32_t last_tv)
+{
+    const uint32_t tv = t_lo + ro_words(pe) * p.ro_cpw + p.meas_latency;
+    return tv > last_tv ? tv : last_tv + 1u;
+}
+
+// the lane's latest readout-drive strobe: its cycle, phase | freq << 17, and
+// amp[15:0] | env length[27:16] | seen[31]
+struct RoDrive {
+    uint32_t t, pp, al;
+};
+
+// outcome of readout m (strobe at t_lo with pulse registers pe / pp) of program
+// `prog`; acc = the accumulated {I, Q}.  t_ref: the lane's latest pulse_reset
+__device__ __forceinline__ uint32_t demod_readout(const KParams &p, uint64_t shot, uint32_t core, uint32_t m,
+                                                  uint32_t thr, uint32_t prog, uint32_t t_lo, uint32_t pe,
+                                                  uint32_t pp, const RoDrive d, uint32_t t_ref, int2 &acc)
+{
+    const uint3 r = philox3(p.seed, shot, core, m);
+    const uint32_t s = (thr == 0xFFFFFFFFu) || (r.x < thr);
+    int64_t sig_i = 0, sig_q = 0;
+    if (d.al >> 31) {
+        const uint32_t n_lo = ro_words(pe) * p.ro_cpw, n_d = ro_words(d.al >> 16 << 12) * p.ro_cpw;
+        const uint32_t r0 = d.t + p.ro_delay;                   // the return starts (< 2^32: t < 2^31)
+        const uint32_t a = max(r0, t_lo), e = min(t_lo + n_lo, r0 + n_d);
+        if (e > a) {
+            const uint32_t n = e - a;
+            const uint4 h = p.ro_hdr[prog];                      // drv_off, drv_len, lo_off, lo_len
+            const uint32_t fi_lo = (pp >> 17) & 0x1FFu, fi_d = (d.pp >> 17) & 0x1FFu;
+            const uint32_t f_lo = fi_lo < h.w ? p.ro_fq[h.z + fi_lo] : 0u;
+            const uint32_t f_d = fi_d < h.y ? p.ro_fq[h.x + fi_d] : 0u;
+            const uint32_t beta = f_d - f_lo;
+            const uint32_t th = s ? p.ro_theta1 : p.ro_theta0;
+            const uint32_t alpha = beta * (a - t_ref) - f_d * p.ro_delay + (((d.pp & 0x1FFFFu) - (pp & 0x1FFFFu)) << 15) + th;
+            const uint32_t gamma = alpha + (uint32_t)(uint64_t)(((int64_t)(n - 1u) * (int32_t)beta) >> 1);
+            const int64_t dq = dirichlet_q16(n, beta);
+            const int64_t c15 = (sin33(((uint64_t)gamma << 1) + 0x80000000ull) + (1ll << 45)) >> 46;
+            const int64_t s15 = (sin33((uint64_t)gamma << 1) + (1ll << 45)) >> 46;
+            const int64_t amp = (int64_t)(((uint64_t)(d.al & 0xFFFFu) * (s ? p.ro_gain1 : p.ro_gain0)) >> 16);
+            const int64_t M = amp * dq;
+            sig_i = (M * c15 + (1ll << 31)) >> 32;
+            sig_q = (M * s15 + (1ll << 31)) >> 32;
+        }
+    }
+    const int32_t u0 = (int32_t)(r.y & 0xFFFFu), u1 = (int32_t)(r.y >> 16);
+    const int32_t u2 = (int32_t)(r.z & 0xFFFFu), u3 = (int32_t)(r.z >> 16);
+    const int64_t zi = u0 + u1 - u2 - u3, zq = u0 - u1 + u2 - u3;
+    acc.x = (int32_t)(sig_i + ((zi * (int64_t)p.ro_sigma) >> 16));
+    acc.y = (int32_t)(sig_q + ((zq * (int64_t)p.ro_sigma) >> 16));
+    const uint32_t ax = p.ro_axis[core];
+    const int64_t x = ((int64_t)acc.x * (int16_t)(ax & 0xFFFFu) + (int64_t)acc.y * (int16_t)(ax >> 16)) >> 15;
+    return x > (int64_t)p.ro_thr;
+}
+
 __device__ __forceinline__ uint64_t group_bits(uint64_t ballot, uint32_t lane_in_wave, uint32_t C)
 {
     const uint32_t base = lane_in_wave & ~(C - 1);

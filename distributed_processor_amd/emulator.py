@@ -131,6 +131,37 @@ class ProgramSet:
     def n_programs(self):
         return len(self.n_instr)
 
+    def readout_freqs(self, drv_elem: int, lo_elem: int):
+        """The DEMOD readout model's frequency tables (dpemu_load_readout_freqs):
+        per program, word 0 of every entry of the readout drive element's and
+        the LO element's freq_buffer (f / f_clk * 2^32, asmparse.py:64-86), from
+        the assembler buffers of a (group, core) that runs it.  Returns (words,
+        drv_off, drv_len, lo_off, lo_len); a program without buffers gets empty
+        tables (its frequency words read 0)."""
+        owner = {}
+        for i, pr in enumerate(self.table):
+            owner.setdefault(int(pr), (i // self.cores_per_shot, i % self.cores_per_shot))
+        words, cache = [], {}
+        off = np.zeros((2, self.n_programs), np.uint32)
+        ln = np.zeros((2, self.n_programs), np.uint32)
+        n = 0
+        for pr in range(self.n_programs):
+            b = self.buffers.get(owner[pr]) if pr in owner else None
+            for k, e in enumerate((drv_elem, lo_elem)):
+                f = b[1][e] if b is not None and e < len(b[1]) else np.zeros(0, np.uint32)
+                key = (id(f), k) if len(f) else None
+                if key is not None and key in cache:
+                    off[k, pr], ln[k, pr] = cache[key]
+                    continue
+                fw = np.asarray(f, np.uint32)[0::16]
+                off[k, pr], ln[k, pr] = n, len(fw)
+                if key is not None:
+                    cache[key] = (n, len(fw))
+                words.append(fw)
+                n += len(fw)
+        w = np.concatenate(words).astype(np.uint32) if n else np.zeros(0, np.uint32)
+        return w, off[0], ln[0], off[1], ln[1]
+
 
 class EmulationResult:
     """Host copies of a run's outputs (layouts as in include/dpemu.h)."""
@@ -195,6 +226,7 @@ class Emulator:
         self.device = device
         self.lib_path = lib_path          # None: the in-tree build
         self.programs: Optional[ProgramSet] = None
+        self._ro_key = None               # (drv_elem, lo_elem) of the loaded DEMOD tables
 
     def close(self):
         if getattr(self, '_h', None):
@@ -240,7 +272,31 @@ class Emulator:
                                          ps.n_groups, ps.cores_per_shot)
         check(self._h, rc, 'dpemu_load_programs', self._L)
         self.programs = ps
+        self._ro_key = None                                 # load_programs clears the DEMOD tables
         return ps
+
+    def load_readout_freqs(self, drv_elem: int, lo_elem: int, tables=None):
+        """dpemu_load_readout_freqs: the DEMOD model's per-program frequency
+        words -- ``tables`` = (words, drv_off, drv_len, lo_off, lo_len), default
+        ProgramSet.readout_freqs(drv_elem, lo_elem) of the loaded programs"""
+        if self.programs is None:
+            raise DpemuError('load() programs first')
+        t = tables if tables is not None else self.programs.readout_freqs(drv_elem, lo_elem)
+        w = np.ascontiguousarray(t[0], np.uint32)
+        arrs = [np.ascontiguousarray(a, np.uint32) for a in t[1:5]]
+        if any(len(a) != self.programs.n_programs for a in arrs):
+            raise DpemuError('readout tables need one entry per loaded program')
+        rc = self._L.dpemu_load_readout_freqs(self._h, w.ctypes.data if len(w) else None, len(w),
+                                              *[a.ctypes.data for a in arrs])
+        check(self._h, rc, 'dpemu_load_readout_freqs', self._L)
+        self._ro_key = (int(drv_elem), int(lo_elem)) if tables is None else ('caller', id(tables))
+
+    def _demod_tables(self, cfg):
+        """a DEMOD run reads the loaded programs' own frequency tables unless the
+        caller loaded others"""
+        if cfg.meas_model == _abi.MEAS_DEMOD and (self._ro_key is None or (
+                self._ro_key[0] != 'caller' and self._ro_key != (cfg.ro_drv_elem, cfg.meas_elem))):
+            self.load_readout_freqs(cfg.ro_drv_elem, cfg.meas_elem)
 
     def config(self, **kw) -> _abi.Config:
         if self.programs is None:
@@ -254,6 +310,7 @@ class Emulator:
             **cfg_kw) -> EmulationResult:
         """Emulate shots [shot_begin, shot_begin + n_shots); results copied to host."""
         cfg = cfg or self.config(**cfg_kw)
+        self._demod_tables(cfg)
         want = set(outputs) | {'summary'}
         arrays = _abi.alloc_host_outputs(cfg, n_shots, want)
         o = _abi.outputs_struct(arrays)
@@ -276,6 +333,7 @@ class Emulator:
             if t is not None:
                 _check_tensor(name, t, want[name], self.device)
             setattr(o, name, None if t is None else t.data_ptr())
+        self._demod_tables(cfg)
         s = getattr(stream, 'cuda_stream', stream)
         rc = self._L.dpemu_run(self._h, C.addressof(cfg), int(shot_begin), int(n_shots), C.addressof(o),
                                C.c_void_p(s) if s else None)
@@ -401,7 +459,8 @@ def device_output_specs(cfg: _abi.Config, n_shots: int):
             'trace': ((cfg.trace_cap, n_lanes, 4), torch.int32),
             'meas': ((cfg.meas_cap, n_lanes, 2), torch.int32), 'regs': ((16, n_lanes), torch.int32),
             'hist': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64),
-            'hist_next': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64)}   # zeroed by the run
+            'hist_next': ((cfg.n_groups, 1 << cfg.cores_per_shot), torch.int64),   # zeroed by the run
+            'acc': ((cfg.meas_cap, n_lanes, 2), torch.int32)}                    # DEMOD runs only
 
 
 def _check_tensor(name, t, spec, device):

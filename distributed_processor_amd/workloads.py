@@ -180,6 +180,38 @@ def config3_active_reset(n_cores=8, extra_pulses=0, read_shift=0):
 
 
 CONFIG3_MEAS_LATENCY = READ_CLKS + 32   # rdlo strobe -> meas_valid, inside the 64-clock hold
+CONFIG3_DEMOD_LATENCY = 32              # DEMOD: the window (READ_CLKS) comes first, then this
+
+
+def config3_demod(ps, sigma=60.0, thr=0):
+    """The demodulation readout model (meas_model DEMOD, include/dpemu.h) for
+    the readouts of ``ps`` (config 1-3 programs: rdrv at t, rdlo RDLO_DELAY
+    later, both 2 us = 250 env words of 4 clocks): the ADC return arrives
+    RDLO_DELAY clocks after the drive, so the rdlo window integrates all of
+    it; the prepared states return with opposite phase (theta = pi, 0); each
+    core's discriminator axis is its state-1 direction, computed from the
+    drive and LO words of its program (with equal drive and LO frequencies
+    the demodulated phase is -F_d * delay + (phase_d - phase_lo) << 15 +
+    theta_1, constant over the window).  sigma: the accumulated value's noise
+    scale (float, see make_config); 60 puts ~1 % of a 2-us readout's shots
+    on the wrong side.  Returns make_config's ``demod`` dict; meas_latency
+    CONFIG3_DEMOD_LATENCY keeps meas_valid where CONFIG3_MEAS_LATENCY put it."""
+    import math
+    w, d_off, d_len, l_off, l_len = ps.readout_freqs(RDRV, RDLO)
+    axes = []
+    for c in range(ps.cores_per_shot):
+        p_ = int(ps.table[c])
+        f_d = int(w[d_off[p_]]) if d_len[p_] else 0
+        words = ps.program(0, c)
+        ph = {}
+        for cmd in words:                     # the phase words of the core's rdrv / rdlo pulses
+            v = int(cmd[0]) | (int(cmd[1]) << 32) | (int(cmd[2]) << 64) | (int(cmd[3]) << 96)
+            if v >> 124 in (0x8, 0x9) and ((v >> 37) & 0xF) & 3 in (RDRV, RDLO):
+                ph.setdefault((v >> 37) & 3, (v >> 71) & 0x1FFFF)
+        g = (-f_d * RDLO_DELAY + ((ph.get(RDRV, 0) - ph.get(RDLO, 0)) << 15)) % 2 ** 32
+        axes.append(g * 2 * math.pi / 2 ** 32)
+    return dict(drv_elem=RDRV, cpw=4, delay=RDLO_DELAY, theta=(math.pi, 0.0), gain=(1.0, 1.0), axis=axes,
+                sigma=sigma, thr=thr)
 
 
 def config3_lut(n_cores=8):

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DPEMU_ABI_VERSION 7
+#define DPEMU_ABI_VERSION 8
 
 /* ---- error codes ---------------------------------------------------- */
 #define DPEMU_OK            0
@@ -133,10 +133,36 @@ typedef struct dpemu_config {
     uint32_t hist_assign;      /* 0: out->hist += this run's counts; 1: out->hist = this run's
                                   counts (no separate zeroing launch before each run)        */
     uint32_t lane_order;       /* DPEMU_LANES_CORE_MAJOR (0) or DPEMU_LANES_SHOT_MAJOR (1), below */
+    /* readout demodulation model (meas_model = DPEMU_MEAS_DEMOD, ABI 8).
+     * The return of the lane's latest readout-drive strobe (cfg & 3 == ro_drv_elem,
+     * t_d <= t_lo) is mixed with the readout strobe's own LO (cfg & 3 == meas_elem,
+     * at t_lo) and accumulated per clock over their overlap; both phases follow the
+     * DDS phase accumulator, F * (k - t_ref) + phase17 << 15 (t_ref = the latest
+     * pulse_reset <= t_lo; F = the 32-bit frequency word of the pulse's freq index,
+     * dpemu_load_readout_freqs).  Per clock k of the overlap, with s the prepared state:
+     *   return  amp_d * ro_gain[s] / 2^16 at phase F_d (k - ro_delay - t_ref)
+     *           + phase_d << 15 + ro_theta[s]
+     *   acc    += return * conj(LO)   (int32 I / Q, closed form: exact integer
+     *                                   arithmetic of DESIGN.md §2, oracle/readout.c)
+     *   acc    += noise: (z_I, z_Q) * ro_sigma / 2^16 (Hadamard pairs of 4 Philox halves)
+     *   x       = (acc_I * axis_I + acc_Q * axis_Q) >> 15, axis = ro_axis[core]
+     *   outcome = x > ro_thr, meas_valid at max(t_lo + window + meas_latency,
+     *             the lane's previous meas_valid + 1)   (an in-order readout pipeline)
+     * window = the readout strobe's env length field (bits 23:12) * ro_cpw clocks
+     * (length 0: a CW envelope, 4096 words); the drive pulse lasts likewise.       */
+    uint32_t ro_drv_elem;      /* element of the readout drive (rdrv) strobes, 0..3, != meas_elem */
+    uint32_t ro_cpw;           /* clocks per env word of the rdrv / rdlo pulses, 1..8 (4 for
+                                  channel_config.json's rdrv 16 samples/clk interp 16, rdlo 4 / 4) */
+    uint32_t ro_delay;         /* drive -> ADC return delay, clocks (< 2^20)                */
+    uint32_t ro_theta[2];      /* return phase shift for prepared state 0 / 1 (2^32 = 2 pi)  */
+    uint32_t ro_gain[2];       /* return amplitude for state 0 / 1, Q16 (<= 65536)         */
+    uint32_t ro_axis[DPEMU_MAX_CORES]; /* discriminator axis per core, Q15: I16 low | Q16 high */
 } dpemu_config;
 
 #define DPEMU_MEAS_STATE   0
 #define DPEMU_MEAS_READOUT 1
+#define DPEMU_MEAS_DEMOD   2      /* rdlo demodulation of the rdrv return (ro_drv_elem ...) */
+#define DPEMU_RO_CPW_MAX   8      /* ro_cpw bound: an accumulation window is <= 2^15 clocks   */
 
 /* lane order of every per-lane output (dpemu_config.lane_order) */
 #define DPEMU_LANES_CORE_MAJOR 0  /* lane = core * n_shots + (shot - shot_begin)                  */
@@ -182,6 +208,8 @@ typedef struct dpemu_outputs {
                              from hist, that this run sets to zero in passing -- the buffer the
                              caller's next run accumulates into, so a pipeline of runs rotating
                              over three histogram buffers needs no zeroing launch (ABI 7) */
+    int32_t  *acc;        /* [meas_cap][n_lanes][2] accumulated {I, Q} of each readout (the
+                             accbuf of hwconfig.py:128,138-140); DEMOD runs only (ABI 8) */
 } dpemu_outputs;
 
 typedef struct dpemu_ctx dpemu_ctx;
@@ -212,6 +240,20 @@ const char *dpemu_last_error(dpemu_ctx *ctx);
 int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, const uint32_t *offsets,
                         const uint32_t *n_instr, uint32_t n_programs,
                         const uint32_t *prog_table, uint32_t n_groups, uint32_t cores_per_shot);
+
+/*
+ * Frequency words of the DEMOD readout model (ABI 8), per loaded program p:
+ * the readout drive element's freq index i reads words[drv_off[p] + i] when
+ * i < drv_len[p], else 0; the LO element's reads words[lo_off[p] + i] (i <
+ * lo_len[p]).  Each word is entry i's first word of the element's
+ * freq_buffer, f / f_clk * 2^32 (python/distproc/asmparse.py:64-86; the
+ * assembler's freq_buffers, assembler.py:510-516).  Arrays hold n_programs
+ * entries (the count of the last dpemu_load_programs); offsets + lengths
+ * must stay within n_words.  dpemu_load_programs clears the tables, and a
+ * DEMOD run without them is DPEMU_E_INVALID.
+ */
+int dpemu_load_readout_freqs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_words, const uint32_t *drv_off,
+                             const uint32_t *drv_len, const uint32_t *lo_off, const uint32_t *lo_len);
 
 /* Emulate shots [shot_begin, shot_begin + n_shots) on `stream` (hipStream_t or
  * NULL).  n_lanes = n_shots * C.  Outputs are device pointers.  out->hist_next,

@@ -20,6 +20,8 @@ import subprocess
 
 import numpy as np
 
+from distributed_processor_amd import _abi
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'liboracle.so')
 
@@ -61,7 +63,8 @@ class ShotCfg(C.Structure):
                 ('sync_mask', C.c_uint64), ('seed', C.c_uint64), ('lut_mask', C.c_uint32),
                 ('p1_threshold', C.c_uint32 * 64), ('lut_table', C.c_uint64 * 256),
                 ('meas_model', C.c_uint32), ('ro_sep', C.c_int32), ('ro_sigma', C.c_uint32),
-                ('ro_thr', C.c_int32), ('ro_win', C.c_uint32)]
+                ('ro_thr', C.c_int32), ('ro_win', C.c_uint32),
+                ('ro', _abi.Config), ('ro_tab', (C.c_void_p * 2) * 64), ('ro_len', (C.c_uint32 * 2) * 64)]
 
 
 class LaneOut(C.Structure):
@@ -69,7 +72,8 @@ class LaneOut(C.Structure):
         'status', 'flags', 't_end', 'ip', 'qclk_end', 'n_instr', 'n_events', 'n_trace',
         'n_meas', 'meas_bits')] + [('regs', C.c_uint32 * 16),
                                    ('ev', C.POINTER(C.c_uint32)),
-                                   ('tr', C.POINTER(C.c_uint32)), ('meas', C.POINTER(C.c_uint32))]
+                                   ('tr', C.POINTER(C.c_uint32)), ('meas', C.POINTER(C.c_uint32)),
+                                   ('acc', C.POINTER(C.c_int32))]
 
 
 def _setup(L):
@@ -102,9 +106,15 @@ def _setup(L):
     L.oracle_philox_u32.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]
     L.oracle_philox_u32.restype = C.c_uint32
     if hasattr(L, 'fast_run'):
-        L.fast_run.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
+        L.fast_run.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_void_p,
+                                                  C.c_void_p]
         L.fast_run.restype = C.c_int
-    L.rtl_run_batch.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_int]
+    L.rtl_run_batch.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_int,
+                                                   C.c_void_p, C.c_void_p]
+    L.oracle_sin33.argtypes = [C.c_int64]
+    L.oracle_sin33.restype = C.c_int64
+    L.oracle_dirichlet_q16.argtypes = [C.c_uint32, C.c_uint32]
+    L.oracle_dirichlet_q16.restype = C.c_int64
     L.rtl_run_batch.restype = C.c_int64
     L.oracle_dds_sin_lut.argtypes = [C.c_void_p]
     L.oracle_dds.argtypes = [C.c_void_p, C.c_int]
@@ -262,13 +272,26 @@ class PulseRegTB:
     cfg = property(lambda self: self.state[4])
 
 
+def _ro_arrays(ro):
+    """(words, hdr [n_programs, 4]) of DEMOD frequency tables, or (None, None):
+    ro = (words, drv_off, drv_len, lo_off, lo_len) as ProgramSet.readout_freqs
+    returns them"""
+    if ro is None:
+        return None, None
+    words = np.ascontiguousarray(ro[0], np.uint32)
+    if len(words) == 0:
+        words = np.zeros(1, np.uint32)
+    hdr = np.ascontiguousarray(np.stack([np.asarray(a, np.uint32) for a in ro[1:5]], axis=1))
+    return words, hdr
+
+
 def fast_run(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots, threads=0,
-             want=('summary', 'events', 'trace', 'meas', 'regs', 'hist')):
+             want=('summary', 'events', 'trace', 'meas', 'regs', 'hist', 'acc'), ro=None):
     """Event-driven model over shots [shot_begin, shot_begin + n_shots).
 
     cfg: distributed_processor_amd._abi.Config; words: (n, 4) uint32 of all
-    programs; returns the dict of host output arrays (dpemu_outputs layout)."""
-    from distributed_processor_amd import _abi
+    programs; ro: the DEMOD frequency tables (ProgramSet.readout_freqs);
+    returns the dict of host output arrays (dpemu_outputs layout)."""
     L = lib()
     words = np.ascontiguousarray(words, dtype=np.uint32)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
@@ -276,15 +299,17 @@ def fast_run(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots, thre
     prog_table = np.ascontiguousarray(prog_table, dtype=np.uint32)
     out = _abi.alloc_host_outputs(cfg, n_shots, want)
     ostruct = _abi.outputs_struct(out)
+    rw, rh = _ro_arrays(ro)
     rc = L.fast_run(C.addressof(cfg), words.ctypes.data, offsets.ctypes.data, n_instr.ctypes.data,
                     prog_table.ctypes.data, int(shot_begin), int(n_shots), C.addressof(ostruct),
-                    int(threads))
+                    int(threads), rw.ctypes.data if rw is not None else None,
+                    rh.ctypes.data if rh is not None else None)
     if rc != 0:
         raise RuntimeError('fast_run failed: {}'.format(rc))
     return out
 
 
-def rtl_run_batch(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots, horizon, threads=0):
+def rtl_run_batch(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots, horizon, threads=0, ro=None):
     """oracle_rtl over shots [shot_begin, shot_begin + n_shots), OpenMP over
     shots: the per-clock CPU baseline.  Returns (summary rows (n_lanes, 8) u32
     in the dpemu layout (core-major lanes), number of shots whose every core
@@ -294,9 +319,11 @@ def rtl_run_batch(cfg, words, offsets, n_instr, prog_table, shot_begin, n_shots,
     n_instr = np.ascontiguousarray(n_instr, dtype=np.uint32)
     prog_table = np.ascontiguousarray(prog_table, dtype=np.uint32)
     summary = np.zeros((int(n_shots) * cfg.cores_per_shot, 8), np.uint32)
+    rw, rh = _ro_arrays(ro)
     done = lib().rtl_run_batch(C.addressof(cfg), words.ctypes.data, offsets.ctypes.data, n_instr.ctypes.data,
                                prog_table.ctypes.data, int(shot_begin), int(n_shots), int(horizon),
-                               summary.ctypes.data, int(threads))
+                               summary.ctypes.data, int(threads), rw.ctypes.data if rw is not None else None,
+                               rh.ctypes.data if rh is not None else None)
     if done < 0:
         raise RuntimeError('rtl_run_batch failed')
     return summary, int(done)
@@ -320,7 +347,18 @@ def shot_cfg_from_config(cfg):
         s.lut_table[i] = cfg.lut_table[i]
     s.meas_model, s.ro_sep, s.ro_sigma, s.ro_thr = cfg.meas_model, cfg.ro_sep, cfg.ro_sigma, cfg.ro_thr
     s.ro_win = cfg.ro_win
+    C.memmove(C.addressof(s.ro), C.addressof(cfg), C.sizeof(cfg))
     return s
+
+
+def sin33(x):
+    """oracle_sin33: sin(2 pi x / 2^33) * 2^61 (oracle/readout.c)"""
+    return int(lib().oracle_sin33(int(x)))
+
+
+def dirichlet_q16(n, beta):
+    """oracle_dirichlet_q16: sin(n b pi / 2^32) / sin(b pi / 2^32) * 2^16, b = (int32) beta"""
+    return int(lib().oracle_dirichlet_q16(int(n), int(beta) & 0xFFFFFFFF))
 
 
 def make_shot_cfg(cores, fproc_mode=FPROC_MEAS, meas_elem=2, meas_latency=1, sync_latency=1,
@@ -344,10 +382,19 @@ def make_shot_cfg(cores, fproc_mode=FPROC_MEAS, meas_elem=2, meas_latency=1, syn
     return cfg
 
 
-def rtl_run_shot(cfg, programs, shot, horizon, ev_cap=256, tr_cap=256, meas_cap=32):
-    """programs: list (per core) of (n,4) uint32 arrays.  Returns (all_done, [lane dicts])."""
+def rtl_run_shot(cfg, programs, shot, horizon, ev_cap=256, tr_cap=256, meas_cap=32, ro_tabs=None):
+    """programs: list (per core) of (n,4) uint32 arrays; ro_tabs: DEMOD, per core
+    (drive freq words, LO freq words).  Returns (all_done, [lane dicts])."""
     L = lib()
     ncore = cfg.cores
+    keep = []
+    if ro_tabs is not None:
+        for c, tabs in enumerate(ro_tabs):
+            for k in (0, 1):
+                a = np.ascontiguousarray(tabs[k], np.uint32)
+                keep.append(a)
+                cfg.ro_tab[c][k] = a.ctypes.data if len(a) else None
+                cfg.ro_len[c][k] = len(a)
     progs = [np.ascontiguousarray(p, dtype=np.uint32).reshape(-1, 4) for p in programs]
     pp = (C.POINTER(C.c_uint32) * ncore)(*[p.ctypes.data_as(C.POINTER(C.c_uint32)) for p in progs])
     ni = (C.c_uint32 * ncore)(*[len(p) for p in progs])
@@ -357,20 +404,22 @@ def rtl_run_shot(cfg, programs, shot, horizon, ev_cap=256, tr_cap=256, meas_cap=
         ev = np.zeros((ev_cap, 4), np.uint32)
         tr = np.zeros((max(tr_cap, 1), 4), np.uint32)
         ms = np.zeros((max(meas_cap, 1), 2), np.uint32)
-        bufs.append((ev, tr, ms))
+        ac = np.zeros((max(meas_cap, 1), 2), np.int32)
+        bufs.append((ev, tr, ms, ac))
         outs[c].ev = ev.ctypes.data_as(C.POINTER(C.c_uint32))
         outs[c].tr = tr.ctypes.data_as(C.POINTER(C.c_uint32))
         outs[c].meas = ms.ctypes.data_as(C.POINTER(C.c_uint32))
+        outs[c].acc = ac.ctypes.data_as(C.POINTER(C.c_int32))
     ok = L.rtl_run_shot(C.byref(cfg), pp, ni, shot, horizon, ev_cap, tr_cap, meas_cap, outs)
     res = []
     for c in range(ncore):
         o = outs[c]
-        ev, tr, ms = bufs[c]
+        ev, tr, ms, ac = bufs[c]
         ne, nt, nm = min(o.n_events, ev_cap), min(o.n_trace, tr_cap), min(o.n_meas, meas_cap)
         res.append({'status': o.status, 'flags': o.flags, 't_end': o.t_end, 'ip': o.ip,
                     'qclk_end': o.qclk_end, 'n_instr': o.n_instr, 'n_events': o.n_events,
                     'n_trace': o.n_trace, 'n_meas': o.n_meas, 'meas_bits': o.meas_bits,
                     'regs': np.array(o.regs[:], np.uint32),
                     'events': ev[:ne].copy(), 'trace': tr[:nt].copy(),
-                    'meas': ms[:nm].copy()})
+                    'meas': ms[:nm].copy(), 'acc': ac[:nm].copy()})
     return bool(ok), res

@@ -48,6 +48,11 @@ typedef struct {
     uint32_t mt[MEAS_LOOKUP]; uint8_t mb[MEAS_LOOKUP];   /* measurement (valid cycle, bit) */
     uint32_t lane;                   /* output lane index (cfg->lane_order) */
     uint32_t core;
+    /* DEMOD (oracle/readout.c): the latest readout-drive strobe and pulse_reset,
+     * the last meas_valid, the program's drive / LO frequency tables */
+    oracle_ro_drive ro_d;
+    uint32_t ro_tref, ro_last_tv;
+    const uint32_t *ro_tab[2]; uint32_t ro_len[2];
 } flane;
 
 typedef struct {
@@ -95,19 +100,43 @@ static void emit_event(fshot *s, flane *l, uint32_t t, uint32_t kind)
     } else l->flags |= DPEMU_F_EVENT_OVF;
     l->n_events++;
 
-    /* measurement model: readout strobe -> meas_valid meas_latency clocks later */
+    const int demod = cfg->meas_model == DPEMU_MEAS_DEMOD;
+    const uint32_t pp = (l->pr[1] & 0x1FFFF) | ((l->pr[2] & 0x1FF) << 17);
+    if (demod) {                 /* the readout drive and the phase reference of the DEMOD model */
+        if (kind == DPEMU_EV_PULSE_RESET) l->ro_tref = t;
+        if (kind == DPEMU_EV_STROBE && (l->pr[4] & 3) == cfg->ro_drv_elem) {
+            l->ro_d.have = 1; l->ro_d.t = t; l->ro_d.env = l->pr[0] & 0xFFFFFF;
+            l->ro_d.pp = pp; l->ro_d.amp = l->pr[3] & 0xFFFF;
+        }
+    }
+    /* measurement model: readout strobe -> meas_valid meas_latency clocks later
+     * (DEMOD: after the readout window, in order) */
     if (kind == DPEMU_EV_STROBE && cfg->meas_elem != 0xFF && (l->pr[4] & 3) == cfg->meas_elem) {
         uint32_t core = l->core;
         uint32_t m = l->n_meas;
-        uint32_t bit = oracle_meas_bit(cfg->seed, s->shot, core, m, cfg->p1_threshold[core], l->pr[3],
-                                       cfg->meas_model, cfg->ro_sep, cfg->ro_sigma, cfg->ro_thr,
-                                       cfg->ro_win, l->pr[0]);
-        uint32_t tv = t + cfg->meas_latency;
+        uint32_t bit, tv;
+        int32_t acc[2] = {0, 0};
+        if (demod) {
+            const uint32_t f_lo = oracle_ro_freq(l->ro_tab[1], l->ro_len[1], pp);
+            const uint32_t f_d = oracle_ro_freq(l->ro_tab[0], l->ro_len[0], l->ro_d.pp);
+            bit = oracle_demod(cfg, s->shot, core, m, t, l->pr[0] & 0xFFFFFF, pp, f_lo, &l->ro_d, f_d, l->ro_tref, acc);
+            tv = oracle_demod_valid(cfg, t, l->pr[0] & 0xFFFFFF, l->ro_last_tv);
+            l->ro_last_tv = tv;
+        } else {
+            bit = oracle_meas_bit(cfg->seed, s->shot, core, m, cfg->p1_threshold[core], l->pr[3],
+                                  cfg->meas_model, cfg->ro_sep, cfg->ro_sigma, cfg->ro_thr,
+                                  cfg->ro_win, l->pr[0]);
+            tv = t + cfg->meas_latency;
+        }
         if (m < MEAS_LOOKUP) { l->mt[m] = tv; l->mb[m] = (uint8_t)bit; }
         if (m < cfg->meas_cap) {
             if (s->out->meas) {
                 uint32_t *e = s->out->meas + 2 * ((uint64_t)m * s->n_lanes + l->lane);
                 e[0] = tv; e[1] = bit;
+            }
+            if (s->out->acc) {
+                int32_t *e = s->out->acc + 2 * ((uint64_t)m * s->n_lanes + l->lane);
+                e[0] = acc[0]; e[1] = acc[1];
             }
         } else l->flags |= DPEMU_F_MEAS_OVF;
         if (m >= MEAS_LOOKUP) l->flags |= DPEMU_F_MEAS_OVF;
@@ -429,7 +458,8 @@ static void run_shot(fshot *s)
 
 int fast_run(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
              const uint32_t *n_instr, const uint32_t *prog_table, uint64_t shot_begin,
-             uint64_t n_shots, const dpemu_outputs *out, int n_threads)
+             uint64_t n_shots, const dpemu_outputs *out, int n_threads,
+             const uint32_t *ro_words, const uint32_t *ro_hdr)
 {
     const uint32_t C = cfg->cores_per_shot;
     if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1))) return DPEMU_E_INVALID;
@@ -460,6 +490,11 @@ int fast_run(const dpemu_config *cfg, const uint32_t *words, const uint32_t *off
             l->lane = cfg->lane_order == DPEMU_LANES_SHOT_MAJOR      /* include/dpemu.h lane order */
                           ? (uint32_t)((uint64_t)si * C + c) : (uint32_t)((uint64_t)c * n_shots + (uint64_t)si);
             l->core = c;
+            if (ro_words && ro_hdr) {
+                const uint32_t *h = ro_hdr + 4 * (uint64_t)p;
+                l->ro_tab[0] = ro_words + h[0]; l->ro_len[0] = h[1];
+                l->ro_tab[1] = ro_words + h[2]; l->ro_len[1] = h[3];
+            }
         }
         run_shot(s);
         uint32_t key = 0;

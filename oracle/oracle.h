@@ -33,6 +33,22 @@ uint32_t oracle_meas_bit(uint64_t seed, uint64_t shot, uint32_t core, uint32_t m
                          uint32_t meas_model, int32_t ro_sep, uint32_t ro_sigma, int32_t ro_thr,
                          uint32_t ro_win, uint32_t env);
 
+/* ---- readout demodulation model (readout.c; meas_model DPEMU_MEAS_DEMOD) ---- */
+typedef struct {
+    uint32_t have;             /* a readout-drive strobe was seen                   */
+    uint32_t t, env, pp, amp;  /* its cycle, env word, phase | freq << 17, amp word */
+} oracle_ro_drive;
+int64_t oracle_sin33(int64_t x);                      /* sin(2 pi x / 2^33) * 2^61 */
+int64_t oracle_dirichlet_q16(uint32_t n, uint32_t beta);
+uint32_t oracle_ro_words(uint32_t env);               /* env length field, 0 (CW) = 4096 */
+uint32_t oracle_ro_freq(const uint32_t *tab, uint32_t len, uint32_t pp);
+/* meas_valid of a readout at t_lo after one valid at last_tv (0: none) */
+uint32_t oracle_demod_valid(const dpemu_config *cfg, uint32_t t_lo, uint32_t env_lo, uint32_t last_tv);
+/* outcome of measurement m; acc = the accumulated {I, Q} */
+uint32_t oracle_demod(const dpemu_config *cfg, uint64_t shot, uint32_t core, uint32_t m, uint32_t t_lo,
+                      uint32_t env_lo, uint32_t pp_lo, uint32_t f_lo, const oracle_ro_drive *d, uint32_t f_d,
+                      uint32_t t_ref, int32_t acc[2]);
+
 /* ---- per-clock model ---------------------------------------------------- */
 typedef struct {
     uint8_t reset_reg, reset_sr, qclk_trig, cstrobe_p;
@@ -87,6 +103,11 @@ typedef struct {
     uint32_t ro_sigma;
     int32_t ro_thr;
     uint32_t ro_win;
+    /* DEMOD: the run's config (its seed, thresholds and ro_* fields are the ones
+     * read) and each core's drive / LO frequency tables */
+    dpemu_config ro;
+    const uint32_t *ro_tab[DPEMU_MAX_CORES][2];
+    uint32_t ro_len[DPEMU_MAX_CORES][2];
 } oracle_shot_cfg;
 
 #define RTL_MQ 64
@@ -130,6 +151,12 @@ typedef struct {
     rtl_meas_q mq[DPEMU_MAX_CORES];
     uint32_t n_meas[DPEMU_MAX_CORES];
     uint64_t cur_valid, cur_meas;
+    /* DEMOD: each core's latest readout-drive strobe and pulse_reset (dpemu
+     * times, cycle - T0), its last meas_valid cycle and accumulated {I, Q} */
+    oracle_ro_drive ro_d[DPEMU_MAX_CORES];
+    uint32_t ro_tref[DPEMU_MAX_CORES];
+    uint64_t ro_last_tv[DPEMU_MAX_CORES];
+    int32_t ro_acc[DPEMU_MAX_CORES][RTL_MQ][2];
     /* sync controller */
     uint64_t sync_arrived; int sync_pend; uint64_t sync_t;
 } rtl_shot;
@@ -164,6 +191,7 @@ typedef struct {
     uint32_t *ev;      /* [ev_cap][4] event records (include/dpemu.h) */
     uint32_t *tr;      /* [tr_cap][4] */
     uint32_t *meas;    /* [meas_cap][2] */
+    int32_t *acc;      /* [meas_cap][2] accumulated {I, Q} (DEMOD), or NULL */
 } oracle_lane_out;
 
 int rtl_run_shot(const oracle_shot_cfg *cfg, const uint32_t *const *progs, const uint32_t *n_instr,
@@ -173,12 +201,16 @@ int rtl_run_shot(const oracle_shot_cfg *cfg, const uint32_t *const *progs, const
 /* per-clock batch over shots (OpenMP), dpemu summary rows; returns shots all-DONE */
 int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
                       const uint32_t *n_instr, const uint32_t *prog_table, uint64_t shot_begin,
-                      uint64_t n_shots, uint32_t horizon, uint32_t *summary, int n_threads);
+                      uint64_t n_shots, uint32_t horizon, uint32_t *summary, int n_threads,
+                      const uint32_t *ro_words, const uint32_t *ro_hdr);
 
 /* ---- event-driven model, dpemu_run-compatible batch entry ------------------ */
+/* ro_words / ro_hdr: the DEMOD frequency tables (dpemu_load_readout_freqs), ro_hdr
+ * [n_programs][4] = drv_off, drv_len, lo_off, lo_len; NULL when not DEMOD */
 int fast_run(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
              const uint32_t *n_instr, const uint32_t *prog_table, uint64_t shot_begin,
-             uint64_t n_shots, const dpemu_outputs *out, int n_threads);
+             uint64_t n_shots, const dpemu_outputs *out, int n_threads,
+             const uint32_t *ro_words, const uint32_t *ro_hdr);
 
 /* ---- DDS restatement --------------------------------------------------------- */
 void oracle_dds_sin_lut(int16_t *out4096);

@@ -27,6 +27,8 @@
 #endif
 #include <string.h>
 
+#define T0 6u   /* clocks from the start of reset to the first DECODE (rtl_run_shot) */
+
 /* ctrl.v:84-91 */
 enum { S_MEM_WAIT = 0, S_DECODE = 1, S_ALU0 = 2, S_ALU1 = 3, S_FPROC_WAIT = 4,
        S_SYNC_WAIT = 6, S_QCLK_RST = 7, S_DONE = 9 };
@@ -368,16 +370,40 @@ void rtl_shot_step(rtl_shot *s, const rtl_ext_inputs *ext)
         rtl_core_eval(&s->core[c], reset, fready[c], fdata[c],
                       sready && (s->cfg.sync_external || ((s->sync_mask >> c) & 1)));
 
-    /* measurement model: a readout strobe schedules meas_valid latency clocks later */
+    /* measurement model: a readout strobe schedules meas_valid latency clocks
+     * later (DEMOD: after its window, in order; oracle/readout.c) */
+    const int demod = s->cfg.meas_model == DPEMU_MEAS_DEMOD;
     for (uint32_t c = 0; c < C; c++) {
         const rtl_core_comb *o = &s->core[c].comb;
+        const uint32_t tnow = (uint32_t)(s->cycle - T0);      /* dpemu time of this clock */
+        if (demod && s->cycle >= T0) {
+            if (o->pulse_reset) s->ro_tref[c] = tnow;
+            if (o->cstrobe && (o->cfg & 3) == s->cfg.ro.ro_drv_elem) {
+                oracle_ro_drive *d = &s->ro_d[c];
+                d->have = 1; d->t = tnow; d->env = o->env & 0xFFFFFF;
+                d->pp = (o->phase & 0x1FFFF) | ((o->freq & 0x1FF) << 17); d->amp = o->amp & 0xFFFF;
+            }
+        }
         if (o->cstrobe && s->cfg.meas_elem != 0xFF && (o->cfg & 3) == s->cfg.meas_elem) {
             uint32_t m = s->n_meas[c]++;
-            int bit = (int)oracle_meas_bit(s->cfg.seed, s->shot, c, m, s->cfg.p1_threshold[c], o->amp,
+            rtl_meas_q *q = &s->mq[c];
+            int bit;
+            if (demod) {
+                const uint32_t pp = (o->phase & 0x1FFFF) | ((o->freq & 0x1FF) << 17);
+                const uint32_t f_lo = oracle_ro_freq(s->cfg.ro_tab[c][1], s->cfg.ro_len[c][1], pp);
+                const uint32_t f_d = oracle_ro_freq(s->cfg.ro_tab[c][0], s->cfg.ro_len[c][0], s->ro_d[c].pp);
+                bit = (int)oracle_demod(&s->cfg.ro, s->shot, c, m, tnow, o->env & 0xFFFFFF, pp, f_lo, &s->ro_d[c],
+                                        f_d, s->ro_tref[c], s->ro_acc[c][q->tail % RTL_MQ]);
+                const uint32_t tv = oracle_demod_valid(&s->cfg.ro, tnow, o->env & 0xFFFFFF,
+                                                       (uint32_t)s->ro_last_tv[c]);
+                s->ro_last_tv[c] = tv;
+                q->t[q->tail % RTL_MQ] = (uint64_t)tv + T0;
+            } else {
+                bit = (int)oracle_meas_bit(s->cfg.seed, s->shot, c, m, s->cfg.p1_threshold[c], o->amp,
                                            s->cfg.meas_model, s->cfg.ro_sep, s->cfg.ro_sigma, s->cfg.ro_thr,
                                            s->cfg.ro_win, o->env);
-            rtl_meas_q *q = &s->mq[c];
-            q->t[q->tail % RTL_MQ] = s->cycle + s->cfg.meas_latency;
+                q->t[q->tail % RTL_MQ] = s->cycle + s->cfg.meas_latency;
+            }
             q->bit[q->tail % RTL_MQ] = (uint8_t)bit;
             q->tail++;
         }
@@ -486,9 +512,8 @@ uint32_t rtl_fproc_tb_ready(const rtl_fproc_tb *tb) { return tb->snap_ready; }
 uint32_t rtl_fproc_tb_data(const rtl_fproc_tb *tb, int c) { return tb->snap_data[c]; }
 
 /* ---------------------------------------------------------------------- */
-/* batch driver with the dpemu output format (t = cycle - 6: first DECODE)  */
+/* batch driver with the dpemu output format (t = cycle - T0: first DECODE) */
 /* ---------------------------------------------------------------------- */
-#define T0 6u
 
 static void put_event(oracle_lane_out *lo, uint32_t cap, uint32_t t, const rtl_core_comb *o, uint32_t kind)
 {
@@ -560,6 +585,7 @@ int rtl_run_shot(const oracle_shot_cfg *cfg, const uint32_t *const *progs, const
                 if (m < meas_cap) {
                     lo->meas[2 * m] = (uint32_t)(q->t[slot] - T0);
                     lo->meas[2 * m + 1] = q->bit[slot];
+                    if (lo->acc) { lo->acc[2 * m] = s->ro_acc[c][slot][0]; lo->acc[2 * m + 1] = s->ro_acc[c][slot][1]; }
                 } else lo->flags |= DPEMU_F_MEAS_OVF;
                 if (m < 32 && q->bit[slot]) lo->meas_bits |= 1u << m;
             }
@@ -586,13 +612,15 @@ int rtl_run_shot(const oracle_shot_cfg *cfg, const uint32_t *const *progs, const
  * run in this image.  Events, traces and measurements go to per-thread
  * buffers of the config's caps (the same work as a dpemu run); the summary
  * rows (dpemu layout, include/dpemu.h) go to `summary` when it is non-null.
- * `horizon`: cycles simulated past the first decode at most.  Returns the
+ * `horizon`: cycles simulated past the first decode at most.  ro_words /
+ * ro_hdr: the DEMOD frequency tables, as fast_run takes them (or NULL).  Returns the
  * number of shots whose every core reached DONE, or -1 for a bad config or
  * a failed scratch allocation (C x event_cap x 16 B per thread).
  */
 int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint32_t *offsets,
                       const uint32_t *n_instr, const uint32_t *prog_table, uint64_t shot_begin,
-                      uint64_t n_shots, uint32_t horizon, uint32_t *summary, int n_threads)
+                      uint64_t n_shots, uint32_t horizon, uint32_t *summary, int n_threads,
+                      const uint32_t *ro_words, const uint32_t *ro_hdr)
 {
     const uint32_t C = cfg->cores_per_shot;
     if (C == 0 || C > DPEMU_MAX_CORES || (C & (C - 1))) return -1;
@@ -605,6 +633,7 @@ int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint
     memcpy(sc.lut_table, cfg->lut_table, sizeof sc.lut_table);
     sc.meas_model = cfg->meas_model; sc.ro_sep = cfg->ro_sep; sc.ro_sigma = cfg->ro_sigma;
     sc.ro_thr = cfg->ro_thr; sc.ro_win = cfg->ro_win;
+    sc.ro = *cfg;
     const uint32_t ev_cap = cfg->event_cap ? cfg->event_cap : 1, tr_cap = cfg->trace_cap ? cfg->trace_cap : 1;
     const uint32_t ms_cap = cfg->meas_cap ? cfg->meas_cap : 1;
     int64_t done = 0;
@@ -628,17 +657,25 @@ int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint
         }
         const uint32_t *progs[DPEMU_MAX_CORES];
         uint32_t ni[DPEMU_MAX_CORES];
+        oracle_shot_cfg *tc = (oracle_shot_cfg *)malloc(sizeof sc);   /* this thread's copy (DEMOD tables) */
+        if (tc) *tc = sc;
+        else oom = 1;
         #pragma omp for schedule(dynamic, 4)
         for (int64_t si = 0; si < (int64_t)n_shots; si++) {
-            if (bad) continue;   /* (no break inside an omp for) */
+            if (bad || !tc) continue;   /* (no break inside an omp for) */
             const uint64_t shot = shot_begin + (uint64_t)si;
             const uint32_t g = (uint32_t)((shot / cfg->shots_per_group) % cfg->n_groups);
             for (uint32_t c = 0; c < C; c++) {
                 const uint32_t p = prog_table[(uint64_t)g * C + c];
                 progs[c] = words + 4 * (uint64_t)offsets[p];
                 ni[c] = n_instr[p];
+                if (ro_words && ro_hdr) {
+                    const uint32_t *h = ro_hdr + 4 * (uint64_t)p;
+                    tc->ro_tab[c][0] = ro_words + h[0]; tc->ro_len[c][0] = h[1];
+                    tc->ro_tab[c][1] = ro_words + h[2]; tc->ro_len[c][1] = h[3];
+                }
             }
-            done += rtl_run_shot(&sc, progs, ni, shot, horizon, cfg->event_cap, cfg->trace_cap, cfg->meas_cap, lo);
+            done += rtl_run_shot(tc, progs, ni, shot, horizon, cfg->event_cap, cfg->trace_cap, cfg->meas_cap, lo);
             if (summary)
                 for (uint32_t c = 0; c < C; c++) {
                     const uint64_t L = cfg->lane_order == DPEMU_LANES_SHOT_MAJOR ? (uint64_t)si * C + c
@@ -650,7 +687,7 @@ int64_t rtl_run_batch(const dpemu_config *cfg, const uint32_t *words, const uint
                     sm[5] = lo[c].n_meas; sm[6] = lo[c].meas_bits; sm[7] = lo[c].n_trace;
                 }
         }
-        free(lo); free(ev); free(tr); free(ms);
+        free(lo); free(ev); free(tr); free(ms); free(tc);
     }
     return oom ? -1 : done;
 }

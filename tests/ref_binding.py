@@ -11,11 +11,11 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 7                                    # DPEMU_ABI_VERSION, include/dpemu.h
+ABI_VERSION = 8                                    # DPEMU_ABI_VERSION, include/dpemu.h
 _vp, _u32, _u64 = C.c_void_p, C.c_uint32, C.c_uint64
 
 
-class DpemuConfig(C.Structure):                    # dpemu_config, include/dpemu.h (ABI 7)
+class DpemuConfig(C.Structure):                    # dpemu_config, include/dpemu.h (ABI 8)
     _fields_ = [(n, C.c_uint32) for n in ('cores_per_shot', 'n_groups', 'shots_per_group',
                 'max_cycles', 'event_cap', 'trace_cap', 'meas_cap', 'fproc_mode', 'meas_elem',
                 'meas_latency', 'sync_latency', 'exec_flags')] + [
@@ -23,11 +23,14 @@ class DpemuConfig(C.Structure):                    # dpemu_config, include/dpemu
                ('meas_model', C.c_uint32), ('p1_threshold', C.c_uint32 * 64),
                ('lut_table', C.c_uint64 * 256), ('ro_sep', C.c_int32), ('ro_sigma', C.c_uint32),
                ('ro_thr', C.c_int32), ('ro_win', C.c_uint32), ('hist_assign', C.c_uint32),
-               ('lane_order', C.c_uint32)]
+               ('lane_order', C.c_uint32), ('ro_drv_elem', C.c_uint32), ('ro_cpw', C.c_uint32),
+               ('ro_delay', C.c_uint32), ('ro_theta', C.c_uint32 * 2), ('ro_gain', C.c_uint32 * 2),
+               ('ro_axis', C.c_uint32 * 64)]
 
 
 class DpemuOutputs(C.Structure):                   # dpemu_outputs
-    _fields_ = [(n, C.c_void_p) for n in ('summary', 'events', 'trace', 'meas', 'regs', 'hist', 'hist_next')]
+    _fields_ = [(n, C.c_void_p) for n in ('summary', 'events', 'trace', 'meas', 'regs', 'hist', 'hist_next',
+                                          'acc')]
 
 
 _L = None

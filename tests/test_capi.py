@@ -31,9 +31,9 @@ def test_abi_version_and_struct_sizes():
     L = _native.load_library()
     assert L.dpemu_abi_version() == _abi.ABI_VERSION
     # dpemu_config: 12 u32 + 2 u64 + 2 u32 + 64 u32 + 256 u64 + the readout model's 4 x 32 bit
-    # + hist_assign, reserved
-    assert C.sizeof(_abi.Config) == 12 * 4 + 16 + 8 + 64 * 4 + 256 * 8 + 16 + 8
-    assert C.sizeof(_abi.Outputs) == 7 * 8
+    # + hist_assign, lane_order + the DEMOD model's 3 + 2 + 2 + 64 u32 (ABI 8), padded to 8
+    assert C.sizeof(_abi.Config) == (12 * 4 + 16 + 8 + 64 * 4 + 256 * 8 + 16 + 8 + 71 * 4 + 7) // 8 * 8
+    assert C.sizeof(_abi.Outputs) == 8 * 8
     assert C.sizeof(_abi.DDSChannels) == 4 * 4 + 8 * 8
     sizes = (C.c_uint64 * 3)()
     assert L.dpemu_struct_sizes(sizes) == 0
@@ -80,6 +80,21 @@ def test_config_validation():
         _abi.make_config(4, event_cap=2 ** 21)
     with pytest.raises(ValueError):
         _abi.make_config(4, readout=dict(sep=1, win=4096))
+    with pytest.raises(ValueError):                  # the drive element must differ from the LO's
+        _abi.make_config(4, meas_elem=2, demod=dict(drv_elem=2))
+    with pytest.raises(ValueError):
+        _abi.make_config(4, demod=dict(cpw=9))
+    with pytest.raises(ValueError):
+        _abi.make_config(4, demod=dict(sigma=256.0))
+    with pytest.raises(ValueError):
+        _abi.make_config(4, demod=dict(gain=(1.5, 1.0)))
+    with pytest.raises(ValueError):
+        _abi.make_config(4, readout=dict(sep=1), demod=dict())
+    d = _abi.make_config(4, demod=dict(drv_elem=1, cpw=4, delay=300, theta=(0.0, 3.141592653589793),
+                                       gain=(0.5, 1.0), axis=[0.0, 1.5707963267948966], sigma=2.0, thr=-7))
+    assert d.meas_model == _abi.MEAS_DEMOD and d.ro_theta[1] == 2 ** 31 and d.ro_gain[0] == 32768
+    assert d.ro_axis[0] == 32767 and d.ro_axis[1] == 32767 << 16 and d.ro_axis[2] == 32767
+    assert d.ro_sigma == 2 << 16 and d.ro_thr == -7 and (d.ro_drv_elem, d.ro_cpw, d.ro_delay) == (1, 4, 300)
     cfg = _abi.make_config(8, p1=[0.0, 1.0, 0.5])
     assert cfg.p1_threshold[0] == 0 and cfg.p1_threshold[1] == 0xFFFFFFFF and cfg.p1_threshold[2] == 2 ** 31
 

@@ -19,23 +19,44 @@ HORIZON = 6000
 EV_CAP, TR_CAP, MEAS_CAP = 128, 128, 16
 
 
-def run_both(case, n_shots=4, seed=0x5EED, meas_latency=20, sync_latency=1, sync_mask=0, shot0=0, readout=None):
+def demod_tables(rng, n_programs):
+    """random DEMOD frequency tables, one (drive, LO) pair per program: lengths
+    0..600 (the fuzzer's 9-bit freq indices also land past them: words 0)"""
+    tabs = [tuple(np.array([rng.getrandbits(32) for _ in range(rng.choice([0, 1, 5, 600]))], np.uint32)
+                  for _ in range(2)) for _ in range(n_programs)]
+    lens = [len(t) for pair in tabs for t in pair]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint32)
+    words = np.concatenate([t for pair in tabs for t in pair] + [np.zeros(0, np.uint32)]).astype(np.uint32)
+    return tabs, (words, offs[0::2], np.array(lens[0::2], np.uint32), offs[1::2], np.array(lens[1::2], np.uint32))
+
+
+def demod_params(rng, C, meas_elem=2):
+    return dict(drv_elem=rng.choice([e for e in range(4) if e != meas_elem]), cpw=rng.randint(1, 8),
+                delay=rng.choice([0, rng.randint(0, 40), 300]), theta=(rng.uniform(-4, 4), rng.uniform(-4, 4)),
+                gain=(rng.random(), rng.random()), axis=[rng.uniform(-4, 4) for _ in range(C)],
+                sigma=rng.choice([0.0, 0.5, 3.0, 200.0]), thr=rng.randint(-2 ** 22, 2 ** 22))
+
+
+def run_both(case, n_shots=4, seed=0x5EED, meas_latency=20, sync_latency=1, sync_mask=0, shot0=0, readout=None,
+             demod=None):
     C = case['ncores']
     mode = _abi.FPROC_MEAS if case['mode'] == 'meas' else _abi.FPROC_LUT
     cfg = _abi.make_config(C, n_groups=case['n_groups'], shots_per_group=1, max_cycles=HORIZON,
                            event_cap=EV_CAP, trace_cap=TR_CAP, meas_cap=MEAS_CAP, fproc_mode=mode,
                            meas_latency=meas_latency, sync_latency=sync_latency, sync_mask=sync_mask,
-                           seed=seed, p1=0.5, readout=readout)
+                           seed=seed, p1=0.5, readout=readout, demod=demod)
     words, offs, ni = pack_programs(case['progs'])
-    fast = oracle.fast_run(cfg, words, offs, ni, case['table'], shot0, n_shots)
+    tabs, ro = demod_tables(case['rng'], len(case['progs'])) if demod is not None else (None, None)
+    fast = oracle.fast_run(cfg, words, offs, ni, case['table'], shot0, n_shots, ro=ro)
     scfg = oracle.shot_cfg_from_config(cfg)
     rtl = []
     for s in range(n_shots):
         shot = shot0 + s
         g = shot % case['n_groups']
-        progs = [np.asarray(__import__('distributed_processor_amd').isa.words_to_u32(case['progs'][case['table'][g * C + c]]))
-                 for c in range(C)]
-        ok, lanes = oracle.rtl_run_shot(scfg, progs, shot, HORIZON + 16, EV_CAP, TR_CAP, MEAS_CAP)
+        prs = [int(case['table'][g * C + c]) for c in range(C)]
+        progs = [np.asarray(__import__('distributed_processor_amd').isa.words_to_u32(case['progs'][p])) for p in prs]
+        ok, lanes = oracle.rtl_run_shot(scfg, progs, shot, HORIZON + 16, EV_CAP, TR_CAP, MEAS_CAP,
+                                        ro_tabs=[tabs[p] for p in prs] if tabs else None)
         rtl.append(lanes)
     return cfg, fast, rtl
 
@@ -69,6 +90,8 @@ def compare(cfg, fast, rtl, n_shots):
                 np.testing.assert_array_equal(ftr, r['trace'], err_msg=ctx)
                 assert summ['n_meas'][L] == r['n_meas'], ctx
                 np.testing.assert_array_equal(fms, r['meas'], err_msg=ctx)
+                if 'acc' in fast:
+                    np.testing.assert_array_equal(fast['acc'][:nm, L], r['acc'], err_msg=ctx)
                 assert summ['meas_bits'][L] == r['meas_bits'], ctx
                 np.testing.assert_array_equal(fast['regs'][:, L], r['regs'], err_msg=ctx)
             else:
@@ -139,3 +162,18 @@ def test_fuzz_readout_model(seed):
               win=[0, 7, 300, 4095][(seed // 4) % 4])
     cfg, fast, rtl = run_both(case, n_shots=3, meas_latency=1 + seed % 9, readout=ro)
     compare(cfg, fast, rtl, 3)
+
+
+@pytest.mark.parametrize('seed', range(24))
+def test_fuzz_demod_model(seed):
+    """meas_model DEMOD (include/dpemu.h, oracle/readout.c): random drive / LO
+    elements, windows, delays, frequency tables and discriminators; outcomes,
+    meas_valid cycles and the accumulated {I, Q} agree per clock and event-driven,
+    and drive fproc branches in both back ends"""
+    import random
+    case = random_case(5000 + seed, ncores=[1, 2, 4][seed % 3], mode=['meas', 'lut'][seed % 2],
+                       allow_late=False, allow_hang=False)
+    d = demod_params(random.Random(seed), case['ncores'])
+    cfg, fast, rtl = run_both(case, n_shots=3, meas_latency=1 + seed % 9, demod=d)
+    compare(cfg, fast, rtl, 3)
+    assert 'acc' in fast

@@ -12,6 +12,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+@pytest.mark.fresh_process        # runs g++ and a binary: before any test touches the GPU (tests/conftest.py)
 @pytest.mark.skipif(shutil.which('g++') is None, reason='g++ not available')
 def test_lds_grants_bookkeeping(tmp_path):
     exe = str(tmp_path / 'lds_grants_test')
