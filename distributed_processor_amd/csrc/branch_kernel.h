@@ -118,8 +118,10 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     // identical; profiles/r04_branch_direct_ab.jsonl): config 3 (fproc_meas)
     // 0.446 ms held vs 0.480 direct; config 3 through the LUT 0.564 held vs
     // 0.494 direct -- the row bookkeeping's VALU costs more there than the
-    // scattered partial rows it avoids
-    constexpr bool DIRECT = LUT;
+    // scattered partial rows it avoids.  With the DEMOD readout the held rows'
+    // 10 VGPRs decide the occupancy (105 -> 95 VGPRs, 4 -> 5 waves per SIMD):
+    // config 3 DEMOD 0.653 ms held vs 0.515 direct (profiles/r06_demod_ab2.json)
+    constexpr bool DIRECT = LUT || DEMOD;
     constexpr int NF = LUT ? LUT_FIRE_CAP : 1;
 
     __shared__ uint32_t s_regs[REGS ? 16 : 1][REGS ? BLOCK : 1];
@@ -129,6 +131,10 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     __shared__ uint32_t s_fire[NF][LUT ? BLOCK : 1];
     __shared__ uint32_t s_pref[PLDS ? BLOCK + 1 : 1];
     __shared__ uint32_t s_scan[BLOCK / 64];
+    // DEMOD: the lane's program's frequency tables {drv_off, drv_len, lo_off,
+    // lo_len} and their index-0 words, loaded once (a global load at a readout
+    // would wait behind the lane's event stores: vmcnt is shared)
+    __shared__ uint32_t s_rof[DEMOD ? 6 : 1][DEMOD ? BLOCK : 1];
     // dynamic LDS: the staged programs (prog_lds_words commands), then the
     // histogram pre-aggregation bins when hist_lds
     extern __shared__ uint4 s_dyn[];
@@ -166,6 +172,12 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     const bool cmd_major = !PLDS && p.fetch_stride != 1u;
     const uint32_t fetch_off = cmd_major ? prog : base, k_max = cmd_major ? p.max_len : nprog;
     const uint32_t thr_core = valid ? p.p1_thr[core] : 0u;
+    if constexpr (DEMOD) {
+        const uint4 h = valid ? p.ro_hdr[prog] : make_uint4(0u, 0u, 0u, 0u);
+        s_rof[0][tid] = h.x; s_rof[1][tid] = h.y; s_rof[2][tid] = h.z; s_rof[3][tid] = h.w;
+        s_rof[4][tid] = ro_freq(p, h.x, h.y, 0u);
+        s_rof[5][tid] = ro_freq(p, h.z, h.w, 0u);
+    }
     if (p.hist_lds) {
         for (uint32_t i = tid; i < HIST_LDS_MAX; i += BLOCK) s_hist[i] = 0;
         __syncthreads();
@@ -237,7 +249,10 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
                 uint32_t bit, tv;
                 if constexpr (DEMOD) {
                     int2 a;
-                    bit = demod_readout(p, shot, core, n_meas, thr_core, prog, te, pe, pp, ro_d, ro_tref, a);
+                    const uint32_t fi_lo = (pp >> 17) & 0x1FFu, fi_d = (ro_d.pp >> 17) & 0x1FFu;
+                    const uint32_t f_lo = fi_lo ? ro_freq(p, s_rof[2][tid], s_rof[3][tid], fi_lo) : s_rof[5][tid];
+                    const uint32_t f_d = fi_d ? ro_freq(p, s_rof[0][tid], s_rof[1][tid], fi_d) : s_rof[4][tid];
+                    bit = demod_readout(p, shot, core, n_meas, thr_core, te, pe, pp, ro_d, ro_tref, f_lo, f_d, a);
                     tv = demod_valid(p, te, pe, ro_ltv);
                     ro_ltv = tv;
                     if (p.acc && n_meas < p.meas_cap) p.acc[(uint64_t)n_meas * n_lanes + lane] = a;

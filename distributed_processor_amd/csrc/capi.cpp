@@ -50,7 +50,7 @@ struct dpemu_ctx {
     uint32_t *d_offsets = nullptr, *d_ninstr = nullptr, *d_table = nullptr;
     uint32_t n_programs = 0, n_groups = 0, C = 0;
     bool has_fproc = false, has_sync = false, straight = false, linear = false, reg_writes = false;
-    // register slots of the macro image (remap_macro_regs): 2 or 4 in VGPRs, else 16 (identity map)
+    // register slots of the macro image (remap_macro_regs): 2 in VGPRs, else 16 (identity map)
     int macro_nr = 16;
     bool macro_addid = false;               // every ALU slot of the macro image is id0 / add
     bool macro_w3 = false;                  // the macro image has three ALU slots (kernels.h MACRO_W3)
@@ -219,6 +219,28 @@ static void pack_macros(const std::vector<uint32_t> &wide, bool w3, std::vector<
 // field that names no register maps to slot 0 (its value is selected away).
 // Returns the slot count (2, or 16 = left as is) and the maps
 // (KParams::reg_map / reg_inv).
+// registers the decode_cmd words u[0 .. n) name (the reg_file reads and
+// writes of reg_alu / inc_qclk and the register-sourced pulse fields), by the
+// rules remap_macro_regs applies to the macro image built from them
+static uint32_t named_regs(const uint32_t *u, uint64_t n)
+{
+    uint32_t used = 0;
+    for (uint64_t i = 0; i < n; i++, u += 4) {
+        const uint32_t op4 = u[1] >> 28, rs0 = (u[3] >> 20) & 15u;
+        if (op4 == 0x1u || op4 == 0x6u) {                      // reg_alu / inc_qclk
+            const uint32_t op = u[1] & 7u;                      // alu.v: 0 id0, 6 id1, 7 zero
+            if ((u[1] & 8u) && op != 6u && op != 7u) used |= 1u << rs0;
+            if (op4 == 0x1u) {
+                used |= 1u << ((u[1] >> 8) & 15u);
+                if (op != 0u && op != 7u) used |= 1u << ((u[1] >> 4) & 15u);
+            }
+        } else if ((op4 == 0x8u || op4 == 0x9u) && (u[3] & UOP_ANY_RS)) {
+            used |= 1u << rs0;
+        }
+    }
+    return used;
+}
+
 static int remap_macro_regs(std::vector<uint32_t> &mac, uint64_t &map, uint64_t &inv, uint32_t &used)
 {
     used = 0;
@@ -483,22 +505,21 @@ int dpemu_load_programs(dpemu_ctx *ctx, const uint32_t *words, uint64_t n_cmds, 
         // (MACRO_W3: RB-like programs then have almost no macro without a
         // pulse, so a wave's programs stay on the same event slot and its
         // stores are whole rows), else two
+        // the register count decides the layout before the image is built
+        // (the guard commands are zero and name none)
         std::vector<uint32_t> wide, mac, moff(n_programs + 1);
-        bool w3 = true;
-        for (int attempt = 0; attempt < 2; attempt++) {
-            wide.clear();
-            wide.reserve((tot * 4 + 8ull * n_programs) / 8 * MACRO_WIDE);
-            for (uint32_t pr = 0; pr < n_programs; pr++) {
-                moff[pr] = (uint32_t)(wide.size() / MACRO_WIDE);
-                build_macros(&uops[4ull * goff[pr]], n_instr[pr], w3 ? 3u : 2u, wide);
-                if (wide.size() / MACRO_WIDE >= (1ull << 32))
-                    return fail(ctx, DPEMU_E_INVALID, "macro image exceeds 2^32 macros");
-            }
-            moff[n_programs] = (uint32_t)(wide.size() / MACRO_WIDE);
-            ctx->macro_nr = remap_macro_regs(wide, ctx->reg_map, ctx->reg_inv, ctx->reg_used);
-            if (ctx->macro_nr == 2 || !w3) break;
-            w3 = false;                               // 16 registers: the two-slot layout
+        const bool w3 = __builtin_popcount(named_regs(uops.data(), tot)) <= 2;
+        wide.reserve((tot * 4 + 8ull * n_programs) / 8 * MACRO_WIDE);
+        for (uint32_t pr = 0; pr < n_programs; pr++) {
+            moff[pr] = (uint32_t)(wide.size() / MACRO_WIDE);
+            build_macros(&uops[4ull * goff[pr]], n_instr[pr], w3 ? 3u : 2u, wide);
+            if (wide.size() / MACRO_WIDE >= (1ull << 32))
+                return fail(ctx, DPEMU_E_INVALID, "macro image exceeds 2^32 macros");
         }
+        moff[n_programs] = (uint32_t)(wide.size() / MACRO_WIDE);
+        ctx->macro_nr = remap_macro_regs(wide, ctx->reg_map, ctx->reg_inv, ctx->reg_used);
+        if ((ctx->macro_nr == 2) != w3)
+            return fail(ctx, DPEMU_E_INVALID, "internal: macro register count disagrees with the decoded commands");
         ctx->macro_w3 = w3;
         pack_macros(wide, w3, mac);
         std::vector<uint32_t>().swap(wide);

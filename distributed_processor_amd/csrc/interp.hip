@@ -158,7 +158,9 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         status = st; mode = M_FIN; t_end = at;
     };
 
-    auto emit_event = [&](uint32_t te, uint32_t kind) {
+    // (always_inline: with the DEMOD readout an out-of-line call would keep the
+    // kernel's state in scratch, tests/test_kernel_resources.py)
+    auto emit_event = [&](uint32_t te, uint32_t kind) __attribute__((always_inline)) {
         if (n_ev < p.event_cap) {
             if (p.events) p.events[(uint64_t)n_ev * n_lanes + lane] = event_record(te, pe, pp, pa, kind);
         } else flags |= F_EVENT_OVF;
@@ -172,7 +174,10 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
             uint32_t bit, tv;
             if (demod) {
                 int2 a;
-                bit = demod_readout(p, shot, core, n_meas, thr_core, prog, te, pe, pp, ro_d, ro_tref, a);
+                const uint4 h = p.ro_hdr[prog];              // drv_off, drv_len, lo_off, lo_len
+                bit = demod_readout(p, shot, core, n_meas, thr_core, te, pe, pp, ro_d, ro_tref,
+                                    ro_freq(p, h.z, h.w, (pp >> 17) & 0x1FFu),
+                                    ro_freq(p, h.x, h.y, (ro_d.pp >> 17) & 0x1FFu), a);
                 tv = demod_valid(p, te, pe, ro_ltv);
                 ro_ltv = tv;
                 if (p.acc && n_meas < p.meas_cap) p.acc[(uint64_t)n_meas * n_lanes + lane] = a;
@@ -193,7 +198,7 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
         }
     };
 
-    auto emit_trace = [&](uint32_t tt, uint32_t addr, uint32_t val) {
+    auto emit_trace = [&](uint32_t tt, uint32_t addr, uint32_t val) __attribute__((always_inline)) {
         if (n_tr < p.trace_cap) {
             if (p.trace) p.trace[(uint64_t)n_tr * n_lanes + lane] = make_uint4(tt, addr, val, 0u);
         } else if (p.trace_cap) flags |= F_TRACE_OVF;
@@ -544,7 +549,10 @@ __global__ void __launch_bounds__(BLOCK) interp_kernel(const KParams p)
                         // the waiting fproc command
                         const uint4 u2 = PLDS ? s_prog[base + ip] : p.uops[base + ip];
                         const uint32_t op4b = u2.y >> 28, alub = u2.y & 7u;
-                        const uint32_t in0b = (u2.y & 8u) ? s_regs[(u2.w >> 20) & 15u][tid] : u2.x;
+                        // both operands loaded, then selected: a select of the two
+                        // addresses would be one flat_load (generic pointer)
+                        const uint32_t rs0v = s_regs[(u2.w >> 20) & 15u][tid];
+                        const uint32_t in0b = (u2.y & 8u) ? rs0v : u2.x;
                         if (tf > p.max_cycles) { finish(ST_MAX_CYCLES, wait_d); }
                         else {
                             const uint32_t out = alu_op(alub, in0b, (uint32_t)((out_bits >> core) & 1ull));

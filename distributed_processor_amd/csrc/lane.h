@@ -154,11 +154,20 @@ struct RoDrive {
     uint32_t t, pp, al;
 };
 
-// outcome of readout m (strobe at t_lo with pulse registers pe / pp) of program
-// `prog`; acc = the accumulated {I, Q}.  t_ref: the lane's latest pulse_reset
+// frequency word of freq index fi from a program's table {off, len}
+// (dpemu_load_readout_freqs): 0 past its end
+__device__ __forceinline__ uint32_t ro_freq(const KParams &p, uint32_t off, uint32_t len, uint32_t fi)
+{
+    return fi < len ? p.ro_fq[off + fi] : 0u;
+}
+
+// outcome of readout m (strobe at t_lo with pulse registers pe / pp, LO
+// frequency word f_lo; the drive's f_d); acc = the accumulated {I, Q}.
+// t_ref: the lane's latest pulse_reset
 __device__ __forceinline__ uint32_t demod_readout(const KParams &p, uint64_t shot, uint32_t core, uint32_t m,
-                                                  uint32_t thr, uint32_t prog, uint32_t t_lo, uint32_t pe,
-                                                  uint32_t pp, const RoDrive d, uint32_t t_ref, int2 &acc)
+                                                  uint32_t thr, uint32_t t_lo, uint32_t pe, uint32_t pp,
+                                                  const RoDrive d, uint32_t t_ref, uint32_t f_lo, uint32_t f_d,
+                                                  int2 &acc)
 {
     const uint3 r = philox3(p.seed, shot, core, m);
     const uint32_t s = (thr == 0xFFFFFFFFu) || (r.x < thr);
@@ -169,10 +178,6 @@ __device__ __forceinline__ uint32_t demod_readout(const KParams &p, uint64_t sho
         const uint32_t a = max(r0, t_lo), e = min(t_lo + n_lo, r0 + n_d);
         if (e > a) {
             const uint32_t n = e - a;
-            const uint4 h = p.ro_hdr[prog];                      // drv_off, drv_len, lo_off, lo_len
-            const uint32_t fi_lo = (pp >> 17) & 0x1FFu, fi_d = (d.pp >> 17) & 0x1FFu;
-            const uint32_t f_lo = fi_lo < h.w ? p.ro_fq[h.z + fi_lo] : 0u;
-            const uint32_t f_d = fi_d < h.y ? p.ro_fq[h.x + fi_d] : 0u;
             const uint32_t beta = f_d - f_lo;
             const uint32_t th = s ? p.ro_theta1 : p.ro_theta0;
             const uint32_t alpha = beta * (a - t_ref) - f_d * p.ro_delay + (((d.pp & 0x1FFFFu) - (pp & 0x1FFFFu)) << 15) + th;

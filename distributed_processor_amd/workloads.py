@@ -183,7 +183,7 @@ CONFIG3_MEAS_LATENCY = READ_CLKS + 32   # rdlo strobe -> meas_valid, inside the 
 CONFIG3_DEMOD_LATENCY = 32              # DEMOD: the window (READ_CLKS) comes first, then this
 
 
-def config3_demod(ps, sigma=60.0, thr=0):
+def config3_demod(ps, sigma=220.0, thr=0):
     """The demodulation readout model (meas_model DEMOD, include/dpemu.h) for
     the readouts of ``ps`` (config 1-3 programs: rdrv at t, rdlo RDLO_DELAY
     later, both 2 us = 250 env words of 4 clocks): the ADC return arrives
@@ -193,8 +193,9 @@ def config3_demod(ps, sigma=60.0, thr=0):
     drive and LO words of its program (with equal drive and LO frequencies
     the demodulated phase is -F_d * delay + (phase_d - phase_lo) << 15 +
     theta_1, constant over the window).  sigma: the accumulated value's noise
-    scale (float, see make_config); 60 puts ~1 % of a 2-us readout's shots
-    on the wrong side.  Returns make_config's ``demod`` dict; meas_latency
+    scale (float, see make_config): the projected noise is 37837 * sigma
+    against a +-1.97e7 signal (0.6 amplitude, 1000 clocks), so 220 puts ~1 %
+    of the shots on the wrong side.  Returns make_config's ``demod`` dict; meas_latency
     CONFIG3_DEMOD_LATENCY keeps meas_valid where CONFIG3_MEAS_LATENCY put it."""
     import math
     w, d_off, d_len, l_off, l_len = ps.readout_freqs(RDRV, RDLO)

@@ -39,6 +39,12 @@ def workload(name):
                                p1={'ar': 0.5, 'ar0': 0.0, 'ar1': 1.0, 'ar0x32': 0.0, 'ar_sm': 0.5}[name],
                                lane_order=_abi.LANES_SHOT_MAJOR if name == 'ar_sm' else _abi.LANES_CORE_MAJOR)
         return ps, cfg, 1250000
+    if name == 'demod_sm':   # config 3 with the demodulation readout model, the bench's launch shape
+        ps = ProgramSet(workloads.config3_active_reset(8))
+        cfg = _abi.make_config(8, max_cycles=50000, event_cap=16, meas_cap=4,
+                               meas_latency=workloads.CONFIG3_DEMOD_LATENCY, seed=0x5EED, p1=0.5,
+                               lane_order=_abi.LANES_SHOT_MAJOR, demod=workloads.config3_demod(ps))
+        return ps, cfg, 1250000
     if name == 'lut_sm':   # config 3 through the fproc_lut back end, the bench's launch shape
         ps = ProgramSet(workloads.config3_lut(8))
         cfg = _abi.make_config(8, max_cycles=50000, event_cap=16, meas_cap=4, fproc_mode=_abi.FPROC_LUT,

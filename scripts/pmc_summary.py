@@ -40,7 +40,8 @@ import sys
 # branches, syncs), config 4 on macro_kernel, config 5 on dds_tile_kernel
 KERNELS = {'ramsey': ('straight_kernel',), 'active_reset': ('branch_kernel<11,', 'branch_kernel<3,', 'branch_kernel<11>', 'branch_kernel<3>'), 'rb': ('macro_kernel', 'macro_staged_kernel'),
            'dds': ('dds_tile_kernel',), 'dds_index': ('dds_index_kernel',), 'hist_reduce': ('hist_reduce_kernel',),
-           'config1': ('straight_kernel',), 'lut': ('branch_kernel<14,', 'branch_kernel<6,', 'branch_kernel<14>', 'branch_kernel<6>')}
+           'config1': ('straight_kernel',), 'lut': ('branch_kernel<14,', 'branch_kernel<6,', 'branch_kernel<14>', 'branch_kernel<6>'),
+           'demod': ('branch_kernel<75,', 'branch_kernel<67,', 'branch_kernel<75>', 'branch_kernel<67>')}
 # legs that share a kernel: the leg's launch grid (threads) picks its dispatches
 # (config 1: 10^6 single-core lanes; config 2: 10^6 shots x 8 cores)
 GRIDS = {'config1': (10 ** 6 + 255) // 256 * 256, 'ramsey': 8 * 10 ** 6}

@@ -221,7 +221,7 @@ def test_outcomes_drive_fproc_branches():
     from distributed_processor_amd.emulator import ProgramSet
     ps = ProgramSet(workloads.config3_active_reset(4))
     cfg = _abi.make_config(4, max_cycles=50000, event_cap=16, trace_cap=16, meas_cap=4, meas_latency=32,
-                           demod=workloads.config3_demod(ps, sigma=60.0))
+                           demod=workloads.config3_demod(ps))
     ro = ps.readout_freqs(RDRV, RDLO)
     fast = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, 0, 64, ro=ro)
     summ = _abi.unpack_summary(fast['summary'])

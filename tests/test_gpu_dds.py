@@ -246,6 +246,38 @@ def test_config5_slice(emu):
     check_equal(host(iq), ref, 'config5 slice')
 
 
+@pytest.mark.parametrize('layout', ['same_element_pairs', 'one_broken_pair'])
+def test_channel_pair_detection(emu, layout):
+    """the index kernel's pair mode (channels 2i and 2i + 1 on one lane share a
+    workgroup; its reset records are written for both): pairs whose two
+    channels play the SAME element (with different sample rates), and an
+    even channel list in which one pair breaks the shared-lane rule, so the
+    host falls back to one workgroup per channel -- both against oracle_dds"""
+    import torch
+    rng = np.random.default_rng(31 if layout == 'same_element_pairs' else 37)
+    cap, n_lanes, n_cycles = 96, 6, 1500
+    env_tab = pack_iq16(np.exp(1j * rng.uniform(0, 2 * np.pi, 2000)) * rng.uniform(0, 1, 2000))
+    freq_tab = np.concatenate([DDSElementConfig(samples_per_clk=16).get_freq_buffer([f])
+                               for f in (91.7e6, -13.1e6, 250e6)])
+    summary, ev = synthetic_timelines(rng, n_lanes, cap, n_cycles, 2000, 3)
+    desc = []
+    for L in range(n_lanes):
+        e = L % 4
+        desc.append((L, e, 16, 1, 0, 2000, 0, len(freq_tab)))
+        desc.append((L, e if layout == 'same_element_pairs' else (e + 1) % 4, 8, 4, 0, 2000, 0, len(freq_tab)))
+    if layout == 'one_broken_pair':
+        desc[7] = (4,) + desc[7][1:]                    # pair 3: lanes 3 and 4 -- not one lane
+    desc = np.array(desc, np.uint32)
+    n_samples = 16 * n_cycles + 4 * 5
+    ref = oracle.dds(desc, summary, ev, env_tab, freq_tab, n_samples, cap)
+    dev = {'summary': torch.from_numpy(summary.view(np.int32)).cuda(),
+           'events': torch.from_numpy(ev.view(np.int32)).cuda()}
+    iq = emu.synthesize(plan_from(desc, env_tab, freq_tab, n_lanes, cap), dev, n_samples)
+    torch.cuda.synchronize()
+    check_equal(host(iq), ref, layout)
+    assert (ref != 0).sum() > 5000
+
+
 def test_global_record_fallback(emu):
     """a staged 32-KiB envelope leaves room for only DDS_REC_LDS_MIN records in
     a tile workgroup's LDS: stripes with denser windows read their strobes and
