@@ -59,7 +59,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s
-PROFILE_TAG = 'r05'            # profiles/<tag>_*: rocprofv3 kernel stats and PMC passes of this bench
+PROFILE_TAG = 'r06'            # profiles/<tag>_*: rocprofv3 kernel stats and PMC passes of this bench
 
 
 def _valu_peak():

@@ -10,7 +10,7 @@ set -e
 peak=$1; pmc=$2; tag=$3; out=$4
 cd "$(dirname "$0")/.."
 tmp=$(mktemp -d)
-for f in straight branch macro dds; do
+for f in straight branch branch_demod macro dds; do
     (cd $tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC --save-temps -c \
         -o $tmp/$f.o $OLDPWD/distributed_processor_amd/csrc/$f.hip 2>/dev/null)
 done
@@ -22,13 +22,15 @@ args=(
     $(mix straight '_ZN5dpemu15straight_kernelILi0ELi1EE' straight_rows_fb1)
     $(mix branch '_ZN5dpemu13branch_kernelILi11ELi8EE' branch_11_8)
     $(mix branch '_ZN5dpemu13branch_kernelILi14ELi8EE' branch_14_8)
-    $(mix macro '_ZN5dpemu19macro_staged_kernelILi2ELb1EE' macro_staged_2_addid)
+    $(mix branch_demod '_ZN5dpemu13branch_kernelILi75ELi8EE' branch_75_8)
+    $(mix macro '_ZN5dpemu19macro_staged_kernelILi2ELb1ELi8EE' macro_staged_2_addid)
     $(mix dds '_ZN5dpemu15dds_tile_kernelE' dds_tile)
 )
 python3 scripts/kernel_valu_peak.py $peak "${args[@]}" \
     --pmc "straight_kernelILi0ELi1=$pmc/${tag}_ramsey_pmc.json" \
     --pmc "branch_kernelILi11=$pmc/${tag}_active_reset_pmc.json" \
     --pmc "branch_kernelILi14=$pmc/${tag}_lut_pmc.json" \
+    --pmc "branch_kernelILi75=$pmc/${tag}_demod_pmc.json" \
     --pmc "macro_staged_kernel=$pmc/${tag}_rb_pmc.json" \
     --pmc "dds_tile_kernel=$pmc/${tag}_dds_pmc.json" \
     --validation profiles/r05_valu_model_check.json --out $out
