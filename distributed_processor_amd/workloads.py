@@ -10,8 +10,10 @@ mirroring what distproc's compiler + assembler emit for the same circuits
 * config 2 -- 8-core Ramsey sweep, 100 delay points selected by shot
 * config 3 -- 8-core active reset: sync, read, hold, jump_fproc on the own
               measurement, conditional X180, sync, read
-* config 4 -- 2-qubit randomized benchmarking, depth-D random Clifford
-              sequences with virtual-Z phase registers (long programs)
+* config 4 -- RB-shaped 2-qubit sequences: depth-D random single-qubit
+              Cliffords + cross-resonance pulses with virtual-Z phase
+              registers (long programs; no CNOT decomposition or recovery
+              Clifford, see config4_rb)
 
 Channel layout per core follows python/test/channel_config.json: element 0
 qdrv (16 samples/clk), element 1 rdrv (16/clk, interp 16), element 2 rdlo
@@ -320,9 +322,16 @@ def _rb_builder(c):
 
 
 def config4_rb(n_seq=1000, depth=200, seed=0x5EED, n_cores=2, first=0):
-    """2-qubit RB-like sequences: per layer each qubit plays a random Clifford
-    (<= 2 X90 pulses on X or Y, virtual Z by reg_alu on its phase register), and
-    with probability 1/2 a cross-resonance pulse on core 0.  Layers are
+    """RB-SHAPED 2-qubit sequences (the program shape of BASELINE configs[3],
+    not its full circuit): per layer each qubit plays a random single-qubit
+    Clifford (<= 2 X90 pulses on X or Y, virtual Z by reg_alu on its phase
+    register), and with probability 1/2 a cross-resonance pulse on core 0;
+    then one readout per core.  There is no CNOT decomposition of two-qubit
+    Cliffords and no recovery Clifford (SURVEY.md §8(d)4 asks for both), so
+    the sequences do not return the qubits to |00>: what the emulator's
+    throughput depends on -- depth-200 programs of ~740 commands, ~7
+    different programs per wave, register phase updates, data-dependent
+    pulse counts -- is kept, the circuit's meaning is not.  Layers are
     fixed-length so the cores stay aligned.  Returns n_seq assembled-program
     dicts for global sequences [first, first + n_seq) -- the per-command
     reference for :func:`config4_rb_set`, which builds the same machine code

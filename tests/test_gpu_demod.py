@@ -205,3 +205,20 @@ def test_gpu_detuned_lo_collapses_separation(emu):
     assert means['detuned'] < 0.01 * means['tuned']
     g, st = _assign_gpu(emu, f_lo=(0x12345678 - det) & 0xFFFFFFFF)
     assert 0.45 < (g['meas'][0, :, 1] == st).mean() < 0.55
+
+
+def test_demod_sharding_invariance(emu):
+    """shards of a DEMOD run (global shot offsets) equal the unsharded run in
+    every output, the accumulated I/Q included: the noise and state draws are
+    keyed by the global shot index, as for the other models"""
+    ps = ProgramSet(workloads.config3_active_reset(8))
+    cfg = config3_demod_cfg(ps)
+    emu.load(ps)
+    outs = ('summary', 'events', 'meas', 'acc')
+    whole = emu.run(3000, 500, cfg=cfg, outputs=outs).arrays
+    parts = [emu.run(n, s0, cfg=cfg, outputs=outs).arrays for s0, n in ((500, 1000), (1500, 1200), (2700, 800))]
+    for k in outs:
+        lane_axis = 0 if k == 'summary' else 1
+        per = [_abi.by_shot(p[k], 8, axis=lane_axis) for p in parts]          # (..., core, shot, ...)
+        got = np.concatenate(per, axis=lane_axis + 1)
+        np.testing.assert_array_equal(got, _abi.by_shot(whole[k], 8, axis=lane_axis), err_msg=k)
