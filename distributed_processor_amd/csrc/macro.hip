@@ -697,6 +697,32 @@ struct MacroLane {
     }
 };
 
+#ifdef DPEMU_PROBE_WAVETIME
+// probe builds only (scripts/wavetime_probe.py): per wave, its start and end on
+// the 100-MHz wall clock, HW_ID and XCC_ID, so the occupancy of the launch over
+// time (its tail) can be read back
+__device__ uint32_t g_wavetime[4u << 18];
+__device__ __forceinline__ void probe_wavetime(uint32_t t0, uint32_t wv)
+{
+    const uint32_t w = blockIdx.x * (BLOCK / 64) + wv;
+    if ((threadIdx.x & 63) == 0 && w < (1u << 18)) {
+        const uint32_t t1 = (uint32_t)wall_clock64();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        *(uint4 *)&g_wavetime[4u * w] = make_uint4(t0, t1, hw, xcc);
+    }
+}
+extern "C" int dpemu_probe_wavetime(void *dst, size_t bytes, int reset)
+{
+    if (reset) {
+        void *a = nullptr;
+        if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_wavetime)) != hipSuccess) return -1;
+        return hipMemset(a, 0, sizeof(g_wavetime)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wavetime), bytes < sizeof(g_wavetime) ? bytes : sizeof(g_wavetime)) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
+
 // NSL: program slots per wave -- MACRO_SLOTS, or MACRO_SLOTS_WIDE (NR == 2
 // only) for runs whose waves span more programs (fewer shots per program);
 // the wide chunks (48 KiB per workgroup) hold 3 workgroups per CU
@@ -721,6 +747,9 @@ __attribute__((amdgpu_waves_per_eu(NR == 16 || NSL > (int)MACRO_SLOTS ? 3 : 4)))
     extern __shared__ uint32_t s_hist[];              // HIST_LDS_MAX words when p.hist_lds (dynamic)
     const uint32_t tid = threadIdx.x, wv = tid >> 6, wl = tid & 63;
     const uint32_t C = p.C;
+#ifdef DPEMU_PROBE_WAVETIME
+    const uint32_t pt0 = (uint32_t)wall_clock64();
+#endif
     uint32_t sl, core;
     clear_hist_next(p);
     block_core_major(p, sl, core);
@@ -848,11 +877,17 @@ __attribute__((amdgpu_waves_per_eu(NR == 16 || NSL > (int)MACRO_SLOTS ? 3 : 4)))
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         stage(c + 1u, s_chunk1[wv], s_info1[wv]);
+#ifdef DPEMU_PROBE_DMA2
+        stage(c + 1u, s_chunk1[wv], s_info1[wv]);   // probe: every chunk fetched twice
+#endif
         phase(s_chunk0[wv], s_info0[wv]);
         if (!__ballot(L.st == 0u)) break;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         stage(c + 2u, s_chunk0[wv], s_info0[wv]);
+#ifdef DPEMU_PROBE_DMA2
+        stage(c + 2u, s_chunk0[wv], s_info0[wv]);
+#endif
         phase(s_chunk1[wv], s_info1[wv]);
     }
     // no LDS DMA may still be in flight when the workgroup's LDS is released
@@ -872,6 +907,9 @@ __attribute__((amdgpu_waves_per_eu(NR == 16 || NSL > (int)MACRO_SLOTS ? 3 : 4)))
                 ((p.reg_used >> r) & 1u) ? L.reg_rd((uint32_t)(p.reg_map >> (4 * r)) & 15u) : 0u;
     }
     count_outcome_block(p, s_hist, s_key, valid, core, sl, valid ? shot_group(p, sl) : 0u, L.last_bit);
+#ifdef DPEMU_PROBE_WAVETIME
+    probe_wavetime(pt0, wv);
+#endif
 }
 
 hipError_t launch_macro(const KParams &p, uint32_t slots, int nr, bool addid, hipStream_t stream)
