@@ -366,7 +366,13 @@ struct MacroLane {
         qa_t = 1; qa_q = 0;
         flags = n_ev = n_meas = meas_bits = last_bit = n_tr = k = 0;
         st = valid ? 0u : ST_DONE;
+#ifdef DPEMU_PROBE_WAVEBLOCK
+        // probe: a wave's records in one contiguous block, slot-major within
+        // it (outputs differ by design)
+        evp = p.events + (uint64_t)(lane >> 6) * 64u * p.event_cap + (lane & 63u);
+#else
         evp = p.events + lane;
+#endif
         tr_on = p.trace != nullptr && p.trace_cap != 0u;
         ev_on = p.events != nullptr;
     }
@@ -401,7 +407,11 @@ struct MacroLane {
         if (ok) {
             if (n_ev < p.event_cap && ev_on)
                 *evp = event_record(te, pe, pp, pa, kind);
+#ifdef DPEMU_PROBE_WAVEBLOCK
+            evp += 64u;
+#else
             evp += p.n_lanes;
+#endif
             n_ev++;
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {        // meas_elem 0xFF: none
                 const uint32_t bit = meas_bit(p, p.shot_begin + sl, core, n_meas, p.p1_thr[core], pa, pe);
