@@ -696,18 +696,20 @@ def leg_active_reset(emu, args, world, rank, stream, lut=False, demod=False):
 
 
 def leg_rb(emu, args, world, rank, stream):
-    """config 4 at its stated size: 10^5 distinct 2-core RB sequences of depth
-    200 (1.5*10^8 commands, a 2.4 GB program image), 10 shots each = 10^6
-    shots = 2*10^6 lanes per GPU.  Branch-free programs with register
-    commands: macro_kernel.  Divergent: a wave's lanes run ~7 different
-    programs.  VALU-bound: the roofline is VALU issue against
+    """config 4 at its stated size: 10^5 distinct two-qubit Clifford RB
+    sequences of depth 200 plus their recovery Cliffords (workloads.config4_rb2q:
+    X90 / Y90 / X-90 / Y-90, virtual Z, CNOT by cross resonance; ~1,300
+    commands per core, 2.6*10^8 commands, a 4.2 GB program image), 10 shots
+    each = 10^6 shots = 2*10^6 lanes per GPU.  Branch-free programs with
+    register commands: macro_staged_kernel.  Divergent: a wave's lanes run ~7
+    different programs.  VALU-bound: the roofline is VALU issue against
     the measured peak, with the VALU ops per emulated instruction and the
     active lanes per VALU instruction (divergence) from the PMC pass."""
     import torch
     from distributed_processor_amd import _abi, isa, sharding, workloads
     from distributed_processor_amd.emulator import RunPipeline, alloc_device_outputs
     t0 = time.perf_counter()
-    ps = workloads.config4_rb_set(args.rb_seqs, 200)
+    ps = workloads.config4_rb2q_set(args.rb_seqs, 200)
     gen_s = time.perf_counter() - t0
     emu.load(ps)
     torch.cuda.synchronize()
@@ -776,14 +778,14 @@ def leg_rb(emu, args, world, rank, stream):
                     active_lanes_per_valu_pct=prof.get('valu_lane_util_pct'), traffic=hbm['traffic'], hbm=hbm)
     else:
         roof = hbm
-    res = {'metric': 'emulated core-shots/s (config 4: 2-qubit RB, 1e5 sequences x depth 200, 10 shots each)',
+    res = {'metric': 'emulated core-shots/s (config 4: 2-qubit Clifford RB, 1e5 sequences x depth 200 + recovery, 10 shots each)',
            'value': n * 2 * world * steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * steps / dt,
            'ms_per_step': ms_step, 'kernel_ms': kernel_ms, 'steps': steps,
            'serial_ms_per_step': dt_serial / steps * 1e3, 'step_mode': mode,
            'batches_in_flight': depth if mode == 'pipelined' else 1,
            'instructions_per_s': instrs * world * steps / dt,
            'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * steps / dt,
-           'config': {'workload': 'config4_rb_2core_1e5seq_depth200', 'sequences': args.rb_seqs,
+           'config': {'workload': 'config4_rb2q_2core_1e5seq_depth200', 'sequences': args.rb_seqs,
                       'lane_order': LANE_ORDER_NAMES[cfg.lane_order],
                       'shots_per_sequence': args.rb_spg, 'shots_per_gpu': n, 'commands': int(ps.words.shape[0]),
                       'program_image_bytes': int(ps.words.nbytes), 'event_cap': cfg.event_cap,

@@ -10,10 +10,14 @@ mirroring what distproc's compiler + assembler emit for the same circuits
 * config 2 -- 8-core Ramsey sweep, 100 delay points selected by shot
 * config 3 -- 8-core active reset: sync, read, hold, jump_fproc on the own
               measurement, conditional X180, sync, read
-* config 4 -- RB-shaped 2-qubit sequences: depth-D random single-qubit
-              Cliffords + cross-resonance pulses with virtual-Z phase
-              registers (long programs; no CNOT decomposition or recovery
-              Clifford, see config4_rb)
+* config 4 -- two-qubit Clifford randomized benchmarking (config4_rb2q):
+              depth-D random elements of the 11,520-element group and the
+              recovery Clifford, decomposed into X90 / Y90 / X-90 / Y-90,
+              virtual Z on a frame register, and CNOT by cross resonance
+              (clifford2q.py); config4_rb is the older RB-SHAPED generator
+              (single-qubit Cliffords + random CR pulses, no recovery), kept as
+              a source of small divergent register programs for kernel tests
+              and as the DDS leg's 8-core timelines
 
 Channel layout per core follows python/test/channel_config.json: element 0
 qdrv (16 samples/clk), element 1 rdrv (16/clk, interp 16), element 2 rdlo
@@ -22,6 +26,7 @@ qdrv (16 samples/clk), element 1 rdrv (16/clk, interp 16), element 2 rdlo
 
 from __future__ import annotations
 
+import functools
 import os
 from collections import OrderedDict
 from typing import Dict, List, Sequence
@@ -70,14 +75,14 @@ class CoreBuilder:
             self._freqs[elem].append(f)
         return self.elems[elem].get_freq_addr(self._freqs[elem].index(f))
 
-    def pulse(self, elem, freq, phase, amp, env, t=None, phase_reg=None, amp_reg=None):
+    def pulse(self, elem, freq, phase, amp, env, t=None, phase_reg=None, amp_reg=None, phase_word=None):
         e = self.elems[elem]
         kw = dict(freq_word=self.freq_addr(elem, freq), env_word=self.env_word(elem, env),
                   cfg_word=e.get_cfg_word(elem, None), cmd_time=t)
         if phase_reg is not None:
             kw['phase_regaddr'] = phase_reg
         else:
-            kw['phase_word'] = e.get_phase_word(phase)
+            kw['phase_word'] = e.get_phase_word(phase) if phase_word is None else int(phase_word)
         if amp_reg is not None:
             kw['amp_regaddr'] = amp_reg
         else:
@@ -471,5 +476,262 @@ def config4_rb_set(n_seq=100000, depth=200, seed=0x5EED, n_cores=2, chunk=8192):
         n_instr = np.append(n_instr, np.uint32(0))
         offsets = np.append(offsets, np.uint64(len(words)))
     bufs = {c: _rb_templates(c)[1] for c in range(n_cores)}
+    return ProgramSet.from_arrays(words, offsets.astype(np.uint32), n_instr, table.reshape(-1), n_seq, C_,
+                                  buffers=_SharedBuffers(bufs))
+
+
+# ------------------------------------------------ config 4: two-qubit Clifford RB
+# random two-qubit Cliffords of depth D, each sequence closed
+# by its recovery Clifford, decomposed into X90 / Y90 / X-90 / Y-90 pulses,
+# virtual Z (reg_alu on the frame register) and CNOT (a cross-resonance ZX90
+# on the control's drive at the target's frequency, S-dagger on the control,
+# X-90 on the target); the group, its decompositions and the native-operation
+# conventions are in clifford2q.py.  Cores (2p, 2p + 1) are qubit pair p
+# (control, target); every pair runs its own sequence (simultaneous RB).
+# Every element is a run of fixed-length stages -- C1 (x) C1 layers and CNOTs
+# alternating -- on a schedule both cores of the pair share, so the CR pulse
+# and the target's X-90 line up.
+RB2_STAGE_CLKS = 2 * X90_CLKS + 8   # a C1 layer (<= 2 pulses per qubit) or a CNOT (CR, then the target's X-90)
+RB2_T0 = 10
+RB2_CR_AMP = 0.3
+# machine-command templates of one core (rb2q_templates): index -> command
+(_R2_RESET, _R2_INIT) = range(2)
+_R2_AXIS = 2            # + a: TREG = PREG + a quarter turns
+_R2_PULSE = 6           # X90-envelope pulse, phase from TREG
+_R2_Z = 6               # + k (k = 1..3): PREG += k quarter turns
+_R2_CR = 10             # + ph: cross-resonance pulse at immediate phase ph quarter turns (control cores)
+(_R2_RDRV, _R2_RDLO, _R2_DONE) = (14, 15, 16)
+_R2_MAXC = 26           # commands of one element on one core, at most (4 C1 layers of 5, 3 CNOTs of 2)
+
+
+def rb2q_draws(seqs, depth, n_pairs, seed=0x5EED):
+    """Two-qubit Clifford indices [len(seqs), n_pairs, depth + 1] of RB
+    sequences ``seqs`` (global indices): depth counter-based random elements
+    (a hash of (seed, sequence, layer, pair), as rb_draws) and, last, the
+    recovery element that returns the pair to the identity."""
+    from . import clifford2q
+    if depth >= 1 << 16 or n_pairs >= 255:
+        raise ValueError('depth < 65536 and fewer than 255 pairs')
+    s = np.asarray(seqs, np.uint64).reshape(-1, 1, 1)
+    d = np.arange(depth, dtype=np.uint64).reshape(1, 1, -1)
+    j = np.arange(n_pairs, dtype=np.uint64).reshape(1, -1, 1)
+    with np.errstate(over='ignore'):
+        key = (np.uint64((int(seed) * 0xD1B54A32D192ED03) & (2 ** 64 - 1))
+               + ((s << np.uint64(24)) | (d << np.uint64(8)) | j))
+    el = (_mix64(key) % np.uint64(clifford2q.N_C2)).astype(np.int64)
+    tab = clifford2q.table()
+    u = np.broadcast_to(np.eye(4, dtype=np.complex128), el.shape[:2] + (4, 4)).copy()
+    for k in range(depth):
+        u = np.matmul(tab.u[el[:, :, k]], u)
+    rec = tab.index(np.conj(np.swapaxes(u, -1, -2))).reshape(el.shape[:2])
+    return np.concatenate([el, rec[:, :, None]], axis=2)
+
+
+def _rb2q_role_cmds(layers, control):
+    """(template, stage, clock offset in the stage, target-frame quarter turns
+    before it) of one element's commands on the control or target core, and
+    the element's stage count and net target-frame turns"""
+    from . import clifford2q
+    cmds, f_t = [], 0
+    for st, (i0, i1) in enumerate(layers):
+        if st:                                          # a CNOT before every layer but the first
+            if control:
+                cmds += [(_R2_CR, 2 * st - 1, 0, f_t), (_R2_Z + 1, 2 * st - 1, 0, 0)]
+            else:
+                cmds += [(_R2_AXIS + 2, 2 * st - 1, 0, 0), (_R2_PULSE, 2 * st - 1, X90_CLKS, 0)]
+        pre, k = clifford2q.c1_ops(i0 if control else i1)
+        for n_, a in enumerate(pre):
+            cmds += [(_R2_AXIS + a, 2 * st, 0, 0), (_R2_PULSE, 2 * st, X90_CLKS * n_, 0)]
+        if k:
+            cmds.append((_R2_Z + k, 2 * st, 0, 0))
+        f_t = (f_t + clifford2q.c1_ops(i1)[1]) % 4
+    return cmds, 2 * len(layers) - 1, f_t
+
+
+@functools.lru_cache(maxsize=1)
+def _rb2q_tables():
+    """per element and role: template ids [N_C2, _R2_MAXC] (-1 = none), clock
+    offsets (-1: untimed), CR target-frame offsets; stages, net target-frame
+    turns and command counts"""
+    from . import clifford2q
+    tab = clifford2q.table()
+    ids = np.full((2, clifford2q.N_C2, _R2_MAXC), -1, np.int8)
+    dt = np.zeros((2, clifford2q.N_C2, _R2_MAXC), np.int32)
+    crf = np.zeros((clifford2q.N_C2, _R2_MAXC), np.int8)
+    stages = np.zeros(clifford2q.N_C2, np.int64)
+    f_t = np.zeros(clifford2q.N_C2, np.int64)
+    ncmd = np.zeros((2, clifford2q.N_C2), np.int64)
+    for e, layers in enumerate(tab.layers):
+        for role in (0, 1):
+            cmds, stages[e], f = _rb2q_role_cmds(layers, role == 0)
+            ncmd[role, e] = len(cmds)
+            for i, (tid, st, off, fr) in enumerate(cmds):
+                ids[role, e, i] = tid
+                dt[role, e, i] = st * RB2_STAGE_CLKS + off if tid in (_R2_PULSE, _R2_CR) else -1
+                if role == 0:
+                    crf[e, i] = fr
+            f_t[e] = f
+    return ids, dt, crf, stages, f_t, ncmd
+
+
+def _rb2q_builder(c, n_cores):
+    """CoreBuilder with core c's RB tables registered in a fixed order"""
+    b = CoreBuilder()
+    b.env_word(QDRV, X90_ENV)
+    b.freq_addr(QDRV, qubit_params(c)['fq'])
+    if c % 2 == 0 and c + 1 < n_cores:
+        b.freq_addr(QDRV, qubit_params(c + 1)['fq'])   # cross-resonance drive at the target's frequency
+    return b
+
+
+def config4_rb2q(n_seq=1000, depth=200, seed=0x5EED, n_cores=2, first=0):
+    """Two-qubit Clifford RB (BASELINE configs[3]): per qubit
+    pair (cores 2p, 2p + 1) ``depth`` random two-qubit Cliffords and the
+    recovery Clifford, each decomposed as clifford2q describes, then one
+    readout per core.  The physical pulse sequence is the identity up to a Z
+    rotation per qubit (tests/test_rb2q.py).  Returns n_seq assembled-program
+    dicts for global sequences [first, first + n_seq) -- the per-command
+    reference for :func:`config4_rb2q_set`, which builds the same machine code
+    vectorised."""
+    from . import clifford2q
+    if n_cores % 2:
+        raise ValueError('config4_rb2q runs qubit pairs: n_cores must be even')
+    el = rb2q_draws(np.arange(first, first + n_seq), depth, n_cores // 2, seed)
+    tab = clifford2q.table()
+    groups = []
+    for s in range(n_seq):
+        prog = {}
+        for c in range(n_cores):
+            q, control = qubit_params(c), c % 2 == 0
+            f_tgt = qubit_params(c + 1)['fq'] if control else None
+            b = _rb2q_builder(c, n_cores)
+            b.emit(isa.pulse_reset())
+            b.emit(isa.alu_cmd('reg_alu', 'i', 0, 'id0', 0, RB_PREG))
+            t0, f_t = RB2_T0, 0                            # element start, target frame (quarter turns)
+            for e in el[s, c // 2]:
+                cmds, n_st, df = _rb2q_role_cmds(tab.layers[e], control)
+                for tid, st, off, fr in cmds:
+                    t = t0 + st * RB2_STAGE_CLKS + off
+                    if tid == _R2_CR:
+                        b.pulse(QDRV, f_tgt, 0.0, RB2_CR_AMP, X90_ENV, t,
+                                phase_word=((f_t + fr) % 4) * RB_QUARTER)
+                    elif tid == _R2_PULSE:
+                        b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, t, phase_reg=RB_TREG)
+                    elif tid >= _R2_Z + 1:
+                        b.emit(isa.alu_cmd('reg_alu', 'i', (tid - _R2_Z) * RB_QUARTER, 'add', RB_PREG, RB_PREG))
+                    else:
+                        b.emit(isa.alu_cmd('reg_alu', 'i', (tid - _R2_AXIS) * RB_QUARTER, 'add', RB_PREG, RB_TREG))
+                t0 += n_st * RB2_STAGE_CLKS
+                f_t = (f_t + df) % 4
+            readout(b, q, t0)
+            b.emit(isa.done_cmd())
+            prog[str(c)] = b.assembled()
+        groups.append(prog)
+    return groups
+
+
+@functools.lru_cache(maxsize=64)
+def _rb2q_templates(c, n_cores):
+    """core c's command templates (cmd_time 0), indexed by the _R2_* ids, and its env / freq buffers"""
+    q, control = qubit_params(c), c % 2 == 0
+    b = _rb2q_builder(c, n_cores)
+    b.emit(isa.pulse_reset())
+    b.emit(isa.alu_cmd('reg_alu', 'i', 0, 'id0', 0, RB_PREG))
+    for a in range(4):
+        b.emit(isa.alu_cmd('reg_alu', 'i', a * RB_QUARTER, 'add', RB_PREG, RB_TREG))
+    b.pulse(QDRV, q['fq'], 0.0, q['ax90'], X90_ENV, 0, phase_reg=RB_TREG)
+    for k in (1, 2, 3):
+        b.emit(isa.alu_cmd('reg_alu', 'i', k * RB_QUARTER, 'add', RB_PREG, RB_PREG))
+    for ph in range(4):
+        if control:
+            b.pulse(QDRV, qubit_params(c + 1)['fq'], 0.0, RB2_CR_AMP, X90_ENV, 0, phase_word=ph * RB_QUARTER)
+        else:
+            b.emit(isa.done_cmd())                      # (no CR on target cores: never used)
+    b.pulse(RDRV, q['fr'], 0.0, q['ar'], RDRV_ENV, 0)
+    b.pulse(RDLO, q['fr'], q['rdlo_phase'], 1.0, RDLO_ENV, 0)
+    b.emit(isa.done_cmd())
+    return isa.words_to_u32(b.words), b.buffers()
+
+
+def rb2q_core_words(el_p, c, n_cores):
+    """Machine code of core c for a batch of sequences of its pair, vectorised:
+    (words (n, 4) u32 of all programs back to back, n_instr per sequence).
+    el_p: [n_seq, depth + 1] element indices (rb2q_draws)."""
+    ids_t, dt_t, crf_t, stages_t, ft_t, ncmd_t = _rb2q_tables()
+    role = c % 2
+    tmpl, _ = _rb2q_templates(c, n_cores)
+    n, L = el_p.shape
+    st = stages_t[el_p]
+    start = RB2_T0 + RB2_STAGE_CLKS * (np.cumsum(st, axis=1) - st)            # [n, L] element start cycles
+    cnt = ncmd_t[role][el_p]                                                  # [n, L] commands per element
+    # one entry per command of the body, sequence after sequence: its element and index in it
+    e_flat = np.repeat(el_p.ravel(), cnt.ravel())
+    first = np.repeat(np.cumsum(cnt.ravel()) - cnt.ravel(), cnt.ravel())
+    j = np.arange(len(e_flat)) - first
+    ids = ids_t[role][e_flat, j].astype(np.int64)
+    dt = dt_t[role][e_flat, j]
+    tt = np.where(dt >= 0, np.repeat(start.ravel(), cnt.ravel()) + dt, 0)
+    if role == 0:
+        f_t = ft_t[el_p]
+        f_entry = (np.cumsum(f_t, axis=1) - f_t) % 4
+        ids = np.where(ids == _R2_CR, _R2_CR + (np.repeat(f_entry.ravel(), cnt.ravel()) + crf_t[e_flat, j]) % 4, ids)
+    body = cnt.sum(axis=1)                                                    # [n]
+    n_instr = (body + 5).astype(np.uint32)                                    # + reset, init, rdrv, rdlo, done
+    t_ro = RB2_T0 + RB2_STAGE_CLKS * st.sum(axis=1)
+    # assemble: head (2), body, tail (3) per sequence
+    out_ids = np.empty(int(n_instr.sum()), np.int64)
+    out_t = np.zeros(len(out_ids), np.int64)
+    seq_start = np.cumsum(n_instr.astype(np.int64)) - n_instr
+    pos = np.repeat(seq_start + 2 - np.cumsum(body) + body, body) + np.arange(len(ids))
+    out_ids[pos] = ids
+    out_t[pos] = tt
+    for k, (tid, tv) in enumerate(((_R2_RESET, 0), (_R2_INIT, 0))):
+        out_ids[seq_start + k] = tid
+    tail0 = seq_start + 2 + body
+    out_ids[tail0], out_t[tail0] = _R2_RDRV, t_ro
+    out_ids[tail0 + 1], out_t[tail0 + 1] = _R2_RDLO, t_ro + RDLO_DELAY
+    out_ids[tail0 + 2] = _R2_DONE
+    words = tmpl[out_ids]
+    ts = out_t.astype(np.uint32)
+    words[:, 0] |= ts << np.uint32(5)                   # cmd_time = cmd[36:5] (template field 0)
+    words[:, 1] |= ts >> np.uint32(27)
+    return words, n_instr
+
+
+def config4_rb2q_set(n_seq=100000, depth=200, seed=0x5EED, n_cores=2, chunk=4096):
+    """Config 4 at its stated size as a ProgramSet, generated vectorised:
+    group g = RB sequence g, program of (g, c) = c * n_seq + g (core-major
+    blocks).  Machine code identical to ``config4_rb2q`` (tests/test_rb2q.py)."""
+    from .emulator import ProgramSet
+    if n_cores % 2:
+        raise ValueError('config4_rb2q runs qubit pairs: n_cores must be even')
+    C_ = 1
+    while C_ < n_cores:
+        C_ <<= 1
+    _rb2q_tables()                                      # (built once, before the threads)
+    from concurrent.futures import ThreadPoolExecutor
+    starts = list(range(0, n_seq, chunk))
+
+    def one(s0):                                        # numpy releases the GIL in the bulk ops
+        el = rb2q_draws(np.arange(s0, min(s0 + chunk, n_seq)), depth, n_cores // 2, seed)
+        return [rb2q_core_words(el[:, c // 2], c, n_cores) for c in range(n_cores)]
+    with ThreadPoolExecutor(max(1, min(8, len(starts), os.cpu_count() or 1))) as pool:
+        parts = list(pool.map(one, starts))
+    blocks = [parts[i][c] for c in range(n_cores) for i in range(len(starts))]
+    n_instr = np.concatenate([b[1] for b in blocks])
+    words = np.concatenate([b[0] for b in blocks]) if blocks else np.zeros((1, 4), np.uint32)
+    del parts, blocks
+    offsets = np.zeros(len(n_instr), np.uint64)
+    np.cumsum(n_instr[:-1], out=offsets[1:])
+    if offsets[-1] + n_instr[-1] >= 2 ** 32:
+        raise ValueError('program set exceeds 2^32 commands')
+    table = np.zeros((n_seq, C_), np.uint32)
+    empty = len(n_instr)
+    for c in range(C_):
+        table[:, c] = c * n_seq + np.arange(n_seq) if c < n_cores else empty
+    if C_ > n_cores:
+        n_instr = np.append(n_instr, np.uint32(0))
+        offsets = np.append(offsets, np.uint64(len(words)))
+    bufs = {c: _rb2q_templates(c, n_cores)[1] for c in range(n_cores)}
     return ProgramSet.from_arrays(words, offsets.astype(np.uint32), n_instr, table.reshape(-1), n_seq, C_,
                                   buffers=_SharedBuffers(bufs))

@@ -295,6 +295,19 @@ def test_config4_rb(emu):
     compare_all(g, f)
 
 
+@pytest.mark.parametrize('n_cores,order', [(2, 'core'), (2, 'shot'), (4, 'core')])
+def test_config4_rb2q(emu, n_cores, order):
+    """two-qubit Clifford RB programs (config 4's generator, CNOTs and
+    recovery Cliffords), every output against oracle_fast in both lane orders
+    and with 4 cores (two pairs)"""
+    ps = ProgramSet(workloads.config4_rb2q(n_seq=24, depth=30, n_cores=n_cores))
+    cfg = _abi.make_config(n_cores, n_groups=24, shots_per_group=5, max_cycles=400000, event_cap=300,
+                           trace_cap=600, meas_cap=4, seed=3, p1=0.3,
+                           lane_order=_abi.LANES_SHOT_MAJOR if order == 'shot' else _abi.LANES_CORE_MAJOR)
+    g, f = run_pair(emu, ps, cfg, 24 * 5)
+    compare_all(g, f, 'rb2q C {} {}'.format(n_cores, order))
+
+
 @pytest.mark.parametrize('mode', ['meas', 'lut'])
 def test_lut_and_meas_fuzz_many_shots(emu, mode):
     for seed in range(6):

@@ -1,7 +1,10 @@
 """Config 4 at its stated size on the GPU (BASELINE.json configs[3]):
-10^5 distinct 2-core randomized-benchmarking sequences of depth 200 (about
-1.5 * 10^8 commands, a 2.4 GB device-resident program image), 10 shots per
-sequence = 10^6 shots = 2 * 10^6 (shot, core) lanes in one launch.
+10^5 distinct two-qubit Clifford RB sequences of depth 200 plus their
+recovery Cliffords (workloads.config4_rb2q: about 2.6 * 10^8 commands, a
+4.2 GB device-resident program image), 10 shots per sequence = 10^6 shots =
+2 * 10^6 (shot, core) lanes in one launch.  (The kernel-edge tests below use
+the RB-shaped generator workloads.config4_rb_set: small tables of the same
+program class.)
 
 * bit-exact, the WHOLE launch: all 10^6 shots (2 * 10^6 lanes) compared
   with oracle_fast on every output array -- summaries, event records,
@@ -35,7 +38,7 @@ WINDOWS, WIN = 50, 40
 @pytest.fixture(scope='module')
 def rb():
     import torch
-    ps = workloads.config4_rb_set(N_SEQ, DEPTH)
+    ps = workloads.config4_rb2q_set(N_SEQ, DEPTH)
     ops = ps.words[:, 3] >> 28
     strobes = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
                               ps.offsets.astype(np.int64))
