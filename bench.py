@@ -533,15 +533,23 @@ def leg_config1(emu, args, world, rank, stream):
 
 
 def leg_dds(emu, args, world, rank, stream):
-    """config 5: DDS over the config-4 RB timelines, 8 cores x {qdrv, rdrv}"""
+    """config 5: DDS over the config-4 RB timelines, 8 cores x {qdrv, rdrv}
+    (--dds-workload rb2q: four qubit pairs of two-qubit Clifford RB, config 4's
+    generator; rb: the RB-shaped 8-core timelines of rounds 2-6)"""
     import torch
-    from distributed_processor_amd import _abi, sharding, workloads
+    from distributed_processor_amd import _abi, isa, sharding, workloads
     from distributed_processor_amd.dds import ChannelPlan, SynthesisPipeline
     from distributed_processor_amd.emulator import ProgramSet, alloc_device_outputs
-    ps = ProgramSet(workloads.config4_rb(n_seq=args.dds_seqs, depth=200, n_cores=8))
+    if args.dds_workload == 'rb2q':
+        ps = workloads.config4_rb2q_set(args.dds_seqs, 200, n_cores=8)
+    else:
+        ps = ProgramSet(workloads.config4_rb(n_seq=args.dds_seqs, depth=200, n_cores=8))
     emu.load(ps)
-    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=512, meas_cap=4,
-                           meas_latency=64, seed=0x5EED)
+    ops = ps.words[:, 3] >> 28
+    strobes = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
+                              ps.offsets.astype(np.int64))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=max(512, int(strobes.max()) + 1),
+                           meas_cap=4, meas_latency=64, seed=0x5EED)
     shot0, n = sharding.weak_shard(args.dds_seqs, rank)
     ev = alloc_device_outputs(cfg, n, want=('summary', 'events'))
     emu.run_device(cfg, n, shot0, ev, stream)
@@ -597,7 +605,8 @@ def leg_dds(emu, args, world, rank, stream):
            'step_mode': mode, 'batches_in_flight': args.dds_depth if mode == 'pipelined' else 1,
            'step_roofline_frac': samples * 4 / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
            'serial_ms_per_step': dt_serial / args.steps * 1e3,
-           'config': {'workload': 'config5_dds_rb8', 'sequences_per_gpu': n, 'channels_per_gpu': plan.n_channels,
+           'config': {'workload': 'config5_dds_{}8'.format(args.dds_workload), 'sequences_per_gpu': n,
+                      'channels_per_gpu': plan.n_channels,
                       'samples_per_channel': n_samples, 'rb_depth': 200},
            'roofline': roof}
     if pipe_ms is not None:
@@ -808,10 +817,13 @@ def main():
     ap.add_argument('--shots', type=int, default=10 ** 6, help='config-2 shots per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--dds-seqs', type=int, default=128, help='RB sequences per GPU for the DDS leg (config 5)')
-    ap.add_argument('--dds-depth', type=int, default=2,
+    ap.add_argument('--dds-depth', type=int, default=1,
                     help='DDS batches in flight (> 1: dds.SynthesisPipeline reported, the serial step measured '
-                         'beside it; 1: serial only).  Default 2: the next batch\'s index kernel runs beside this '
-                         'batch\'s tiles (profiles/r05_dds_depth.json: 0.312 vs 0.327 ms)')
+                         'beside it; 1: serial only).  Default 1: on the two-qubit RB timelines two batches in '
+                         'flight measured slower than one context (0.846 vs 0.779 ms kernel, r06)')
+    ap.add_argument('--dds-workload', default='rb2q', choices=('rb2q', 'rb'),
+                    help='config-5 timelines: rb2q = config 4\'s two-qubit Clifford RB on 4 qubit pairs; rb = the '
+                         'RB-shaped 8-core generator of rounds 2-6')
     ap.add_argument('--rb-depth', type=int, default=1,
                     help='config-4 batches in flight (opt-in, > 1: emulator.RunPipeline, reported with the serial '
                          'step measured beside it)')

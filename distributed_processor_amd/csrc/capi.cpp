@@ -1030,12 +1030,23 @@ extern "C" int dpemu_dds(dpemu_ctx *ctx, const dpemu_dds_channels *ch, const uin
     p.env_lds = (env_max + 3) & ~3u;
     p.freq_lds = (freq_max + 3) & ~3u;
     p.tiles = (uint32_t)(((uint64_t)p.n_samples + DDS_TILE - 1) / DDS_TILE);
-    p.stripes = std::max<uint32_t>(1, (p.tiles + DDS_TILES_PER_STRIPE - 1) / DDS_TILES_PER_STRIPE);
-    p.wg_tiles = (p.tiles + p.stripes - 1) / p.stripes;
+    auto stripe_plan = [&](uint32_t per_stripe) {
+        p.stripes = std::max<uint32_t>(1, (p.tiles + per_stripe - 1) / per_stripe);
+        p.wg_tiles = (p.tiles + p.stripes - 1) / p.stripes;
+        return dds_lds_bytes(0, p.wg_tiles, p.env_lds, p.freq_lds);
+    };
     {
-        const uint32_t fixed = dds_lds_bytes(0, p.wg_tiles, p.env_lds, p.freq_lds);
+        const uint32_t fixed = stripe_plan(DDS_TILES_PER_STRIPE);
         const uint32_t fit = fixed < DDS_WG_LDS_BUDGET ? (DDS_WG_LDS_BUDGET - fixed) / 20 & ~7u : 0u;
         p.rec_lds = std::min(p.ev_lds, std::max(fit, DDS_REC_LDS_MIN));
+        if (p.rec_lds < p.ev_lds) {
+            // dense channels: stage every record under the larger budget, with
+            // more tiles per workgroup to spread its larger prologue
+            if (stripe_plan(DDS_TILES_PER_STRIPE_DENSE) + p.ev_lds * 20 <= (uint32_t)DDS_WG_LDS_DENSE)
+                p.rec_lds = p.ev_lds;
+            else
+                stripe_plan(DDS_TILES_PER_STRIPE);
+        }
     }
     const uint64_t need = dds_index_bytes(p.n_channels, p.ev_lds);
     if (need > ctx->dds_index_cap) {         // the event index (grown, never shrunk)

@@ -254,7 +254,9 @@ constexpr uint32_t DDS_MAX_EVENTS = 1024;
 constexpr uint32_t DDS_TILE = 4 * BLOCK;      // samples per tile: 4 per thread, one 16-B store each
 // tiles per stripe workgroup: 8 / 12 / 20 / 24 / 32 measured 0.419 / 0.346 /
 // 0.315 / 0.325 / 0.345 ms against 0.313 for 16 (config 5)
-constexpr uint32_t DDS_TILES_PER_STRIPE = 16;
+#ifndef DDS_TILES_PER_STRIPE
+#define DDS_TILES_PER_STRIPE 16u
+#endif
 constexpr uint32_t DDS_ENV_LDS_MAX = 8192;    // words: tables up to 32 KiB are staged in LDS
 constexpr uint32_t DDS_FREQ_LDS_MAX = 2048;   // words: 64 freq entries as (R, R') pairs
 
@@ -275,6 +277,20 @@ __host__ __device__ inline uint32_t dds_lds_bytes(uint32_t rec_lds, uint32_t til
 // (less 512 B: the compiler's static LDS of the kernel, so 8 fit in 160 KiB)
 constexpr uint32_t DDS_WG_LDS_BUDGET = 20 * 1024 - 512;
 constexpr uint32_t DDS_REC_LDS_MIN = 64;
+// Dense channels (more strobes than the 20-KiB budget holds, e.g. depth-200
+// two-qubit RB drive channels, ~560-720 strobes): every record is staged when
+// the workgroup then stays within this larger budget (fewer workgroups per CU,
+// but no sweep reading records from the global index)
+#ifndef DDS_WG_LDS_DENSE
+#define DDS_WG_LDS_DENSE (32 * 1024 - 512)
+#endif
+// tiles per stripe workgroup under the dense budget (5 workgroups per CU
+// instead of 8): config 5 on the two-qubit RB timelines, 16 / 20 / 22 / 24 /
+// 26 / 28 / 32 tiles: 0.892 / 0.809 / 0.795 / 0.780 / 0.785 / 0.859 / 0.861
+// ms (profiles/r06_dds_dense_ab.json); the sparse case keeps 16
+#ifndef DDS_TILES_PER_STRIPE_DENSE
+#define DDS_TILES_PER_STRIPE_DENSE 24u
+#endif
 
 // LDS words of an interp-1 envelope of n words staged as swizzled (E, E')
 // pairs (dds.hip env_pair): whole groups of 8 16-B chunks

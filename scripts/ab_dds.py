@@ -23,6 +23,8 @@ def main():
     ap.add_argument('--reps', type=int, default=4)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--align', type=int, default=4, help='round n_samples up to a multiple of this')
+    ap.add_argument('--workload', default='rb2q', choices=('rb2q', 'rb'),
+                    help='timelines: config 4\'s two-qubit RB on 4 pairs, or the RB-shaped 8-core generator')
     a = ap.parse_args()
     import torch
     from distributed_processor_amd import _abi, workloads
@@ -30,9 +32,14 @@ def main():
     from distributed_processor_amd.emulator import Emulator, ProgramSet, alloc_device_outputs
     libs = [os.path.abspath(x) for x in a.libs.split(',')]
     emus = [Emulator(0, lib_path=l) for l in libs]
-    ps = ProgramSet(workloads.config4_rb(n_seq=a.seqs, depth=200, n_cores=8))
-    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=512, meas_cap=4,
-                           meas_latency=64, seed=0x5EED)
+    if a.workload == 'rb2q':
+        ps = workloads.config4_rb2q_set(a.seqs, 200, n_cores=8)
+    else:
+        ps = ProgramSet(workloads.config4_rb(n_seq=a.seqs, depth=200, n_cores=8))
+    ops = ps.words[:, 3] >> 28
+    strobes = np.add.reduceat(((ops == 0x9) | (ops == 0xB)).astype(np.int64), ps.offsets.astype(np.int64))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=max(512, int(strobes.max()) + 1),
+                           meas_cap=4, meas_latency=64, seed=0x5EED)
     emus[0].load(ps)
     ev = alloc_device_outputs(cfg, a.seqs, want=('summary', 'events'))
     emus[0].run_device(cfg, a.seqs, 0, ev)
@@ -84,7 +91,7 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         fills.append(t0.elapsed_time(t1) / a.steps)
-    print(json.dumps({'same_iq': same, 'GB': gb, 'n_samples': n_samples, 'fill_ms': float(np.median(fills)),
+    print(json.dumps({'workload': a.workload, 'same_iq': same, 'GB': gb, 'n_samples': n_samples, 'fill_ms': float(np.median(fills)),
                       'kernel_ms': {os.path.basename(l): float(np.median(k)) for l, k in zip(libs, kern)},
                       'kernel_min_ms': {os.path.basename(l): float(np.min(k)) for l, k in zip(libs, kern)},
                       'step_ms': {os.path.basename(l): float(np.median(k)) for l, k in zip(libs, step)}}))

@@ -306,6 +306,32 @@ def test_global_record_fallback(emu):
     assert (ref != 0).sum() > 10000
 
 
+@pytest.mark.parametrize('cap', [600, 720, 1024])
+def test_dense_channels_staged(emu, cap):
+    """event caps past what the 20-KiB workgroup budget holds (the two-qubit
+    RB drive channels: 560-720 strobes): with a small envelope every record
+    is staged under the dense budget with 24 tiles per stripe, up to the
+    largest cap (DDS_MAX_EVENTS); against oracle_dds.  (A budget the records
+    exceed even then: test_global_record_fallback.)"""
+    import torch
+    rng = np.random.default_rng(cap)
+    n_lanes, n_cycles = 6, 40000
+    env_tab = pack_iq16(np.exp(1j * rng.uniform(0, 2 * np.pi, 64)) * rng.uniform(0, 1, 64))
+    freq_tab = np.concatenate([DDSElementConfig(samples_per_clk=16).get_freq_buffer([f])
+                               for f in (91.7e6, -13.1e6, 250e6)])
+    summary, ev = synthetic_timelines(rng, n_lanes, cap, n_cycles, 64, 3)
+    desc = np.array([(L, e, 16, 1 + 3 * (e & 1), 0, 64, 0, len(freq_tab)) for L in range(n_lanes) for e in range(4)],
+                    np.uint32)
+    n_samples = 16 * n_cycles + 4 * 7
+    ref = oracle.dds(desc, summary, ev, env_tab, freq_tab, n_samples, cap)
+    dev = {'summary': torch.from_numpy(summary.view(np.int32)).cuda(),
+           'events': torch.from_numpy(ev.view(np.int32)).cuda()}
+    iq = emu.synthesize(plan_from(desc, env_tab, freq_tab, n_lanes, cap), dev, n_samples)
+    torch.cuda.synchronize()
+    check_equal(host(iq), ref, 'dense channels cap {}'.format(cap))
+    assert (ref != 0).sum() > 100000
+
+
 def test_dense_tile_raw_event_lookup(emu):
     """a 32-KiB envelope leaves the multi-pass kernel room for only
     DDS_REC_MIN (64) records of each kind; lanes with 150 strobes and 120

@@ -103,14 +103,22 @@ def test_config3_shard_bit_exact(emu, rank, shape):
     assert abs(flip.mean() - 0.5) < 0.01
 
 
-def config5_timelines(emu):
+def config5_timelines(emu, workload='rb2q'):
     """the bench's config-5 inputs: 128 8-core RB timelines (depth 200) on the
-    device, the 2048-channel plan and the sample count"""
+    device -- two-qubit Clifford RB on four qubit pairs (the bench default,
+    ~560-720 drive strobes per lane: the dense-channel LDS plan) or the
+    RB-shaped generator (the 20-KiB plan) -- the 2048-channel plan and the
+    sample count"""
     import torch
     n_seq = 128
-    ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
-    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=512, meas_cap=4,
-                           meas_latency=64, seed=0x5EED)
+    if workload == 'rb2q':
+        ps = workloads.config4_rb2q_set(n_seq, 200, n_cores=8)
+    else:
+        ps = ProgramSet(workloads.config4_rb(n_seq=n_seq, depth=200, n_cores=8))
+    ops = ps.words[:, 3] >> 28
+    strobes = np.add.reduceat(((ops == 0x9) | (ops == 0xB)).astype(np.int64), ps.offsets.astype(np.int64))
+    cfg = _abi.make_config(8, n_groups=ps.n_groups, max_cycles=1 << 20, event_cap=max(512, int(strobes.max()) + 1),
+                           meas_cap=4, meas_latency=64, seed=0x5EED)
     emu.load(ps)
     ev = alloc_device_outputs(cfg, n_seq, want=('summary', 'events'))
     ev['events'].zero_()
@@ -124,9 +132,10 @@ def config5_timelines(emu):
     return cfg, ev, plan, n_samples
 
 
-def test_config5_full_launch_all_channels(emu):
+@pytest.mark.parametrize('workload', ['rb2q', 'rb'])
+def test_config5_full_launch_all_channels(emu, workload):
     import torch
-    cfg, ev, plan, n_samples = config5_timelines(emu)
+    cfg, ev, plan, n_samples = config5_timelines(emu, workload)
     iq = emu.synthesize(plan, ev, n_samples)
     torch.cuda.synchronize()
     summ, events = ev['summary'].cpu().numpy(), ev['events'].cpu().numpy()
