@@ -64,7 +64,7 @@ def test_recovery_closes_sequences():
     assert len(np.unique(el[:, :, :-1])) > 1500
 
 
-@pytest.mark.parametrize('n_cores,depth,chunk', [(2, 12, 4), (4, 7, 3)])
+@pytest.mark.parametrize('n_cores,depth,chunk', [(2, 12, 4), (4, 7, 3), (8, 5, 3)])
 def test_rb2q_vectorised_matches_builder(n_cores, depth, chunk):
     n_seq = 7
     ref = ProgramSet(workloads.config4_rb2q(n_seq=n_seq, depth=depth, n_cores=n_cores))
