@@ -704,21 +704,24 @@ def leg_active_reset(emu, args, world, rank, stream, lut=False, demod=False):
     return res
 
 
-def leg_rb(emu, args, world, rank, stream):
+def leg_rb(emu, args, world, rank, stream, shaped=False):
     """config 4 at its stated size: 10^5 distinct two-qubit Clifford RB
     sequences of depth 200 plus their recovery Cliffords (workloads.config4_rb2q:
     X90 / Y90 / X-90 / Y-90, virtual Z, CNOT by cross resonance; ~1,300
     commands per core, 2.6*10^8 commands, a 4.2 GB program image), 10 shots
     each = 10^6 shots = 2*10^6 lanes per GPU.  Branch-free programs with
     register commands: macro_staged_kernel.  Divergent: a wave's lanes run ~7
-    different programs.  VALU-bound: the roofline is VALU issue against
+    different programs.  shaped: the RB-SHAPED programs of rounds 2-6
+    (workloads.config4_rb_set: single-qubit Cliffords + random CR pulses, no
+    recovery; ~740 commands per core), kept on the line as the round-over-round
+    comparison for the same kernel (no CPU baseline, no PMC pass).  VALU-bound: the roofline is VALU issue against
     the measured peak, with the VALU ops per emulated instruction and the
     active lanes per VALU instruction (divergence) from the PMC pass."""
     import torch
     from distributed_processor_amd import _abi, isa, sharding, workloads
     from distributed_processor_amd.emulator import RunPipeline, alloc_device_outputs
     t0 = time.perf_counter()
-    ps = workloads.config4_rb2q_set(args.rb_seqs, 200)
+    ps = (workloads.config4_rb_set if shaped else workloads.config4_rb2q_set)(args.rb_seqs, 200)
     gen_s = time.perf_counter() - t0
     emu.load(ps)
     torch.cuda.synchronize()
@@ -776,7 +779,7 @@ def leg_rb(emu, args, world, rank, stream):
     ms_step = dt / steps * 1e3
     serial_ms = dt_serial / steps * 1e3
     k_ms = min(kernel_ms, serial_ms)            # (capped at the one-context step: batches in flight overlap)
-    prof = pmc('rb') if (args.rb_seqs, args.rb_spg) == (100000, 10) else None
+    prof = pmc('rb') if (args.rb_seqs, args.rb_spg) == (100000, 10) and not shaped else None
     alg = float(bytes_per_lane(summ, cfg).sum())
     hbm = hbm_roofline(alg, kernel_ms, serial_ms, 'dpemu::' + kernel, prof, kernel.split('<')[0])
     hbm['kernel_ms_block'] = kernel_ms_blk
@@ -787,14 +790,16 @@ def leg_rb(emu, args, world, rank, stream):
                     active_lanes_per_valu_pct=prof.get('valu_lane_util_pct'), traffic=hbm['traffic'], hbm=hbm)
     else:
         roof = hbm
-    res = {'metric': 'emulated core-shots/s (config 4: 2-qubit Clifford RB, 1e5 sequences x depth 200 + recovery, 10 shots each)',
+    res = {'metric': 'emulated core-shots/s (config 4: {}, 1e5 sequences x depth 200, 10 shots each)'.format(
+               'RB-shaped programs of rounds 2-6' if shaped else '2-qubit Clifford RB + recovery'),
            'value': n * 2 * world * steps / dt, 'unit': 'core-shots/s', 'shots_per_s': n * world * steps / dt,
            'ms_per_step': ms_step, 'kernel_ms': kernel_ms, 'steps': steps,
            'serial_ms_per_step': dt_serial / steps * 1e3, 'step_mode': mode,
            'batches_in_flight': depth if mode == 'pipelined' else 1,
            'instructions_per_s': instrs * world * steps / dt,
            'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * steps / dt,
-           'config': {'workload': 'config4_rb2q_2core_1e5seq_depth200', 'sequences': args.rb_seqs,
+           'config': {'workload': 'config4_{}_2core_1e5seq_depth200'.format('rb_shaped' if shaped else 'rb2q'),
+                      'sequences': args.rb_seqs,
                       'lane_order': LANE_ORDER_NAMES[cfg.lane_order],
                       'shots_per_sequence': args.rb_spg, 'shots_per_gpu': n, 'commands': int(ps.words.shape[0]),
                       'program_image_bytes': int(ps.words.nbytes), 'event_cap': cfg.event_cap,
@@ -802,7 +807,7 @@ def leg_rb(emu, args, world, rank, stream):
            'roofline': roof}
     if pipe_ms is not None:
         res['pipelined_ms_per_step'] = pipe_ms
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not shaped:
         res['cpu_baseline'] = cpu_baselines(ps, cfg, 1 << 20, 'config 4 RB', all_cores=True)
     del out
     torch.cuda.empty_cache()
@@ -831,7 +836,7 @@ def main():
     ap.add_argument('--rb-seqs', type=int, default=100000, help='config-4 RB sequences')
     ap.add_argument('--rb-spg', type=int, default=10, help='config-4 shots per sequence')
     ap.add_argument('--c1-shots', type=int, default=10 ** 6, help='config-1 shots per GPU per step')
-    ap.add_argument('--legs', default='config1,dds,active_reset,demod,lut,rb',
+    ap.add_argument('--legs', default='config1,dds,active_reset,demod,lut,rb,rb_shaped',
                     help='sub-legs to run (comma list; "" for none)')
     args = ap.parse_args()
 
@@ -877,6 +882,7 @@ def main():
         if k in main_leg:
             result[k] = main_leg[k]
     fns = {'config1': leg_config1, 'dds': leg_dds, 'active_reset': leg_active_reset, 'rb': leg_rb,
+           'rb_shaped': lambda *a: leg_rb(*a, shaped=True),
            'lut': lambda *a: leg_active_reset(*a, lut=True), 'demod': lambda *a: leg_active_reset(*a, demod=True)}
     for name in [x for x in args.legs.split(',') if x]:
         result[name] = fns[name](emu, args, world, rank, stream)

@@ -7,7 +7,8 @@ out=$1
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 tag=${2:-$(python -c "import re; print(re.search(r\"PROFILE_TAG = '(\\w+)'\", open('bench.py').read()).group(1))")}
 mkdir -p $out/profiles
-bash scripts/prof_cmd.sh $out/prof bench.py --steps 8 --warmup 2 --no-cpu-baseline > $out/prof.log 2>&1 || { echo "prof failed"; exit 1; }
+# (rb_shaped left out: it shares the rb leg's kernel and grid, which key the PMC summary)
+bash scripts/prof_cmd.sh $out/prof bench.py --steps 8 --warmup 2 --no-cpu-baseline --legs config1,dds,active_reset,demod,lut,rb > $out/prof.log 2>&1 || { echo "prof failed"; exit 1; }
 python scripts/pmc_summary.py $out/prof $tag $out/profiles > $out/pmc_summary.log 2>&1 || { echo "pmc_summary failed"; exit 1; }
 cp $(find $out/prof/trace -name "*kernel_stats.csv") $out/profiles/${tag}_kernel_stats.csv
 # the raw per-dispatch CSVs are summarised now: drop them (gpurun merges back <= 64 MiB)
