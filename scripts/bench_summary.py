@@ -3,7 +3,7 @@ import json
 import sys
 
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-legs = [('ramsey', d)] + [(k, d[k]) for k in ('config1', 'dds', 'active_reset', 'demod', 'lut', 'rb') if k in d]
+legs = [('ramsey', d)] + [(k, d[k]) for k in ('config1', 'dds', 'active_reset', 'demod', 'lut', 'rb', 'rb_shaped') if k in d]
 for name, a in legs:
     r = a['roofline']
     h = r.get('hbm', r)
