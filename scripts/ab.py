@@ -19,9 +19,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def workload(name):
     from distributed_processor_amd import _abi, isa, workloads
     from distributed_processor_amd.emulator import ProgramSet
-    if name in ('rb', 'rb_sm', 'rb8'):   # rb_sm: 10^4 shots (a quick check of a new build); rb8: 8 shots per sequence
+    if name in ('rb', 'rb_sm', 'rb8', 'rb2q'):
+        # rb: the RB-shaped programs of rounds 2-6; rb2q: config 4's two-qubit
+        # Clifford RB; rb_sm: 10^4 shots (a quick check of a new build); rb8: 8 shots per sequence
         spg = 8 if name == 'rb8' else 10
-        ps = workloads.config4_rb_set(100000 if name != 'rb_sm' else 1000, 200)
+        gen = workloads.config4_rb2q_set if name == 'rb2q' else workloads.config4_rb_set
+        ps = gen(100000 if name != 'rb_sm' else 1000, 200)
         ops = ps.words[:, 3] >> 28
         ev = np.add.reduceat(((ops == isa.OP_PULSE_TRIG) | (ops == isa.OP_PULSE_RESET)).astype(np.int64),
                              ps.offsets.astype(np.int64))
