@@ -48,6 +48,13 @@
 
 namespace dpemu {
 
+// cache policy of the event / measurement rows (A/B builds: bit 1 events,
+// bit 2 measurements nontemporal)
+#ifndef DPEMU_BRANCH_NT
+#define DPEMU_BRANCH_NT 0
+#endif
+constexpr bool BR_NT_EV = (DPEMU_BRANCH_NT & 1) != 0, BR_NT_MEAS = (DPEMU_BRANCH_NT & 2) != 0;
+
 namespace {
 
 enum : uint32_t { B_RUN = 0, B_SYNC = 1, B_LUT = 2, B_FIN = 3 };
@@ -228,11 +235,11 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     auto emit = [&](bool ok, uint32_t te, uint32_t kind) __attribute__((always_inline)) {
         if (ok) {
             if (DIRECT && n_ev < p.event_cap && p.events)
-                ev_lane[(uint64_t)n_ev * n_lanes] = event_record(te, pe, pp, pa, kind);
+                st_out(&ev_lane[(uint64_t)n_ev * n_lanes], event_record(te, pe, pp, pa, kind), BR_NT_EV);
             if (!DIRECT && n_ev < p.event_cap && p.events) {
                 const uint4 rec = event_record(te, pe, pp, pa, kind);
                 const bool full = n_ev - n_st == 2u;    // the oldest goes out now
-                if (full) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
+                if (full) st_out(&ev_lane[(uint64_t)n_st * n_lanes], pend0, BR_NT_EV);
                 pend0 = sel4(full, pend1, pend0);
                 n_st += full ? 1u : 0u;
                 const bool first = n_ev == n_st;
@@ -263,7 +270,7 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
                 if constexpr (XMEAS) {
                     if (n_meas < (uint32_t)MT) s_mt[n_meas < (uint32_t)MT ? n_meas : 0u][tid] = (tv << 1) | bit;
                 }
-                if (p.meas && n_meas < p.meas_cap) p.meas[(uint64_t)n_meas * n_lanes + lane] = make_uint2(tv, bit);
+                if (p.meas && n_meas < p.meas_cap) st_out(&p.meas[(uint64_t)n_meas * n_lanes + lane], make_uint2(tv, bit), BR_NT_MEAS);
                 meas_bits |= (n_meas < 32u ? bit : 0u) << (n_meas & 31u);
                 last_bit = bit;
                 n_meas++;
@@ -331,9 +338,9 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         const bool f1 = n_st < ne && n_st < done;
         if (!__any(f1)) return;                      // most iterations complete no row
         const bool f2 = f1 && n_st + 1u < ne && n_st + 1u < done;
-        if (f1) ev_lane[(uint64_t)n_st * n_lanes] = pend0;
+        if (f1) st_out(&ev_lane[(uint64_t)n_st * n_lanes], pend0, BR_NT_EV);
         if (__any(f2)) {
-            if (f2) ev_lane[(uint64_t)(n_st + 1u) * n_lanes] = pend1;
+            if (f2) st_out(&ev_lane[(uint64_t)(n_st + 1u) * n_lanes], pend1, BR_NT_EV);
         }
         pend0 = sel4(f1 && !f2, pend1, pend0);
         n_st += (f1 ? 1u : 0u) + (f2 ? 1u : 0u);

@@ -247,6 +247,21 @@ __device__ __forceinline__ uint32_t out_lane(const KParams &p, uint32_t sl, uint
     return p.shot_major ? (sl << p.log2C) + core : core * p.n_shots + sl;
 }
 
+// an output store, nontemporal (streaming: written whole, never read back
+// by the kernel) when nt
+typedef uint32_t st_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t st_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_out(uint4 *dst, const uint4 v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(st_u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<st_u32x4 *>(dst));
+    else *dst = v;
+}
+__device__ __forceinline__ void st_out(uint2 *dst, const uint2 v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(st_u32x2{v.x, v.y}, reinterpret_cast<st_u32x2 *>(dst));
+    else *dst = v;
+}
+
 // the 16-B event record (include/dpemu.h): pulse_iface snapshot at cycle te
 __device__ __forceinline__ uint4 event_record(uint32_t te, uint32_t pe, uint32_t pp, uint32_t pa, uint32_t kind)
 {
@@ -370,8 +385,15 @@ __device__ __forceinline__ void write_summary(const KParams &p, uint32_t lane, u
                                               uint32_t qclk_end, uint32_t n_meas, uint32_t meas_bits, uint32_t n_tr)
 {
     uint4 *s = reinterpret_cast<uint4 *>(p.summary + 8ull * lane);
-    s[0] = make_uint4(t_end, (ip & 0xFFFFu) | ((status & 0xFFu) << 16) | ((flags & 0xFFu) << 24), n_ev, n_exec);
-    s[1] = make_uint4(qclk_end, n_meas, meas_bits, n_tr);
+    const uint4 s0 = make_uint4(t_end, (ip & 0xFFFFu) | ((status & 0xFFu) << 16) | ((flags & 0xFFu) << 24), n_ev, n_exec);
+    const uint4 s1 = make_uint4(qclk_end, n_meas, meas_bits, n_tr);
+#if defined(DPEMU_ST_POLICY) && (DPEMU_ST_POLICY & 4)
+    st_out(s, s0, true);
+    st_out(s + 1, s1, true);
+#else
+    s[0] = s0;
+    s[1] = s1;
+#endif
 }
 
 // outcome histogram: bit c of the key = last measurement of core c; one count per

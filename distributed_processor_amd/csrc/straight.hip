@@ -37,6 +37,16 @@
 
 namespace dpemu {
 
+// Cache policy of the output rows (DPEMU_ST_POLICY bits, A/B builds: 1 events,
+// 2 measurements, 4 summaries nontemporal).  Events + measurements
+// nontemporal is the product setting: config 2 (shot-major lanes) 0.1618 ->
+// 0.1462 ms, core-major 0.1713 -> 0.1614, config 1 unchanged; either one
+// alone measured neutral, and nontemporal summaries (two 16-B halves of a
+// 32-B record, written by separate instructions) 0.20 ms
+// (profiles/r06_straight_nt_ab.json)
+#ifndef DPEMU_ST_POLICY
+#define DPEMU_ST_POLICY 3
+#endif
 
 template <int SRC, int FB>
 __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
@@ -86,14 +96,14 @@ __global__ void __launch_bounds__(BLOCK) straight_kernel(const KParams p)
     // final counts (a record is dropped iff its count exceeds the cap)
     auto emit = [&](bool ok, uint32_t te, uint32_t kind) {
         if (ok && n_ev < p.event_cap && p.events)
-            p.events[(uint64_t)n_ev * n_lanes + lane] = event_record(te, pe, pp, pa, kind);
+            st_out(&p.events[(uint64_t)n_ev * n_lanes + lane], event_record(te, pe, pp, pa, kind), (DPEMU_ST_POLICY & 1) != 0);
         n_ev += ok ? 1u : 0u;
         const bool is_meas = ok && kind == 0u && ((pe >> 24) & 3u) == p.meas_elem;   // meas_elem 0xFF: none
         uint32_t bit = 0;
         if (is_meas) {
             bit = meas_bit(p, shot, core, n_meas, thr, pa, pe);
             if (p.meas && n_meas < p.meas_cap)
-                p.meas[(uint64_t)n_meas * n_lanes + lane] = make_uint2(te + p.meas_latency, bit);
+                st_out(&p.meas[(uint64_t)n_meas * n_lanes + lane], make_uint2(te + p.meas_latency, bit), (DPEMU_ST_POLICY & 2) != 0);
         }
         meas_bits |= (n_meas < 32u ? bit : 0u) << (n_meas & 31u);
         last_bit = is_meas ? bit : last_bit;

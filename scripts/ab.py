@@ -31,6 +31,10 @@ def workload(name):
         cfg = _abi.make_config(2, n_groups=ps.n_groups, shots_per_group=spg, max_cycles=1 << 20,
                                event_cap=int(ev.max()) + 1, meas_cap=2, seed=0x5EED)
         return ps, cfg, 10 ** 4 if name == 'rb_sm' else spg * 10 ** 5
+    if name == 'config1':   # the reference's golden single-core program, 10^6 shots
+        ps = ProgramSet(workloads.config1_linear())
+        cfg = _abi.make_config(1, max_cycles=10000, event_cap=8, meas_cap=4, seed=0x5EED)
+        return ps, cfg, 10 ** 6
     if name == 'ramsey':
         ps = ProgramSet(workloads.config2_ramsey(n_cores=8, n_points=100))
         cfg = _abi.make_config(8, n_groups=100, max_cycles=1 << 20, event_cap=8, meas_cap=2, seed=0x5EED)
