@@ -127,12 +127,20 @@ __device__ __forceinline__ int last_le(const uint32_t *t, int n, uint32_t x)
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// I/Q stores nontemporal (A/B builds only)
+#ifndef DPEMU_DDS_NT
+#define DPEMU_DDS_NT 0
+#endif
 
 __device__ __forceinline__ void store4(uint32_t *out, uint32_t j0, uint32_t c_end, const uint32_t v[4])
 {
     if (j0 + 3 < c_end) {
         const u32x4 w = {v[0], v[1], v[2], v[3]};
+#if DPEMU_DDS_NT
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(out + j0));
+#else
         *reinterpret_cast<u32x4 *>(out + j0) = w;
+#endif
     } else {
         for (int s = 0; s < 4 && j0 + s < c_end; s++) out[j0 + s] = v[s];
     }
