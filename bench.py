@@ -731,7 +731,11 @@ def leg_rb(emu, args, world, rank, stream, shaped=False):
                               ps.offsets.astype(np.int64))
     cfg = _abi.make_config(2, n_groups=ps.n_groups, shots_per_group=args.rb_spg, max_cycles=1 << 20,
                            event_cap=int(strobes.max()) + 1, trace_cap=0, meas_cap=2, meas_latency=64,
-                           seed=0x5EED, p1=0.5)
+                           seed=0x5EED, p1=0.5,
+                           # the caller's cache hint: event rows nontemporal on the two-qubit RB
+                           # programs (-6 to -9 % same-process); it costs the RB-shaped ones +10-13 %
+                           # (profiles/r06_stpol_ab.json), which run without it
+                           exec_flags=0 if shaped else _abi.X_STREAM_EVENTS)
     shot0, n = sharding.weak_shard(args.rb_seqs * args.rb_spg, rank)
     want = ('summary', 'events', 'meas', 'hist')
     steps = max(1, args.steps)
@@ -800,7 +804,7 @@ def leg_rb(emu, args, world, rank, stream, shaped=False):
            'qclk_cycles_per_s': float(s['t_end'].astype(np.float64).sum()) * world * steps / dt,
            'config': {'workload': 'config4_{}_2core_1e5seq_depth200'.format('rb_shaped' if shaped else 'rb2q'),
                       'sequences': args.rb_seqs,
-                      'lane_order': LANE_ORDER_NAMES[cfg.lane_order],
+                      'lane_order': LANE_ORDER_NAMES[cfg.lane_order], 'exec_flags': hex(cfg.exec_flags),
                       'shots_per_sequence': args.rb_spg, 'shots_per_gpu': n, 'commands': int(ps.words.shape[0]),
                       'program_image_bytes': int(ps.words.nbytes), 'event_cap': cfg.event_cap,
                       'generate_s': gen_s, 'load_s': load_s},

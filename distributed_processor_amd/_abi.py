@@ -24,6 +24,7 @@ X_HIST_REPL = 0x8
 X_PROG_MAJOR = 0x10
 X_GENERAL = 0x20
 X_MACRO_DIRECT = 0x40
+X_STREAM_EVENTS = 0x80
 
 STATUS_NAMES = {0: 'running', ST_DONE: 'done', ST_MAX_CYCLES: 'max_cycles',
                 ST_HUNG_OPCODE: 'hung_opcode', ST_DEADLOCK: 'deadlock'}

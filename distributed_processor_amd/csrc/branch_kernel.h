@@ -48,12 +48,13 @@
 
 namespace dpemu {
 
-// cache policy of the event / measurement rows (A/B builds: bit 1 events,
-// bit 2 measurements nontemporal)
+// cache policy of the event / measurement rows (A/B builds: bits 0-1 the
+// events' StPolicy (lane.h), bit 2 measurements nontemporal)
 #ifndef DPEMU_BRANCH_NT
 #define DPEMU_BRANCH_NT 0
 #endif
-constexpr bool BR_NT_EV = (DPEMU_BRANCH_NT & 1) != 0, BR_NT_MEAS = (DPEMU_BRANCH_NT & 2) != 0;
+constexpr StPolicy BR_EV_POLICY = (StPolicy)(DPEMU_BRANCH_NT & 3);
+constexpr bool BR_NT_MEAS = (DPEMU_BRANCH_NT & 4) != 0;
 
 namespace {
 
@@ -235,11 +236,11 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
     auto emit = [&](bool ok, uint32_t te, uint32_t kind) __attribute__((always_inline)) {
         if (ok) {
             if (DIRECT && n_ev < p.event_cap && p.events)
-                st_out(&ev_lane[(uint64_t)n_ev * n_lanes], event_record(te, pe, pp, pa, kind), BR_NT_EV);
+                st_rec<BR_EV_POLICY>(&ev_lane[(uint64_t)n_ev * n_lanes], event_record(te, pe, pp, pa, kind));
             if (!DIRECT && n_ev < p.event_cap && p.events) {
                 const uint4 rec = event_record(te, pe, pp, pa, kind);
                 const bool full = n_ev - n_st == 2u;    // the oldest goes out now
-                if (full) st_out(&ev_lane[(uint64_t)n_st * n_lanes], pend0, BR_NT_EV);
+                if (full) st_rec<BR_EV_POLICY>(&ev_lane[(uint64_t)n_st * n_lanes], pend0);
                 pend0 = sel4(full, pend1, pend0);
                 n_st += full ? 1u : 0u;
                 const bool first = n_ev == n_st;
@@ -338,9 +339,9 @@ __global__ void __launch_bounds__(BLOCK) branch_kernel(const KParams p)
         const bool f1 = n_st < ne && n_st < done;
         if (!__any(f1)) return;                      // most iterations complete no row
         const bool f2 = f1 && n_st + 1u < ne && n_st + 1u < done;
-        if (f1) st_out(&ev_lane[(uint64_t)n_st * n_lanes], pend0, BR_NT_EV);
+        if (f1) st_rec<BR_EV_POLICY>(&ev_lane[(uint64_t)n_st * n_lanes], pend0);
         if (__any(f2)) {
-            if (f2) st_out(&ev_lane[(uint64_t)(n_st + 1u) * n_lanes], pend1, BR_NT_EV);
+            if (f2) st_rec<BR_EV_POLICY>(&ev_lane[(uint64_t)(n_st + 1u) * n_lanes], pend1);
         }
         pend0 = sel4(f1 && !f2, pend1, pend0);
         n_st += (f1 ? 1u : 0u) + (f2 ? 1u : 0u);

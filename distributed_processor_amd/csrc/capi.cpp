@@ -704,6 +704,7 @@ static int run_impl(dpemu_ctx *ctx, const dpemu_config *cfg, uint64_t shot_begin
     p.lut_mask = cfg->lut_mask;
     const uint64_t guard = (uint64_t)C * (cfg->max_cycles / 3u + 4u) + 1024u;
     p.iter_guard = guard > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)guard;
+    p.ev_stream = (cfg->exec_flags & DPEMU_X_STREAM_EVENTS) ? 1u : 0u;
     // LDS program staging: a workgroup of S = BLOCK / C shots spans at most w
     // consecutive program groups; stage their programs if they fit
     const uint32_t S = BLOCK / C, ng = cfg->n_groups;

@@ -162,6 +162,7 @@ struct KParams {
     const uint4 *ro_hdr;          // [n_programs] {drv_off, drv_len, lo_off, lo_len}
     int2 *acc;                    // dpemu_outputs.acc (nullable)
     uint32_t iter_guard;
+    uint32_t ev_stream;           // DPEMU_X_STREAM_EVENTS: macro_staged_kernel's event rows nontemporal
     uint32_t prog_lds_words;      // dynamic LDS commands (FEAT_PROG_LDS)
     uint32_t *hist_rep;           // [hist_reps][hist_stride] u32 replicas (128-B aligned rows)
     uint32_t hist_reps, hist_lds; // hist_lds: n_groups << C <= HIST_LDS_MAX, aggregate in LDS

@@ -262,6 +262,25 @@ __device__ __forceinline__ void st_out(uint2 *dst, const uint2 v, bool nt)
     else *dst = v;
 }
 
+// cache policy of a 16-B record store from a possibly partial wave: ST_WB
+// write-back (L2 merges partial lines of later stores), ST_NT nontemporal,
+// ST_NT_LINE nontemporal for the lanes whose 8-lane group -- one 128-B line
+// of consecutive lanes -- all store (the rest write-back), ST_NT_WAVE
+// nontemporal when the whole wave stores
+enum StPolicy { ST_WB = 0, ST_NT = 1, ST_NT_LINE = 2, ST_NT_WAVE = 3 };
+template <StPolicy P>
+__device__ __forceinline__ void st_rec(uint4 *dst, const uint4 v)
+{
+    if constexpr (P == ST_WB || P == ST_NT) {
+        st_out(dst, v, P == ST_NT);
+    } else {
+        const uint64_t m = __builtin_amdgcn_read_exec();
+        const bool full = P == ST_NT_WAVE ? m == ~0ull : ((m >> (__lane_id() & 56u)) & 0xFFull) == 0xFFull;
+        if (full) st_out(dst, v, true);
+        else *dst = v;
+    }
+}
+
 // the 16-B event record (include/dpemu.h): pulse_iface snapshot at cycle te
 __device__ __forceinline__ uint4 event_record(uint32_t te, uint32_t pe, uint32_t pp, uint32_t pa, uint32_t kind)
 {

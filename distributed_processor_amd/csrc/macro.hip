@@ -37,8 +37,16 @@
 #ifndef DPEMU_MACRO_DMA_AUX
 #define DPEMU_MACRO_DMA_AUX 0
 #endif
+// cache policy of macro_staged_kernel's event / measurement rows (A/B
+// builds: bits 0-1 the events' StPolicy (lane.h), bit 2 measurements
+// nontemporal)
+#ifndef DPEMU_MACRO_NT
+#define DPEMU_MACRO_NT 0
+#endif
 
 namespace dpemu {
+
+constexpr StPolicy MACRO_EV_POLICY = (StPolicy)(DPEMU_MACRO_NT & 3);
 
 // alu.v:20-50; le = sub[31] ^ overflow == signed a < b
 __device__ __forceinline__ uint32_t alu_macro(uint32_t op, uint32_t a, uint32_t b)
@@ -411,7 +419,11 @@ struct MacroLane {
     {
         if (ok) {
             if (n_ev < p.event_cap && ev_on)
-                *evp = event_record(te, pe, pp, pa, kind);
+            {
+                const uint4 rec = event_record(te, pe, pp, pa, kind);
+                if (p.ev_stream) st_rec<ST_NT_WAVE>(evp, rec);   // DPEMU_X_STREAM_EVENTS (uniform)
+                else st_rec<MACRO_EV_POLICY>(evp, rec);
+            }
 #ifdef DPEMU_PROBE_WAVEBLOCK
             evp += 64u;
 #else
@@ -421,7 +433,8 @@ struct MacroLane {
             if (kind == 0u && ((pe >> 24) & 3u) == p.meas_elem) {        // meas_elem 0xFF: none
                 const uint32_t bit = meas_bit(p, p.shot_begin + sl, core, n_meas, p.p1_thr[core], pa, pe);
                 if (p.meas && n_meas < p.meas_cap)
-                    p.meas[(uint64_t)n_meas * p.n_lanes + lane] = make_uint2(te + p.meas_latency, bit);
+                    st_out(&p.meas[(uint64_t)n_meas * p.n_lanes + lane], make_uint2(te + p.meas_latency, bit),
+                           (DPEMU_MACRO_NT & 4) != 0);
                 meas_bits |= (n_meas < 32u ? bit : 0u) << (n_meas & 31u);
                 last_bit = bit;
                 n_meas++;

@@ -85,6 +85,10 @@ extern "C" {
 #define DPEMU_X_GENERAL     0x20  /* run every program on the general interpreter (interp_kernel) */
 #define DPEMU_X_MACRO_DIRECT 0x40 /* branch-free register programs: per-lane macro fetch (macro_kernel),
                                      not the LDS-staged program chunks (macro_staged_kernel) */
+#define DPEMU_X_STREAM_EVENTS 0x80 /* cache hint: branch-free register programs store their event rows
+                                     nontemporal (whole-wave stores; others write-back).  Workload-
+                                     dependent: config 4 two-qubit RB -9 %, RB-shaped programs +10 %
+                                     (profiles/r06_stpol_ab.json) */
 
 #define DPEMU_MAX_CORES 64
 #define DPEMU_MEAS_LOOKUP 16      /* a core's first 16 measurements are visible to fproc;

@@ -10,5 +10,5 @@ git -C "$repo" archive "$rev" distributed_processor_amd/csrc include | tar -x -C
 mkdir -p "$repo/ab_build"
 cd "$tmp/distributed_processor_amd/csrc"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -shared \
-    -o "$repo/ab_build/libdpemu_$name.so" interp.hip branch.hip straight.hip macro.hip dds.hip capi.cpp
+    -o "$repo/ab_build/libdpemu_$name.so" *.hip capi.cpp
 rm -rf "$tmp"

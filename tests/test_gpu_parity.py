@@ -44,13 +44,13 @@ def run_pair(emu, ps, cfg, n_shots, shot0=0):
     """GPU run and oracle; the execution variants (LDS-staged programs,
     histogram strategy, program-major fetch, the general interpreter for
     branch-free programs, the per-lane macro fetch instead of the staged
-    macro chunks) must produce the same bytes"""
+    macro chunks, nontemporal event rows) must produce the same bytes"""
     emu.load(ps)
     g = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
     f = oracle.fast_run(cfg, ps.words, ps.offsets, ps.n_instr, ps.table, shot0, n_shots, want=ALL_OUT)
     base = cfg.exec_flags
     for flags in (_abi.X_PROG_LDS | _abi.X_HIST_REPL, _abi.X_HIST_DIRECT | _abi.X_PROG_MAJOR,
-                  _abi.X_GENERAL | _abi.X_PROG_LDS, _abi.X_MACRO_DIRECT):
+                  _abi.X_GENERAL | _abi.X_PROG_LDS, _abi.X_MACRO_DIRECT, _abi.X_STREAM_EVENTS):
         cfg.exec_flags = flags
         g2 = emu.run(n_shots, shot0, cfg=cfg, outputs=ALL_OUT)
         compare_all(g2.arrays, g.arrays, 'execution variant {:#x}'.format(flags))
