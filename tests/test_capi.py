@@ -111,3 +111,13 @@ def test_struct_layout_mismatch_refused(tmp_path, monkeypatch):
     monkeypatch.setattr(_abi, 'Config', Shorter)
     with pytest.raises(_native.DpemuError, match='struct layout mismatch'):
         _native.load_library(lib)
+
+
+def test_exec_flags_mirror_header():
+    """every DPEMU_X_* execution knob of include/dpemu.h has the same value in _abi"""
+    with open(os.path.join(REPO, 'include', 'dpemu.h')) as f:
+        txt = f.read()
+    flags = dict(re.findall(r'#define DPEMU_(X_[A-Z_]+)\s+(0x[0-9a-fA-F]+)', txt))
+    assert 'X_STREAM_EVENTS' in flags and len(flags) >= 7
+    for name, val in flags.items():
+        assert getattr(_abi, name) == int(val, 16), name
