@@ -418,8 +418,7 @@ struct MacroLane {
     __device__ __forceinline__ void emit1(bool ok, uint32_t te, uint32_t kind)
     {
         if (ok) {
-            if (n_ev < p.event_cap && ev_on)
-            {
+            if (n_ev < p.event_cap && ev_on) {
                 const uint4 rec = event_record(te, pe, pp, pa, kind);
                 if (p.ev_stream) st_rec<ST_NT_WAVE>(evp, rec);   // DPEMU_X_STREAM_EVENTS (uniform)
                 else st_rec<MACRO_EV_POLICY>(evp, rec);
