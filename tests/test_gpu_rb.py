@@ -97,6 +97,30 @@ def test_full_launch_bit_exact(rb):
     assert np.array_equal(out['hist'].cpu().numpy().view(f['hist'].dtype).reshape(f['hist'].shape), f['hist'])
 
 
+def test_full_launch_stream_hint_same_bytes(rb):
+    """the bench's config-4 launch sets DPEMU_X_STREAM_EVENTS (nontemporal
+    event rows): the whole launch's outputs equal the oracle-checked launch
+    without it"""
+    import torch
+    emu, ps, cfg, out = rb
+    base = cfg.exec_flags
+    cfg.exec_flags = base | _abi.X_STREAM_EVENTS
+    out2 = None
+    try:
+        out2 = alloc_device_outputs(cfg, N_SHOTS, want=('summary', 'events', 'meas', 'regs', 'hist'))
+        for t in out2.values():
+            t.zero_()
+        emu.run_device(cfg, N_SHOTS, 0, out2)
+        torch.cuda.synchronize()
+        assert emu.last_kernel().startswith('macro_staged_kernel'), emu.last_kernel()
+        for k in out2:
+            assert torch.equal(out2[k], out[k]), k
+    finally:
+        cfg.exec_flags = base
+        del out2
+        torch.cuda.empty_cache()
+
+
 def test_full_table_windows_with_traces(rb):
     """the same windows as small launches (the small-grid kernel) with every
     output, register traces included"""
